@@ -1,0 +1,429 @@
+/* ORACLE -- test infrastructure only.
+ *
+ * CPU restatement of the reference's MSM + radix-2 NTT path (Tachyon,
+ * /root/reference, 2025-01-31 snapshot) in plain C.  It is the parity checker
+ * for the HIP product path and the `cpu_baseline` of bench.py; nothing in the
+ * product (tachyon_amd/, include/) links, imports or calls it.
+ *
+ * Pinning: the restatement is checked against (1) golden vectors written by an
+ * independent pure-Python big-int restatement (oracle/pyref.py ->
+ * tests/golden/), (2) the reference's own known-answer tests -- the "Easy" MSM
+ * set sum_{i=1..n} i*G = n(n+1)/2*G (msm/test/variable_base_msm_test_set.h:55-68),
+ * the curve generators of the BUILD files, and the real BN254 G1/G2 points of
+ * vendors/circom/examples/multiplier_3.zkey whose decimal coordinates the
+ * reference's zkey_unittest.cc:71-140 states, and (3) the arkworks-compatible
+ * BN254 Fr two-adic root of unity.  The reference itself
+ * cannot be built here (bazel + absl/glog/gtest + genrule constants).
+ *
+ * Build: `make -C oracle` -> oracle/liboracle.so (gcc -O3 -march=native -fopenmp).
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "oracle_constants.h"
+
+/* ---- fields -------------------------------------------------------------- */
+#define FF bn254_fq
+#define FF_N 4
+#define FF_P BN254_FQ_P
+#define FF_R BN254_FQ_R
+#define FF_R2 BN254_FQ_R2
+#define FF_INV BN254_FQ_INV
+#include "ff_impl.h"
+#undef FF
+#undef FF_N
+#undef FF_P
+#undef FF_R
+#undef FF_R2
+#undef FF_INV
+
+#define FF bn254_fr
+#define FF_N 4
+#define FF_P BN254_FR_P
+#define FF_R BN254_FR_R
+#define FF_R2 BN254_FR_R2
+#define FF_INV BN254_FR_INV
+#include "ff_impl.h"
+#undef FF
+#undef FF_N
+#undef FF_P
+#undef FF_R
+#undef FF_R2
+#undef FF_INV
+
+#define FF bls12_381_fq
+#define FF_N 6
+#define FF_P BLS12_381_FQ_P
+#define FF_R BLS12_381_FQ_R
+#define FF_R2 BLS12_381_FQ_R2
+#define FF_INV BLS12_381_FQ_INV
+#include "ff_impl.h"
+#undef FF
+#undef FF_N
+#undef FF_P
+#undef FF_R
+#undef FF_R2
+#undef FF_INV
+
+#define FF bls12_381_fr
+#define FF_N 4
+#define FF_P BLS12_381_FR_P
+#define FF_R BLS12_381_FR_R
+#define FF_R2 BLS12_381_FR_R2
+#define FF_INV BLS12_381_FR_INV
+#include "ff_impl.h"
+#undef FF
+#undef FF_N
+#undef FF_P
+#undef FF_R
+#undef FF_R2
+#undef FF_INV
+
+#define F2 bn254_fq2
+#define F1 bn254_fq
+#include "fp2_impl.h"
+#undef F2
+#undef F1
+#define F2 bls12_381_fq2
+#define F1 bls12_381_fq
+#include "fp2_impl.h"
+#undef F2
+#undef F1
+
+/* ---- curves -------------------------------------------------------------- */
+#define EC bn254_g1
+#define EF bn254_fq
+#include "ec_impl.h"
+#undef EC
+#undef EF
+#define EC bn254_g2
+#define EF bn254_fq2
+#include "ec_impl.h"
+#undef EC
+#undef EF
+#define EC bls12_381_g1
+#define EF bls12_381_fq
+#include "ec_impl.h"
+#undef EC
+#undef EF
+#define EC bls12_381_g2
+#define EF bls12_381_fq2
+#include "ec_impl.h"
+#undef EC
+#undef EF
+
+/* ---- MSM ------------------------------------------------------------------ */
+#define EC bn254_g1
+#define EF bn254_fq
+#define SF bn254_fr
+#define SF_N 4
+#define SF_BITS BN254_FR_BITS
+#include "msm_impl.h"
+#undef EC
+#undef EF
+#define EC bn254_g2
+#define EF bn254_fq2
+#include "msm_impl.h"
+#undef EC
+#undef EF
+#undef SF
+#undef SF_BITS
+#define SF bls12_381_fr
+#define SF_BITS BLS12_381_FR_BITS
+#define EC bls12_381_g1
+#define EF bls12_381_fq
+#include "msm_impl.h"
+#undef EC
+#undef EF
+#define EC bls12_381_g2
+#define EF bls12_381_fq2
+#include "msm_impl.h"
+#undef EC
+#undef EF
+#undef SF
+#undef SF_N
+#undef SF_BITS
+
+/* ---- NTT ------------------------------------------------------------------ */
+#define FF bn254_fr
+#define FF_TWO_ADICITY BN254_FR_TWO_ADICITY
+#define FF_TWO_ADIC_ROOT BN254_FR_TWO_ADIC_ROOT_MONT
+#include "ntt_impl.h"
+#undef FF
+#undef FF_TWO_ADICITY
+#undef FF_TWO_ADIC_ROOT
+#define FF bls12_381_fr
+#define FF_TWO_ADICITY BLS12_381_FR_TWO_ADICITY
+#define FF_TWO_ADIC_ROOT BLS12_381_FR_TWO_ADIC_ROOT_MONT
+#include "ntt_impl.h"
+#undef FF
+#undef FF_TWO_ADICITY
+#undef FF_TWO_ADIC_ROOT
+
+/* ========================================================================== */
+/* Exported API (ctypes).  Field ids: 0 bn254_fq, 1 bn254_fr, 2 bls12_381_fq,
+ * 3 bls12_381_fr.  Curve ids: 0 bn254_g1, 1 bn254_g2, 2 bls12_381_g1,
+ * 3 bls12_381_g2.  All field data is Montgomery-form 64-bit LE limbs unless a
+ * function says "canonical". */
+#define EXPORT __attribute__((visibility("default")))
+
+EXPORT int oracle_field_limbs(int field) {
+  switch (field) {
+    case 0: case 1: case 3: return 4;
+    case 2: return 6;
+  }
+  return 0;
+}
+
+#define FIELD_OP_CASE(F, NL)                                                     \
+  {                                                                               \
+    const F##_t* A = (const F##_t*)a;                                             \
+    const F##_t* B = (const F##_t*)b;                                             \
+    F##_t* O = (F##_t*)out;                                                       \
+    for (size_t i = 0; i < count; ++i) {                                          \
+      switch (op) {                                                               \
+        case 0: O[i] = F##_add(A[i], B[i]); break;                                \
+        case 1: O[i] = F##_sub(A[i], B[i]); break;                                \
+        case 2: O[i] = F##_mul(A[i], B[i]); break;                                \
+        case 3: O[i] = F##_sqr(A[i]); break;                                      \
+        case 4: O[i] = F##_neg(A[i]); break;                                      \
+        case 5: O[i] = F##_inv(A[i]); break;                                      \
+        case 6: O[i] = F##_from_bigint(A[i].l); break;                            \
+        case 7: F##_to_bigint(&A[i], O[i].l); break;                              \
+        case 8: O[i] = F##_dbl(A[i]); break;                                      \
+        default: return -1;                                                       \
+      }                                                                           \
+    }                                                                             \
+    return 0;                                                                     \
+  }
+
+/* op: 0 add, 1 sub, 2 mul, 3 square, 4 negate, 5 inverse, 6 canonical->Montgomery,
+ *     7 Montgomery->canonical, 8 double. */
+EXPORT int oracle_field_op(int field, int op, const void* a, const void* b, void* out, size_t count) {
+  switch (field) {
+    case 0: FIELD_OP_CASE(bn254_fq, 4)
+    case 1: FIELD_OP_CASE(bn254_fr, 4)
+    case 2: FIELD_OP_CASE(bls12_381_fq, 6)
+    case 3: FIELD_OP_CASE(bls12_381_fr, 4)
+  }
+  return -1;
+}
+
+/* ---- deterministic synthetic inputs ---------------------------------------
+ * Counter-based splitmix64: u64(seed, ctr) = mix(seed + (ctr+1)*gamma), i.e.
+ * the ctr-th output of a splitmix64 stream seeded with `seed`.  The product's
+ * GPU input generator implements the identical scheme, so parity tests can
+ * cross-check it.
+ *   scalar i : limbs u64(seed, i*4 + k), k<4, halved until < r (BigInt::Random,
+ *              big_int.h:107-115), then FromBigInt (Montgomery).
+ *   bases    : chunks of `chunk` points; chunk j starts at k_j*G with
+ *              k_j = scalar(seed ^ BASE_SEED_XOR, j) and continues by doubling
+ *              (CreatePseudoRandomPoints, test/random.h:12-28). */
+#define SM_GAMMA UINT64_C(0x9E3779B97F4A7C15)
+#define BASE_SEED_XOR UINT64_C(0xBA5E5EEDBA5E5EED)
+
+static inline uint64_t sm_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * UINT64_C(0xBF58476D1CE4E5B9);
+  z = (z ^ (z >> 27)) * UINT64_C(0x94D049BB133111EB);
+  return z ^ (z >> 31);
+}
+EXPORT uint64_t oracle_rand_u64(uint64_t seed, uint64_t ctr) { return sm_mix(seed + (ctr + 1) * SM_GAMMA); }
+
+static inline int geq_limbs(const uint64_t* a, const uint64_t* b, int n) {
+  for (int i = n - 1; i >= 0; --i) {
+    if (a[i] > b[i]) return 1;
+    if (a[i] < b[i]) return 0;
+  }
+  return 1;
+}
+
+/* canonical random scalar (4 limbs) below modulus m */
+static inline void rand_scalar_canonical(uint64_t seed, uint64_t i, const uint64_t* m, uint64_t* out) {
+  for (int k = 0; k < 4; ++k) out[k] = oracle_rand_u64(seed, i * 4 + k);
+  while (geq_limbs(out, m, 4)) {
+    for (int k = 0; k < 3; ++k) out[k] = (out[k] >> 1) | (out[k + 1] << 63);
+    out[3] >>= 1;
+  }
+}
+
+/* scalar_field: 1 bn254_fr, 3 bls12_381_fr.  Writes Montgomery scalars
+ * [start, start+n). */
+EXPORT int oracle_gen_scalars(int scalar_field, uint64_t seed, size_t start, size_t n, void* out) {
+  const uint64_t* m = scalar_field == 1 ? BN254_FR_P : BLS12_381_FR_P;
+  if (scalar_field != 1 && scalar_field != 3) return -1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t c[4];
+    rand_scalar_canonical(seed, start + i, m, c);
+    if (scalar_field == 1) ((bn254_fr_t*)out)[i] = bn254_fr_from_bigint(c);
+    else ((bls12_381_fr_t*)out)[i] = bls12_381_fr_from_bigint(c);
+  }
+  return 0;
+}
+
+#define GEN_BASES(EC, EF, GX, GY)                                                      \
+  {                                                                                     \
+    EC##_affine_t* O = (EC##_affine_t*)out;                                             \
+    EC##_affine_t G;                                                                    \
+    memcpy(&G.x, GX, sizeof G.x);                                                       \
+    memcpy(&G.y, GY, sizeof G.y);                                                       \
+    size_t nchunks = (n + chunk - 1) / chunk;                                           \
+    int failed = 0;                                                                     \
+    _Pragma("omp parallel for schedule(dynamic)")                                       \
+    for (size_t j = 0; j < nchunks; ++j) {                                              \
+      size_t s = j * chunk, len = (s + chunk <= n) ? chunk : n - s;                     \
+      EC##_xyzz_t* tmp = (EC##_xyzz_t*)malloc(sizeof(EC##_xyzz_t) * len);               \
+      EF##_t* scr = (EF##_t*)malloc(sizeof(EF##_t) * len);                              \
+      if (!tmp || !scr) { failed = 1; free(tmp); free(scr); continue; }                 \
+      uint64_t k[4];                                                                    \
+      rand_scalar_canonical(seed ^ BASE_SEED_XOR, j, sm, k);                            \
+      EC##_xyzz_t r = EC##_scalar_mul(&G, k, 4);                                        \
+      for (size_t i = 0; i < len; ++i) { tmp[i] = r; r = EC##_xyzz_dbl(&r); }          \
+      EC##_batch_to_affine(tmp, O + s, len, scr);                                       \
+      free(tmp);                                                                        \
+      free(scr);                                                                        \
+    }                                                                                   \
+    return failed ? -2 : 0;                                                             \
+  }
+
+EXPORT int oracle_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* out) {
+  if (chunk == 0) return -1;
+  const uint64_t* sm = (curve <= 1) ? BN254_FR_P : BLS12_381_FR_P;
+  switch (curve) {
+    case 0: GEN_BASES(bn254_g1, bn254_fq, BN254_G1_X_MONT, BN254_G1_Y_MONT)
+    case 1: GEN_BASES(bn254_g2, bn254_fq2, BN254_G2_X_MONT, BN254_G2_Y_MONT)
+    case 2: GEN_BASES(bls12_381_g1, bls12_381_fq, BLS12_381_G1_X_MONT, BLS12_381_G1_Y_MONT)
+    case 3: GEN_BASES(bls12_381_g2, bls12_381_fq2, BLS12_381_G2_X_MONT, BLS12_381_G2_Y_MONT)
+  }
+  return -1;
+}
+
+/* ---- MSM ------------------------------------------------------------------ */
+/* method: 0 PippengerAdapter kParallelTerm (reference default), 1 single
+ * Pippenger (kNone), 2 naive double-and-add.  Writes the affine result (x, y)
+ * and, if out_jac != NULL, the Jacobian the reference C-ABI would return
+ * (ConvertPoint<Jacobian>(XYZZ), point_xyzz.h:228-237). */
+#define MSM_CASE(EC)                                                                     \
+  {                                                                                      \
+    const EC##_affine_t* B = (const EC##_affine_t*)bases;                                \
+    EC##_xyzz_t r;                                                                       \
+    if (method == 0) r = EC##_msm_parallel_term(B, S, n, threads);                       \
+    else if (method == 1) r = EC##_pippenger(B, S, n);                                   \
+    else r = EC##_msm_naive(B, S, n);                                                    \
+    *(EC##_affine_t*)out_affine = EC##_xyzz_to_affine(&r);                               \
+    if (out_jac) *(EC##_jacobian_t*)out_jac = EC##_xyzz_to_jacobian(&r);                 \
+    return 0;                                                                            \
+  }
+
+EXPORT int oracle_msm(int curve, const void* bases, const void* scalars, size_t n, int method,
+                      int threads, void* out_affine, void* out_jac) {
+  switch (curve) {
+    case 0: { const bn254_fr_t* S = (const bn254_fr_t*)scalars; MSM_CASE(bn254_g1) }
+    case 1: { const bn254_fr_t* S = (const bn254_fr_t*)scalars; MSM_CASE(bn254_g2) }
+    case 2: { const bls12_381_fr_t* S = (const bls12_381_fr_t*)scalars; MSM_CASE(bls12_381_g1) }
+    case 3: { const bls12_381_fr_t* S = (const bls12_381_fr_t*)scalars; MSM_CASE(bls12_381_g2) }
+  }
+  return -1;
+}
+
+/* Point helpers for tests.  op: 0 P+Q (affine,affine -> affine), 1 2P,
+ * 2 is_on_curve(P) -> return value, 3 k*P (k canonical 4 limbs in `q`),
+ * 4 jacobian -> affine (p = jacobian). */
+#define EC_OP_CASE(EC, BCONST)                                                           \
+  {                                                                                      \
+    const EC##_affine_t* A = (const EC##_affine_t*)p;                                    \
+    switch (op) {                                                                        \
+      case 0: {                                                                          \
+        EC##_xyzz_t t = EC##_affine_to_xyzz(A);                                          \
+        t = EC##_xyzz_madd(&t, (const EC##_affine_t*)q);                                 \
+        *(EC##_affine_t*)out = EC##_xyzz_to_affine(&t);                                  \
+        return 0;                                                                        \
+      }                                                                                  \
+      case 1: {                                                                          \
+        EC##_xyzz_t t = EC##_affine_to_xyzz(A);                                          \
+        t = EC##_xyzz_dbl(&t);                                                           \
+        *(EC##_affine_t*)out = EC##_xyzz_to_affine(&t);                                  \
+        return 0;                                                                        \
+      }                                                                                  \
+      case 2: {                                                                          \
+        __typeof__(((EC##_affine_t*)0)->x) b;                                                            \
+        memcpy(&b, BCONST, sizeof b);                                                    \
+        return EC##_affine_is_on_curve(A, &b);                                           \
+      }                                                                                  \
+      case 3: {                                                                          \
+        EC##_xyzz_t t = EC##_scalar_mul(A, (const uint64_t*)q, 4);                       \
+        *(EC##_affine_t*)out = EC##_xyzz_to_affine(&t);                                  \
+        return 0;                                                                        \
+      }                                                                                  \
+      case 4: {                                                                          \
+        *(EC##_affine_t*)out = EC##_jacobian_to_affine((const EC##_jacobian_t*)p);       \
+        return 0;                                                                        \
+      }                                                                                  \
+    }                                                                                    \
+    return -1;                                                                           \
+  }
+
+EXPORT int oracle_ec_op(int curve, int op, const void* p, const void* q, void* out) {
+  switch (curve) {
+    case 0: EC_OP_CASE(bn254_g1, BN254_G1_B_MONT)
+    case 1: EC_OP_CASE(bn254_g2, BN254_G2_B_MONT)
+    case 2: EC_OP_CASE(bls12_381_g1, BLS12_381_G1_B_MONT)
+    case 3: EC_OP_CASE(bls12_381_g2, BLS12_381_G2_B_MONT)
+  }
+  return -1;
+}
+
+/* ---- NTT ------------------------------------------------------------------ */
+/* field: 1 bn254_fr, 3 bls12_381_fr.  v has room for the domain size
+ * (bit_ceil(domain_num_coeffs)); `len` input elements.  offset (Montgomery) may
+ * be NULL for the plain domain.  Returns the output length (FFT: domain size
+ * or 0; IFFT: length after RemoveHighDegreeZeros), or -1. */
+#define NTT_CASE(F, FN)                                                                  \
+  {                                                                                      \
+    F##_domain_t* d = F##_domain_create(domain_num_coeffs);                              \
+    if (!d) return -1;                                                                   \
+    if (offset) { F##_t o; memcpy(&o, offset, sizeof o); F##_domain_set_offset(d, o); }  \
+    long r = (long)F##_domain_##FN(d, (F##_t*)v, len);                                   \
+    F##_domain_destroy(d);                                                               \
+    return r;                                                                            \
+  }
+
+EXPORT long oracle_fft(int field, size_t domain_num_coeffs, const void* offset, void* v, size_t len) {
+  if (field == 1) NTT_CASE(bn254_fr, fft)
+  if (field == 3) NTT_CASE(bls12_381_fr, fft)
+  return -1;
+}
+
+EXPORT long oracle_ifft(int field, size_t domain_num_coeffs, const void* offset, void* v, size_t len) {
+  if (field == 1) NTT_CASE(bn254_fr, ifft)
+  if (field == 3) NTT_CASE(bls12_381_fr, ifft)
+  return -1;
+}
+
+/* Domain scalars for tests: writes group_gen, group_gen_inv, size_inv. */
+EXPORT int oracle_domain_info(int field, size_t num_coeffs, void* out3) {
+  if (field == 1) {
+    bn254_fr_domain_t* d = bn254_fr_domain_create(num_coeffs);
+    if (!d) return -1;
+    bn254_fr_t* o = (bn254_fr_t*)out3;
+    o[0] = d->group_gen; o[1] = d->group_gen_inv; o[2] = d->size_inv;
+    bn254_fr_domain_destroy(d);
+    return 0;
+  }
+  return -1;
+}
+
+EXPORT int oracle_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
