@@ -1,0 +1,252 @@
+/*
+ * tachyon_mi355x.h -- C-ABI of the MI355X MSM + NTT backend.
+ *
+ * The entry points in the "reference C-ABI" sections keep the names, argument
+ * meaning, ownership and error behaviour of Tachyon's tachyon/c API
+ * (reference snapshot /root/reference, cited per declaration) so a binary
+ * linked against libtachyon.so's MSM / univariate-domain symbols can link
+ * against libtachyon_mi355x.so instead.  Entry points prefixed
+ * tachyon_mi355x_ are extensions (device-resident buffers, G2 MSM, multi-GPU
+ * helpers, synthetic inputs, timings); they have no reference counterpart.
+ *
+ * Data layout (identical to the reference, msm_input_provider.h:23-29
+ * bit-casts these structs to its native types):
+ *   field elements: Montgomery form, R = 2^(64*N), little-endian 64-bit limbs
+ *   affine / point2: {x, y}, identity = (0, 0) (affine_point.h:39,125)
+ *   jacobian / projective: {x, y, z};  xyzz: {x, y, zz, zzz}
+ *
+ * Ownership: returned points / containers are allocated with C++ operator
+ * new (as msm.h:45 / msm_gpu.h:81 / bn254_univariate_evaluation_domain.cc:50-85
+ * do); free them with delete (C++) or the matching *_destroy / free helper.
+ * Errors: like the reference's CHECK, any failure prints a message and aborts.
+ * There is no CPU fallback: every compute entry point needs a HIP device.
+ */
+#ifndef TACHYON_MI355X_H_
+#define TACHYON_MI355X_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#define TACHYON_C_EXPORT __attribute__((visibility("default")))
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- field and point types (prime_field.h.tpl / point.h.tpl:22-94) -------- */
+typedef struct tachyon_bn254_fq { uint64_t limbs[4]; } tachyon_bn254_fq;
+typedef struct tachyon_bn254_fr { uint64_t limbs[4]; } tachyon_bn254_fr;
+typedef struct tachyon_bn254_fq2 { tachyon_bn254_fq c0, c1; } tachyon_bn254_fq2;
+typedef struct tachyon_bls12_381_fq { uint64_t limbs[6]; } tachyon_bls12_381_fq;
+typedef struct tachyon_bls12_381_fr { uint64_t limbs[4]; } tachyon_bls12_381_fr;
+typedef struct tachyon_bls12_381_fq2 { tachyon_bls12_381_fq c0, c1; } tachyon_bls12_381_fq2;
+
+#define TACHYON_MI355X_POINT_TYPES(C, G, F)                                   \
+  typedef struct tachyon_##C##_##G##_affine { F x, y; } tachyon_##C##_##G##_affine;             \
+  typedef struct tachyon_##C##_##G##_point2 { F x, y; } tachyon_##C##_##G##_point2;             \
+  typedef struct tachyon_##C##_##G##_jacobian { F x, y, z; } tachyon_##C##_##G##_jacobian;      \
+  typedef struct tachyon_##C##_##G##_projective { F x, y, z; } tachyon_##C##_##G##_projective;  \
+  typedef struct tachyon_##C##_##G##_xyzz { F x, y, zz, zzz; } tachyon_##C##_##G##_xyzz;
+
+TACHYON_MI355X_POINT_TYPES(bn254, g1, tachyon_bn254_fq)
+TACHYON_MI355X_POINT_TYPES(bn254, g2, tachyon_bn254_fq2)
+TACHYON_MI355X_POINT_TYPES(bls12_381, g1, tachyon_bls12_381_fq)
+TACHYON_MI355X_POINT_TYPES(bls12_381, g2, tachyon_bls12_381_fq2)
+#undef TACHYON_MI355X_POINT_TYPES
+
+/* ========================================================================== */
+/* Reference C-ABI: MSM (generated per curve from                              */
+/* tachyon/c/math/elliptic_curves/generator/msm{,_gpu}.h.tpl; G1 only there)   */
+/* ========================================================================== */
+typedef struct tachyon_bn254_g1_msm* tachyon_bn254_g1_msm_ptr;               /* msm.h.tpl:21 */
+typedef struct tachyon_bn254_g1_msm_gpu* tachyon_bn254_g1_msm_gpu_ptr;       /* msm_gpu.h.tpl:17 */
+typedef struct tachyon_bls12_381_g1_msm* tachyon_bls12_381_g1_msm_ptr;
+typedef struct tachyon_bls12_381_g1_msm_gpu* tachyon_bls12_381_g1_msm_gpu_ptr;
+
+/* point.cc.tpl:7-9 -- curve constant initialisation; constants are compiled in here, so a no-op. */
+TACHYON_C_EXPORT void tachyon_bn254_g1_init(void);
+TACHYON_C_EXPORT void tachyon_bls12_381_g1_init(void);
+TACHYON_C_EXPORT void tachyon_bn254_g2_init(void);
+TACHYON_C_EXPORT void tachyon_bls12_381_g2_init(void);
+
+/* msm.h.tpl:30-58 (CPU-named entry points; served by the MI355X backend). */
+TACHYON_C_EXPORT tachyon_bn254_g1_msm_ptr tachyon_bn254_g1_create_msm(uint8_t degree);
+TACHYON_C_EXPORT void tachyon_bn254_g1_destroy_msm(tachyon_bn254_g1_msm_ptr ptr);
+TACHYON_C_EXPORT tachyon_bn254_g1_jacobian* tachyon_bn254_g1_point2_msm(
+    tachyon_bn254_g1_msm_ptr ptr, const tachyon_bn254_g1_point2* bases, const tachyon_bn254_fr* scalars,
+    size_t size);
+TACHYON_C_EXPORT tachyon_bn254_g1_jacobian* tachyon_bn254_g1_affine_msm(
+    tachyon_bn254_g1_msm_ptr ptr, const tachyon_bn254_g1_affine* bases, const tachyon_bn254_fr* scalars,
+    size_t size);
+
+/* msm_gpu.h.tpl:26-54 -> tachyon/c/math/elliptic_curves/msm/msm_gpu.h:23-122. */
+TACHYON_C_EXPORT tachyon_bn254_g1_msm_gpu_ptr tachyon_bn254_g1_create_msm_gpu(uint8_t degree);
+TACHYON_C_EXPORT void tachyon_bn254_g1_destroy_msm_gpu(tachyon_bn254_g1_msm_gpu_ptr ptr);
+TACHYON_C_EXPORT tachyon_bn254_g1_jacobian* tachyon_bn254_g1_point2_msm_gpu(
+    tachyon_bn254_g1_msm_gpu_ptr ptr, const tachyon_bn254_g1_point2* bases, const tachyon_bn254_fr* scalars,
+    size_t size);
+TACHYON_C_EXPORT tachyon_bn254_g1_jacobian* tachyon_bn254_g1_affine_msm_gpu(
+    tachyon_bn254_g1_msm_gpu_ptr ptr, const tachyon_bn254_g1_affine* bases, const tachyon_bn254_fr* scalars,
+    size_t size);
+
+TACHYON_C_EXPORT tachyon_bls12_381_g1_msm_ptr tachyon_bls12_381_g1_create_msm(uint8_t degree);
+TACHYON_C_EXPORT void tachyon_bls12_381_g1_destroy_msm(tachyon_bls12_381_g1_msm_ptr ptr);
+TACHYON_C_EXPORT tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_point2_msm(
+    tachyon_bls12_381_g1_msm_ptr ptr, const tachyon_bls12_381_g1_point2* bases,
+    const tachyon_bls12_381_fr* scalars, size_t size);
+TACHYON_C_EXPORT tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_affine_msm(
+    tachyon_bls12_381_g1_msm_ptr ptr, const tachyon_bls12_381_g1_affine* bases,
+    const tachyon_bls12_381_fr* scalars, size_t size);
+TACHYON_C_EXPORT tachyon_bls12_381_g1_msm_gpu_ptr tachyon_bls12_381_g1_create_msm_gpu(uint8_t degree);
+TACHYON_C_EXPORT void tachyon_bls12_381_g1_destroy_msm_gpu(tachyon_bls12_381_g1_msm_gpu_ptr ptr);
+TACHYON_C_EXPORT tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_point2_msm_gpu(
+    tachyon_bls12_381_g1_msm_gpu_ptr ptr, const tachyon_bls12_381_g1_point2* bases,
+    const tachyon_bls12_381_fr* scalars, size_t size);
+TACHYON_C_EXPORT tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_affine_msm_gpu(
+    tachyon_bls12_381_g1_msm_gpu_ptr ptr, const tachyon_bls12_381_g1_affine* bases,
+    const tachyon_bls12_381_fr* scalars, size_t size);
+
+/* ========================================================================== */
+/* Reference C-ABI: univariate evaluation domain over BN254 Fr                 */
+/* (tachyon/c/math/polynomials/univariate/bn254_univariate_*.h)               */
+/* ========================================================================== */
+typedef struct tachyon_bn254_univariate_evaluation_domain tachyon_bn254_univariate_evaluation_domain;
+typedef struct tachyon_bn254_univariate_evaluations tachyon_bn254_univariate_evaluations;
+typedef struct tachyon_bn254_univariate_dense_polynomial tachyon_bn254_univariate_dense_polynomial;
+
+/* bn254_univariate_evaluation_domain.h:38-136 */
+TACHYON_C_EXPORT tachyon_bn254_univariate_evaluation_domain* tachyon_bn254_univariate_evaluation_domain_create(
+    size_t num_coeffs);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_evaluation_domain_destroy(
+    tachyon_bn254_univariate_evaluation_domain* domain);
+TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_empty_evals(
+    const tachyon_bn254_univariate_evaluation_domain* domain);
+TACHYON_C_EXPORT tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_empty_poly(
+    const tachyon_bn254_univariate_evaluation_domain* domain);
+TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_fft(
+    const tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_univariate_dense_polynomial* poly);
+TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_fft_inplace(
+    const tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_univariate_dense_polynomial* poly);
+TACHYON_C_EXPORT tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_ifft(
+    const tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_univariate_evaluations* evals);
+TACHYON_C_EXPORT tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_ifft_inplace(
+    const tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_univariate_evaluations* evals);
+
+/* bn254_univariate_evaluations.h:36-79 */
+TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluations_create(void);
+TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluations_clone(
+    const tachyon_bn254_univariate_evaluations* evals);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_evaluations_destroy(tachyon_bn254_univariate_evaluations* evals);
+TACHYON_C_EXPORT size_t tachyon_bn254_univariate_evaluations_len(const tachyon_bn254_univariate_evaluations* evals);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_evaluations_set_value(tachyon_bn254_univariate_evaluations* evals,
+                                                                     size_t i, const tachyon_bn254_fr* value);
+
+/* bn254_univariate_dense_polynomial.h (create/clone/destroy) */
+TACHYON_C_EXPORT tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_dense_polynomial_create(void);
+TACHYON_C_EXPORT tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_dense_polynomial_clone(
+    const tachyon_bn254_univariate_dense_polynomial* poly);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_dense_polynomial_destroy(
+    tachyon_bn254_univariate_dense_polynomial* poly);
+
+/* ========================================================================== */
+/* Extensions (no reference counterpart)                                       */
+/* ========================================================================== */
+/* Container access the reference performs through C++ native_cast. */
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluations_get_value(
+    const tachyon_bn254_univariate_evaluations* evals, size_t i, tachyon_bn254_fr* value);
+TACHYON_C_EXPORT tachyon_bn254_fr* tachyon_mi355x_bn254_univariate_evaluations_data(
+    tachyon_bn254_univariate_evaluations* evals);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluations_resize(tachyon_bn254_univariate_evaluations* evals,
+                                                                         size_t len);
+TACHYON_C_EXPORT size_t tachyon_mi355x_bn254_univariate_dense_polynomial_len(
+    const tachyon_bn254_univariate_dense_polynomial* poly);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_dense_polynomial_resize(
+    tachyon_bn254_univariate_dense_polynomial* poly, size_t len);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_dense_polynomial_set_value(
+    tachyon_bn254_univariate_dense_polynomial* poly, size_t i, const tachyon_bn254_fr* value);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_dense_polynomial_get_value(
+    const tachyon_bn254_univariate_dense_polynomial* poly, size_t i, tachyon_bn254_fr* value);
+TACHYON_C_EXPORT tachyon_bn254_fr* tachyon_mi355x_bn254_univariate_dense_polynomial_data(
+    tachyon_bn254_univariate_dense_polynomial* poly);
+
+/* Domain queries and the coset hook (UnivariateEvaluationDomain::GetCoset,
+ * univariate_evaluation_domain.h:102-117): set_offset turns the domain into
+ * its coset h*<w>; offset 1 restores it. */
+TACHYON_C_EXPORT size_t tachyon_mi355x_bn254_univariate_evaluation_domain_size(
+    const tachyon_bn254_univariate_evaluation_domain* domain);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_group_gen(
+    const tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_fr* out);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset(
+    tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_fr* offset);
+/* Device-resident in-place transform of size() elements at d_data (HBM),
+ * enqueued on `stream` (hipStream_t, NULL = the domain's own stream).
+ * inverse = 0: FFT, 1: IFFT (no trimming).  Not synchronised. */
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(
+    tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_fr* d_data, int inverse);
+TACHYON_C_EXPORT void* tachyon_mi355x_bn254_univariate_evaluation_domain_stream(
+    tachyon_bn254_univariate_evaluation_domain* domain);
+/* per-pass device time (ms) of the last transform when profiling is on;
+ * returns the number of passes written. */
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(
+    tachyon_bn254_univariate_evaluation_domain* domain, int on);
+TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(
+    const tachyon_bn254_univariate_evaluation_domain* domain, float* total_ms, float* pass_ms, int max_passes);
+
+/* G2 MSM contexts (Groth16's B-in-G2, BLS12-381 config 4); same semantics as
+ * the G1 *_msm_gpu entry points. */
+typedef struct tachyon_bn254_g2_msm_gpu* tachyon_bn254_g2_msm_gpu_ptr;
+typedef struct tachyon_bls12_381_g2_msm_gpu* tachyon_bls12_381_g2_msm_gpu_ptr;
+TACHYON_C_EXPORT tachyon_bn254_g2_msm_gpu_ptr tachyon_bn254_g2_create_msm_gpu(uint8_t degree);
+TACHYON_C_EXPORT void tachyon_bn254_g2_destroy_msm_gpu(tachyon_bn254_g2_msm_gpu_ptr ptr);
+TACHYON_C_EXPORT tachyon_bn254_g2_jacobian* tachyon_bn254_g2_affine_msm_gpu(
+    tachyon_bn254_g2_msm_gpu_ptr ptr, const tachyon_bn254_g2_affine* bases, const tachyon_bn254_fr* scalars,
+    size_t size);
+TACHYON_C_EXPORT tachyon_bls12_381_g2_msm_gpu_ptr tachyon_bls12_381_g2_create_msm_gpu(uint8_t degree);
+TACHYON_C_EXPORT void tachyon_bls12_381_g2_destroy_msm_gpu(tachyon_bls12_381_g2_msm_gpu_ptr ptr);
+TACHYON_C_EXPORT tachyon_bls12_381_g2_jacobian* tachyon_bls12_381_g2_affine_msm_gpu(
+    tachyon_bls12_381_g2_msm_gpu_ptr ptr, const tachyon_bls12_381_g2_affine* bases,
+    const tachyon_bls12_381_fr* scalars, size_t size);
+
+/* Curve-generic extension API.  curve: 0 bn254_g1, 1 bn254_g2, 2 bls12_381_g1,
+ * 3 bls12_381_g2.  A context is any *_msm_gpu_ptr / *_msm_ptr of that curve. */
+/* Affine result written to out_affine (identity = all zero bytes). */
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const void* bases, const void* scalars,
+                                                    size_t size, void* out_affine);
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c);
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
+/* ms: h2d, recode, sort, acc, reduce, total (6 floats) */
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out6);
+/* window bits / windows the planner picks for `size` points */
+TACHYON_C_EXPORT void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows);
+/* Host-side group arithmetic on affine points (multi-GPU partial sums):
+ * out = sum of `count` affine points. */
+TACHYON_C_EXPORT void tachyon_mi355x_affine_sum(int curve, const void* points, size_t count, void* out_affine);
+/* Jacobian -> affine. */
+TACHYON_C_EXPORT void tachyon_mi355x_jacobian_to_affine(int curve, const void* jacobian, void* out_affine);
+
+/* Synthetic inputs generated on the device (bench / tests):
+ *   scalars: splitmix64 counter stream, BigInt::Random halving, Montgomery
+ *   bases:   chunks of `chunk` points, chunk j = k_j * G, 2 k_j * G, 4 k_j * G ...
+ * field: 1 bn254_fr, 3 bls12_381_fr.  d_out is device memory. stream may be NULL. */
+TACHYON_C_EXPORT void tachyon_mi355x_gen_scalars(int field, uint64_t seed, size_t start, size_t n, void* d_out,
+                                                 void* stream);
+TACHYON_C_EXPORT void tachyon_mi355x_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* d_out,
+                                               void* stream);
+
+/* Elementwise device parity kernels (prime_field_correctness_gpu_test.cc,
+ * (non_)affine_point_correctness_gpu_test.cc).  field: 0 bn254_fq, 1 bn254_fr,
+ * 2 bls12_381_fq, 3 bls12_381_fr; op: 0 add 1 sub 2 mul 3 sqr 4 neg 5 inv
+ * 6 to_mont 7 from_mont 8 dbl.  Host buffers in, host buffer out. */
+TACHYON_C_EXPORT void tachyon_mi355x_field_op(int field, int op, const void* a, const void* b, void* out,
+                                              size_t count);
+/* point op: 0 add (affine + affine), 1 double, 2 add-mixed into xyzz of a. Affine in/out. */
+TACHYON_C_EXPORT void tachyon_mi355x_ec_op(int curve, int op, const void* a, const void* b, void* out, size_t count);
+
+TACHYON_C_EXPORT const char* tachyon_mi355x_version(void);
+TACHYON_C_EXPORT int tachyon_mi355x_device_count(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* TACHYON_MI355X_H_ */

@@ -1,0 +1,530 @@
+// C-ABI of the MI355X backend (include/tachyon_mi355x.h).
+//
+// Reference entry points restated here:
+//   tachyon/c/math/elliptic_curves/generator/msm.cc.tpl, msm_gpu.cc.tpl
+//   tachyon/c/math/elliptic_curves/msm/msm.h:13-48 (MSMApi / DoMSM)
+//   tachyon/c/math/elliptic_curves/msm/msm_gpu.h:23-122 (MSMGpuApi / DoMSMGpu,
+//     TACHYON_MSM_GPU_INPUT_DIR / TACHYON_LOG_MSM hooks)
+//   tachyon/c/math/polynomials/univariate/bn254_univariate_evaluation_domain.cc:22-85
+//   tachyon/c/math/polynomials/univariate/bn254_univariate_evaluations.cc
+//   tachyon/c/math/polynomials/univariate/bn254_univariate_dense_polynomial.cc
+#include "../../../include/tachyon_mi355x.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../msm/msm.h"
+#include "../ntt/ntt.h"
+#include "../util/device_ops.h"
+
+using namespace tachyon_amd;
+
+namespace {
+
+[[noreturn]] void die(const char* fn, const char* what) {
+  fprintf(stderr, "[tachyon_mi355x] %s failed: %s\n", fn, what);
+  fflush(stderr);
+  abort();  // the reference CHECK-aborts (msm.h:42-43, msm_gpu.h:79-80)
+}
+
+#define GUARD_BEGIN try {
+#define GUARD_END                                   \
+  }                                                 \
+  catch (const std::exception& e) { die(__func__, e.what()); } \
+  catch (...) { die(__func__, "unknown exception"); }
+
+template <class Curve>
+struct MsmCtx {
+  msm::MsmGpu<Curve> impl;
+  std::string input_dir;  // TACHYON_MSM_GPU_INPUT_DIR
+  bool log = false;       // TACHYON_LOG_MSM=1
+  size_t idx = 0;
+  MsmCtx() {
+    if (const char* d = getenv("TACHYON_MSM_GPU_INPUT_DIR")) input_dir = d;
+    if (const char* l = getenv("TACHYON_LOG_MSM")) log = (std::string(l) == "1");
+  }
+};
+
+template <class F>
+void write_canonical(FILE* f, const F& x);
+
+template <class C>
+void write_canonical(FILE* f, const Fp<C>& x) {
+  Fp<C> c = x.from_mont();
+  fwrite(c.v, sizeof(c.v), 1, f);
+}
+template <class B>
+void write_canonical(FILE* f, const Fp2<B>& x) {
+  write_canonical(f, x.c0);
+  write_canonical(f, x.c1);
+}
+
+// Replay dump (msm_gpu.h:99-119): u64 count, then canonical LE limbs
+// (Buffer serialisation with s_is_in_montgomery = false, copyable.h:137-155).
+template <class Curve>
+void dump_inputs(const std::string& dir, size_t idx, const void* bases, const void* scalars, size_t n) {
+  using F = typename Curve::F;
+  using Fr = typename Curve::Fr;
+  std::vector<Affine<F>> hb(n);
+  std::vector<Fr> hs(n);
+  TA_HIP(hipMemcpy(hb.data(), bases, n * sizeof(Affine<F>), hipMemcpyDefault));
+  TA_HIP(hipMemcpy(hs.data(), scalars, n * sizeof(Fr), hipMemcpyDefault));
+  std::string pb = dir + "/bases" + std::to_string(idx) + ".txt";
+  std::string ps = dir + "/scalars" + std::to_string(idx) + ".txt";
+  FILE* f = fopen(pb.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot open " + pb);
+  uint64_t cnt = n;
+  fwrite(&cnt, 8, 1, f);
+  for (auto& p : hb) {
+    write_canonical(f, p.x);
+    write_canonical(f, p.y);
+  }
+  fclose(f);
+  f = fopen(ps.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot open " + ps);
+  fwrite(&cnt, 8, 1, f);
+  for (auto& s : hs) write_canonical(f, s);
+  fclose(f);
+}
+
+template <class F>
+void print_hex(const F& x) {
+  const uint64_t* l = reinterpret_cast<const uint64_t*>(&x);
+  printf("0x");
+  for (size_t i = sizeof(F) / 8; i-- > 0;) printf("%016lx", (unsigned long)l[i]);
+}
+
+// DoMSMGpu: run, normalise, return a new Jacobian (z = 1, or the (1,1,0) zero).
+template <class Curve, class CJac>
+CJac* do_msm(MsmCtx<Curve>* ctx, const void* bases, const void* scalars, size_t n) {
+  using F = typename Curve::F;
+  XYZZ<F> r = ctx->impl.run(bases, scalars, n);
+  Affine<F> a = r.to_affine();
+  Jacobian<F> j = a.is_zero() ? Jacobian<F>::zero() : Jacobian<F>{a.x, a.y, F::one()};
+  static_assert(sizeof(CJac) == sizeof(Jacobian<F>), "layout");
+  CJac* out = new CJac();
+  memcpy(out, &j, sizeof(j));
+  if (ctx->log) {
+    printf("DoMSMGpu()%zu\n(", ctx->idx);
+    print_hex(a.x);
+    printf(", ");
+    print_hex(a.y);
+    printf(")\n");
+  }
+  ctx->idx++;
+  if (!ctx->input_dir.empty()) dump_inputs<Curve>(ctx->input_dir, ctx->idx - 1, bases, scalars, n);
+  return out;
+}
+
+template <class Curve>
+void msm_affine_out(void* ctx, const void* bases, const void* scalars, size_t n, void* out) {
+  using F = typename Curve::F;
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  Affine<F> a = c->impl.run(bases, scalars, n).to_affine();
+  memcpy(out, &a, sizeof(a));
+}
+
+template <class Curve>
+void affine_sum(const void* pts, size_t count, void* out) {
+  using F = typename Curve::F;
+  const Affine<F>* p = static_cast<const Affine<F>*>(pts);
+  XYZZ<F> acc = XYZZ<F>::zero();
+  for (size_t i = 0; i < count; ++i) acc = acc.madd(p[i]);
+  Affine<F> a = acc.to_affine();
+  memcpy(out, &a, sizeof(a));
+}
+
+template <class Curve>
+void jac_to_affine(const void* jac, void* out) {
+  using F = typename Curve::F;
+  Jacobian<F> j;
+  memcpy(&j, jac, sizeof(j));
+  Affine<F> a = XYZZ<F>::from_jacobian(j).to_affine();
+  memcpy(out, &a, sizeof(a));
+}
+
+}  // namespace
+
+namespace tachyon_amd::capi_detail {
+// univariate containers hold std::vector<bn254::Fr>, like the reference
+using FrC = tachyon_bn254_fr;
+struct Vec {
+  std::vector<FrC> v;
+};
+struct Domain {
+  std::unique_ptr<ntt::NttDomain<Bn254Fr>> impl;
+};
+}  // namespace tachyon_amd::capi_detail
+using tachyon_amd::capi_detail::Domain;
+using tachyon_amd::capi_detail::FrC;
+using tachyon_amd::capi_detail::Vec;
+
+struct tachyon_bn254_univariate_evaluations : Vec {};
+struct tachyon_bn254_univariate_dense_polynomial : Vec {};
+struct tachyon_bn254_univariate_evaluation_domain : Domain {};
+
+struct tachyon_bn254_g1_msm : MsmCtx<Bn254G1> {};
+struct tachyon_bn254_g1_msm_gpu : MsmCtx<Bn254G1> {};
+struct tachyon_bls12_381_g1_msm : MsmCtx<Bls381G1> {};
+struct tachyon_bls12_381_g1_msm_gpu : MsmCtx<Bls381G1> {};
+struct tachyon_bn254_g2_msm_gpu : MsmCtx<Bn254G2> {};
+struct tachyon_bls12_381_g2_msm_gpu : MsmCtx<Bls381G2> {};
+
+extern "C" {
+
+void tachyon_bn254_g1_init(void) {}
+void tachyon_bls12_381_g1_init(void) {}
+void tachyon_bn254_g2_init(void) {}
+void tachyon_bls12_381_g2_init(void) {}
+
+// ---- BN254 G1 ----
+tachyon_bn254_g1_msm_ptr tachyon_bn254_g1_create_msm(uint8_t degree) {
+  (void)degree;  // unused, as in msm.h:23
+  GUARD_BEGIN return new tachyon_bn254_g1_msm(); GUARD_END
+}
+void tachyon_bn254_g1_destroy_msm(tachyon_bn254_g1_msm_ptr ptr) { delete ptr; }
+tachyon_bn254_g1_jacobian* tachyon_bn254_g1_point2_msm(tachyon_bn254_g1_msm_ptr ptr,
+                                                       const tachyon_bn254_g1_point2* bases,
+                                                       const tachyon_bn254_fr* scalars, size_t size) {
+  GUARD_BEGIN return do_msm<Bn254G1, tachyon_bn254_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+tachyon_bn254_g1_jacobian* tachyon_bn254_g1_affine_msm(tachyon_bn254_g1_msm_ptr ptr,
+                                                       const tachyon_bn254_g1_affine* bases,
+                                                       const tachyon_bn254_fr* scalars, size_t size) {
+  GUARD_BEGIN return do_msm<Bn254G1, tachyon_bn254_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+tachyon_bn254_g1_msm_gpu_ptr tachyon_bn254_g1_create_msm_gpu(uint8_t degree) {
+  (void)degree;
+  GUARD_BEGIN return new tachyon_bn254_g1_msm_gpu(); GUARD_END
+}
+void tachyon_bn254_g1_destroy_msm_gpu(tachyon_bn254_g1_msm_gpu_ptr ptr) { delete ptr; }
+tachyon_bn254_g1_jacobian* tachyon_bn254_g1_point2_msm_gpu(tachyon_bn254_g1_msm_gpu_ptr ptr,
+                                                           const tachyon_bn254_g1_point2* bases,
+                                                           const tachyon_bn254_fr* scalars, size_t size) {
+  GUARD_BEGIN return do_msm<Bn254G1, tachyon_bn254_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+tachyon_bn254_g1_jacobian* tachyon_bn254_g1_affine_msm_gpu(tachyon_bn254_g1_msm_gpu_ptr ptr,
+                                                           const tachyon_bn254_g1_affine* bases,
+                                                           const tachyon_bn254_fr* scalars, size_t size) {
+  GUARD_BEGIN return do_msm<Bn254G1, tachyon_bn254_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+
+// ---- BLS12-381 G1 ----
+tachyon_bls12_381_g1_msm_ptr tachyon_bls12_381_g1_create_msm(uint8_t degree) {
+  (void)degree;
+  GUARD_BEGIN return new tachyon_bls12_381_g1_msm(); GUARD_END
+}
+void tachyon_bls12_381_g1_destroy_msm(tachyon_bls12_381_g1_msm_ptr ptr) { delete ptr; }
+tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_point2_msm(tachyon_bls12_381_g1_msm_ptr ptr,
+                                                               const tachyon_bls12_381_g1_point2* bases,
+                                                               const tachyon_bls12_381_fr* scalars, size_t size) {
+  GUARD_BEGIN return do_msm<Bls381G1, tachyon_bls12_381_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_affine_msm(tachyon_bls12_381_g1_msm_ptr ptr,
+                                                               const tachyon_bls12_381_g1_affine* bases,
+                                                               const tachyon_bls12_381_fr* scalars, size_t size) {
+  GUARD_BEGIN return do_msm<Bls381G1, tachyon_bls12_381_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+tachyon_bls12_381_g1_msm_gpu_ptr tachyon_bls12_381_g1_create_msm_gpu(uint8_t degree) {
+  (void)degree;
+  GUARD_BEGIN return new tachyon_bls12_381_g1_msm_gpu(); GUARD_END
+}
+void tachyon_bls12_381_g1_destroy_msm_gpu(tachyon_bls12_381_g1_msm_gpu_ptr ptr) { delete ptr; }
+tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_point2_msm_gpu(tachyon_bls12_381_g1_msm_gpu_ptr ptr,
+                                                                   const tachyon_bls12_381_g1_point2* bases,
+                                                                   const tachyon_bls12_381_fr* scalars,
+                                                                   size_t size) {
+  GUARD_BEGIN return do_msm<Bls381G1, tachyon_bls12_381_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_affine_msm_gpu(tachyon_bls12_381_g1_msm_gpu_ptr ptr,
+                                                                   const tachyon_bls12_381_g1_affine* bases,
+                                                                   const tachyon_bls12_381_fr* scalars,
+                                                                   size_t size) {
+  GUARD_BEGIN return do_msm<Bls381G1, tachyon_bls12_381_g1_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+
+// ---- G2 (extension) ----
+tachyon_bn254_g2_msm_gpu_ptr tachyon_bn254_g2_create_msm_gpu(uint8_t degree) {
+  (void)degree;
+  GUARD_BEGIN return new tachyon_bn254_g2_msm_gpu(); GUARD_END
+}
+void tachyon_bn254_g2_destroy_msm_gpu(tachyon_bn254_g2_msm_gpu_ptr ptr) { delete ptr; }
+tachyon_bn254_g2_jacobian* tachyon_bn254_g2_affine_msm_gpu(tachyon_bn254_g2_msm_gpu_ptr ptr,
+                                                           const tachyon_bn254_g2_affine* bases,
+                                                           const tachyon_bn254_fr* scalars, size_t size) {
+  GUARD_BEGIN return do_msm<Bn254G2, tachyon_bn254_g2_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+tachyon_bls12_381_g2_msm_gpu_ptr tachyon_bls12_381_g2_create_msm_gpu(uint8_t degree) {
+  (void)degree;
+  GUARD_BEGIN return new tachyon_bls12_381_g2_msm_gpu(); GUARD_END
+}
+void tachyon_bls12_381_g2_destroy_msm_gpu(tachyon_bls12_381_g2_msm_gpu_ptr ptr) { delete ptr; }
+tachyon_bls12_381_g2_jacobian* tachyon_bls12_381_g2_affine_msm_gpu(tachyon_bls12_381_g2_msm_gpu_ptr ptr,
+                                                                   const tachyon_bls12_381_g2_affine* bases,
+                                                                   const tachyon_bls12_381_fr* scalars,
+                                                                   size_t size) {
+  GUARD_BEGIN return do_msm<Bls381G2, tachyon_bls12_381_g2_jacobian>(ptr, bases, scalars, size); GUARD_END
+}
+
+// ---- curve-generic extensions ----
+#define CURVE_DISPATCH(curve, CALL)                               \
+  switch (curve) {                                                \
+    case 0: { using C = Bn254G1; CALL; } break;                   \
+    case 1: { using C = Bn254G2; CALL; } break;                   \
+    case 2: { using C = Bls381G1; CALL; } break;                  \
+    case 3: { using C = Bls381G2; CALL; } break;                  \
+    default: throw std::runtime_error("unknown curve id");        \
+  }
+
+void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const void* bases, const void* scalars, size_t size,
+                                   void* out_affine) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, msm_affine_out<C>(ctx, bases, scalars, size, out_affine)) GUARD_END
+}
+void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_force_window_bits(c)) GUARD_END
+}
+void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_profile(on != 0)) GUARD_END
+}
+void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out6) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    const msm::MsmTimings& t = static_cast<const MsmCtx<C>*>(ctx)->impl.timings();
+    out6[0] = t.h2d; out6[1] = t.recode; out6[2] = t.sort; out6[3] = t.acc; out6[4] = t.reduce; out6[5] = t.total;
+  }) GUARD_END
+}
+void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    msm::MsmPlan p = msm::MsmPlan::make(size, C::Fr::Config::kModulusBits);
+    *c = p.c;
+    *windows = p.windows;
+  }) GUARD_END
+}
+void tachyon_mi355x_affine_sum(int curve, const void* points, size_t count, void* out_affine) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, affine_sum<C>(points, count, out_affine)) GUARD_END
+}
+void tachyon_mi355x_jacobian_to_affine(int curve, const void* jacobian, void* out_affine) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, jac_to_affine<C>(jacobian, out_affine)) GUARD_END
+}
+
+void tachyon_mi355x_gen_scalars(int field, uint64_t seed, size_t start, size_t n, void* d_out, void* stream) {
+  GUARD_BEGIN util::gen_scalars(field, seed, start, n, d_out, static_cast<hipStream_t>(stream)); GUARD_END
+}
+void tachyon_mi355x_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* d_out, void* stream) {
+  GUARD_BEGIN util::gen_bases(curve, seed, n, chunk, d_out, static_cast<hipStream_t>(stream)); GUARD_END
+}
+void tachyon_mi355x_field_op(int field, int op, const void* a, const void* b, void* out, size_t count) {
+  GUARD_BEGIN util::field_op(field, op, a, b, out, count); GUARD_END
+}
+void tachyon_mi355x_ec_op(int curve, int op, const void* a, const void* b, void* out, size_t count) {
+  GUARD_BEGIN util::ec_op(curve, op, a, b, out, count); GUARD_END
+}
+
+const char* tachyon_mi355x_version(void) { return "tachyon_mi355x 0.1 (gfx950)"; }
+int tachyon_mi355x_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ---- univariate evaluation domain over BN254 Fr ----
+tachyon_bn254_univariate_evaluation_domain* tachyon_bn254_univariate_evaluation_domain_create(size_t num_coeffs) {
+  GUARD_BEGIN
+  auto* d = new tachyon_bn254_univariate_evaluation_domain();
+  d->impl.reset(new ntt::NttDomain<Bn254Fr>(num_coeffs));
+  return d;
+  GUARD_END
+}
+void tachyon_bn254_univariate_evaluation_domain_destroy(tachyon_bn254_univariate_evaluation_domain* domain) {
+  delete domain;
+}
+// Domain::Zero<Evals>() = size() zeros (univariate_evaluations.h:251-255)
+tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_empty_evals(
+    const tachyon_bn254_univariate_evaluation_domain* domain) {
+  GUARD_BEGIN
+  auto* e = new tachyon_bn254_univariate_evaluations();
+  e->v.assign(domain->impl->size(), FrC{});
+  return e;
+  GUARD_END
+}
+tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_empty_poly(
+    const tachyon_bn254_univariate_evaluation_domain* domain) {
+  GUARD_BEGIN
+  auto* p = new tachyon_bn254_univariate_dense_polynomial();
+  p->v.assign(domain->impl->size(), FrC{});
+  return p;
+  GUARD_END
+}
+
+}  // extern "C"
+
+namespace {
+// UnivariateEvaluationDomain::FFT (univariate_evaluation_domain.h:141-182):
+// empty poly -> empty evals; otherwise n evaluations.
+std::vector<FrC> do_fft(const Domain* d, const std::vector<FrC>& coeffs) {
+  std::vector<FrC> out;
+  if (coeffs.empty()) return out;
+  out.resize(d->impl->size());
+  d->impl->forward_host(reinterpret_cast<const Bn254Fr*>(coeffs.data()), coeffs.size(),
+                        reinterpret_cast<Bn254Fr*>(out.data()));
+  return out;
+}
+// IFFT + RemoveHighDegreeZeros (radix2_evaluation_domain.h:218-223)
+std::vector<FrC> do_ifft(const Domain* d, const std::vector<FrC>& evals) {
+  std::vector<FrC> out;
+  if (evals.empty()) return out;
+  out.resize(d->impl->size());
+  d->impl->inverse_host(reinterpret_cast<const Bn254Fr*>(evals.data()), evals.size(),
+                        reinterpret_cast<Bn254Fr*>(out.data()));
+  size_t len = out.size();
+  while (len > 0) {
+    const FrC& x = out[len - 1];
+    if (x.limbs[0] | x.limbs[1] | x.limbs[2] | x.limbs[3]) break;
+    --len;
+  }
+  out.resize(len);
+  return out;
+}
+}  // namespace
+
+extern "C" {
+
+tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_fft(
+    const tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_univariate_dense_polynomial* poly) {
+  GUARD_BEGIN
+  auto* e = new tachyon_bn254_univariate_evaluations();
+  e->v = do_fft(domain, poly->v);
+  return e;
+  GUARD_END
+}
+tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_fft_inplace(
+    const tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_univariate_dense_polynomial* poly) {
+  GUARD_BEGIN
+  auto* e = new tachyon_bn254_univariate_evaluations();
+  std::vector<FrC> in = std::move(poly->v);  // moved-from, as FFT(DensePoly&&)
+  poly->v.clear();
+  e->v = do_fft(domain, in);
+  return e;
+  GUARD_END
+}
+tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_ifft(
+    const tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_univariate_evaluations* evals) {
+  GUARD_BEGIN
+  auto* p = new tachyon_bn254_univariate_dense_polynomial();
+  p->v = do_ifft(domain, evals->v);
+  return p;
+  GUARD_END
+}
+tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_ifft_inplace(
+    const tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_univariate_evaluations* evals) {
+  GUARD_BEGIN
+  auto* p = new tachyon_bn254_univariate_dense_polynomial();
+  std::vector<FrC> in = std::move(evals->v);
+  evals->v.clear();
+  p->v = do_ifft(domain, in);
+  return p;
+  GUARD_END
+}
+
+tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluations_create(void) {
+  return new tachyon_bn254_univariate_evaluations();
+}
+tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluations_clone(
+    const tachyon_bn254_univariate_evaluations* evals) {
+  auto* e = new tachyon_bn254_univariate_evaluations();
+  e->v = evals->v;
+  return e;
+}
+void tachyon_bn254_univariate_evaluations_destroy(tachyon_bn254_univariate_evaluations* evals) { delete evals; }
+size_t tachyon_bn254_univariate_evaluations_len(const tachyon_bn254_univariate_evaluations* evals) {
+  return evals->v.size();
+}
+void tachyon_bn254_univariate_evaluations_set_value(tachyon_bn254_univariate_evaluations* evals, size_t i,
+                                                    const tachyon_bn254_fr* value) {
+  GUARD_BEGIN evals->v.at(i) = *value; GUARD_END  // .at() as in the reference: OOB aborts
+}
+tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_dense_polynomial_create(void) {
+  return new tachyon_bn254_univariate_dense_polynomial();
+}
+tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_dense_polynomial_clone(
+    const tachyon_bn254_univariate_dense_polynomial* poly) {
+  auto* p = new tachyon_bn254_univariate_dense_polynomial();
+  p->v = poly->v;
+  return p;
+}
+void tachyon_bn254_univariate_dense_polynomial_destroy(tachyon_bn254_univariate_dense_polynomial* poly) {
+  delete poly;
+}
+
+void tachyon_mi355x_bn254_univariate_evaluations_get_value(const tachyon_bn254_univariate_evaluations* evals,
+                                                           size_t i, tachyon_bn254_fr* value) {
+  GUARD_BEGIN *value = evals->v.at(i); GUARD_END
+}
+tachyon_bn254_fr* tachyon_mi355x_bn254_univariate_evaluations_data(tachyon_bn254_univariate_evaluations* evals) {
+  return evals->v.data();
+}
+void tachyon_mi355x_bn254_univariate_evaluations_resize(tachyon_bn254_univariate_evaluations* evals, size_t len) {
+  GUARD_BEGIN evals->v.resize(len, FrC{}); GUARD_END
+}
+size_t tachyon_mi355x_bn254_univariate_dense_polynomial_len(const tachyon_bn254_univariate_dense_polynomial* poly) {
+  return poly->v.size();
+}
+void tachyon_mi355x_bn254_univariate_dense_polynomial_resize(tachyon_bn254_univariate_dense_polynomial* poly,
+                                                             size_t len) {
+  GUARD_BEGIN poly->v.resize(len, FrC{}); GUARD_END
+}
+void tachyon_mi355x_bn254_univariate_dense_polynomial_set_value(tachyon_bn254_univariate_dense_polynomial* poly,
+                                                                size_t i, const tachyon_bn254_fr* value) {
+  GUARD_BEGIN poly->v.at(i) = *value; GUARD_END
+}
+void tachyon_mi355x_bn254_univariate_dense_polynomial_get_value(
+    const tachyon_bn254_univariate_dense_polynomial* poly, size_t i, tachyon_bn254_fr* value) {
+  GUARD_BEGIN *value = poly->v.at(i); GUARD_END
+}
+tachyon_bn254_fr* tachyon_mi355x_bn254_univariate_dense_polynomial_data(tachyon_bn254_univariate_dense_polynomial* poly) {
+  return poly->v.data();
+}
+
+size_t tachyon_mi355x_bn254_univariate_evaluation_domain_size(const tachyon_bn254_univariate_evaluation_domain* d) {
+  return d->impl->size();
+}
+void tachyon_mi355x_bn254_univariate_evaluation_domain_group_gen(const tachyon_bn254_univariate_evaluation_domain* d,
+                                                                 tachyon_bn254_fr* out) {
+  memcpy(out, &d->impl->group_gen(), sizeof(*out));
+}
+void tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset(tachyon_bn254_univariate_evaluation_domain* d,
+                                                                  const tachyon_bn254_fr* offset) {
+  GUARD_BEGIN
+  Bn254Fr h;
+  memcpy(&h, offset, sizeof(h));
+  d->impl->set_offset(h);
+  GUARD_END
+}
+void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(tachyon_bn254_univariate_evaluation_domain* d,
+                                                                        tachyon_bn254_fr* d_data, int inverse) {
+  GUARD_BEGIN
+  if (inverse) d->impl->inverse_device(reinterpret_cast<Bn254Fr*>(d_data));
+  else d->impl->forward_device(reinterpret_cast<Bn254Fr*>(d_data));
+  GUARD_END
+}
+void* tachyon_mi355x_bn254_univariate_evaluation_domain_stream(tachyon_bn254_univariate_evaluation_domain* d) {
+  return d->impl->stream();
+}
+void tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(tachyon_bn254_univariate_evaluation_domain* d,
+                                                                   int on) {
+  d->impl->set_profile(on != 0);
+}
+int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(const tachyon_bn254_univariate_evaluation_domain* d,
+                                                                   float* total_ms, float* pass_ms, int max_passes) {
+  const auto& t = d->impl->timings();
+  if (total_ms) *total_ms = t.total;
+  int np = (int)t.passes.size();
+  for (int i = 0; i < np && i < max_passes; ++i) pass_ms[i] = t.passes[i];
+  return np;
+}
+
+}  // extern "C"

@@ -1,0 +1,216 @@
+// Montgomery prime-field arithmetic for CDNA4 (gfx950), 32-bit limbs.
+//
+// Same values as the reference's PrimeField (tachyon/math/finite_fields/
+// prime_field_fallback.h): Montgomery form with R = 2^(64*N64), canonical in
+// [0, p), little-endian limbs -- so a tachyon_bn254_fq {uint64_t limbs[4]} is
+// bit-identical to an Fp<bn254_fq> {uint32_t v[8]}.
+//
+// Multiplication is the CIOS "no-carry" variant (the reference's DoFastMul,
+// prime_field_fallback.h:331-355) restated on 32-bit limbs, because gfx950 has
+// no 64x64 multiplier: every partial product is one v_mad_u64_u32
+// (32x32+64 -> 64, measured at ~1/2 of the full VALU rate on MI355X), carries
+// ride v_add_co/v_addc chains.  All moduli here leave the top limb < 2^31 - 1,
+// which is the condition for the no-carry trick.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "constants.h"
+
+#define TA_HD __host__ __device__ __forceinline__
+
+namespace tachyon_amd {
+
+TA_HD uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  uint64_t s = (uint64_t)a + b + cin;
+  *cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+
+TA_HD uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  uint64_t d = (uint64_t)a - b - bin;
+  *bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+}
+
+template <class Cfg>
+struct Fp {
+  static constexpr int N = Cfg::N32;
+  using Config = Cfg;
+  uint32_t v[N];
+
+  TA_HD static Fp zero() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = 0;
+    return r;
+  }
+  TA_HD static Fp one() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = Cfg::kR32[i];
+    return r;
+  }
+  TA_HD static Fp modulus() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = Cfg::kP32[i];
+    return r;
+  }
+  TA_HD bool is_zero() const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc |= v[i];
+    return acc == 0;
+  }
+  TA_HD bool operator==(const Fp& o) const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc |= v[i] ^ o.v[i];
+    return acc == 0;
+  }
+  TA_HD bool operator!=(const Fp& o) const { return !(*this == o); }
+  TA_HD bool is_one() const { return *this == one(); }
+
+  // r = a - p if a >= p else a   (a < 2p, no overflow past N limbs)
+  TA_HD static void reduce_once(uint32_t* a) {
+    uint32_t t[N];
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = subb(a[i], Cfg::kP32[i], br, &br);
+    // br == 1  <=>  a < p  -> keep a
+#pragma unroll
+    for (int i = 0; i < N; ++i) a[i] = br ? a[i] : t[i];
+  }
+
+  // prime_field_fallback.h:199-214 (Add + Clamp)
+  TA_HD Fp operator+(const Fp& o) const {
+    Fp r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = addc(v[i], o.v[i], c, &c);
+    reduce_once(r.v);  // spare top bit: no carry out of the top limb
+    return r;
+  }
+  TA_HD Fp dbl() const { return *this + *this; }
+
+  // prime_field_fallback.h:234-251 (Sub: add p back on borrow)
+  TA_HD Fp operator-(const Fp& o) const {
+    Fp r;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = subb(v[i], o.v[i], br, &br);
+    uint32_t mask = 0u - br;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = addc(r.v[i], Cfg::kP32[i] & mask, c, &c);
+    return r;
+  }
+  TA_HD Fp operator-() const { return zero() - *this; }
+
+  // CIOS no-carry Montgomery product (DoFastMul, prime_field_fallback.h:331-355).
+  TA_HD Fp operator*(const Fp& b) const {
+    uint32_t t[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint32_t bi = b.v[i];
+      uint64_t s = (uint64_t)v[0] * bi + t[0];
+      t[0] = (uint32_t)s;
+      uint32_t hi1 = (uint32_t)(s >> 32);
+      const uint32_t k = t[0] * Cfg::kInv32;
+      uint64_t s2 = (uint64_t)k * Cfg::kP32[0] + t[0];
+      uint32_t hi2 = (uint32_t)(s2 >> 32);
+#pragma unroll
+      for (int j = 1; j < N; ++j) {
+        s = (uint64_t)v[j] * bi + ((uint64_t)t[j] + hi1);
+        t[j] = (uint32_t)s;
+        hi1 = (uint32_t)(s >> 32);
+        s2 = (uint64_t)k * Cfg::kP32[j] + ((uint64_t)t[j] + hi2);
+        t[j - 1] = (uint32_t)s2;
+        hi2 = (uint32_t)(s2 >> 32);
+      }
+      t[N - 1] = hi1 + hi2;
+    }
+    Fp r;
+    reduce_once(t);
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = t[i];
+    return r;
+  }
+  TA_HD Fp sqr() const { return (*this) * (*this); }
+
+  // Montgomery -> canonical (ToBigInt, prime_field_fallback.h:166-169).
+  TA_HD Fp from_mont() const {
+    Fp one_plain = zero();
+    one_plain.v[0] = 1;
+    return (*this) * one_plain;
+  }
+  // canonical (< p) -> Montgomery
+  TA_HD Fp to_mont() const {
+    Fp r2;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r2.v[i] = Cfg::kR232[i];
+    return (*this) * r2;
+  }
+
+  TA_HD Fp pow(const uint32_t* e, int nlimbs) const {
+    Fp r = one();
+    for (int i = nlimbs - 1; i >= 0; --i)
+      for (int bit = 31; bit >= 0; --bit) {
+        r = r.sqr();
+        if ((e[i] >> bit) & 1) r = r * (*this);
+      }
+    return r;
+  }
+  // Fermat inverse (same canonical value as the reference's BY inverter).
+  TA_HD Fp inverse() const {
+    uint32_t e[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) e[i] = Cfg::kP32[i];
+    e[0] -= 2;
+    return pow(e, N);
+  }
+};
+
+// Fq2 = Fq[u]/(u^2 + 1)  (non-residue -1 for BN254 and BLS12-381;
+// quadratic_extension_field.h:315-360 Karatsuba).
+template <class F>
+struct Fp2 {
+  using Base = F;
+  F c0, c1;
+  TA_HD static Fp2 zero() { return {F::zero(), F::zero()}; }
+  TA_HD static Fp2 one() { return {F::one(), F::zero()}; }
+  TA_HD bool is_zero() const { return c0.is_zero() && c1.is_zero(); }
+  TA_HD bool is_one() const { return c0.is_one() && c1.is_zero(); }
+  TA_HD bool operator==(const Fp2& o) const { return c0 == o.c0 && c1 == o.c1; }
+  TA_HD bool operator!=(const Fp2& o) const { return !(*this == o); }
+  TA_HD Fp2 operator+(const Fp2& o) const { return {c0 + o.c0, c1 + o.c1}; }
+  TA_HD Fp2 operator-(const Fp2& o) const { return {c0 - o.c0, c1 - o.c1}; }
+  TA_HD Fp2 operator-() const { return {-c0, -c1}; }
+  TA_HD Fp2 dbl() const { return {c0.dbl(), c1.dbl()}; }
+  TA_HD Fp2 operator*(const Fp2& o) const {
+    F v0 = c0 * o.c0;
+    F v1 = c1 * o.c1;
+    F m = (c0 + c1) * (o.c0 + o.c1);
+    return {v0 - v1, m - v0 - v1};
+  }
+  TA_HD Fp2 sqr() const {
+    F ab = c0 * c1;
+    return {(c0 + c1) * (c0 - c1), ab.dbl()};
+  }
+  TA_HD Fp2 inverse() const {
+    F t = (c0.sqr() + c1.sqr()).inverse();
+    return {c0 * t, -(c1 * t)};
+  }
+};
+
+using Bn254Fq = Fp<consts::bn254_fq>;
+using Bn254Fr = Fp<consts::bn254_fr>;
+using Bls381Fq = Fp<consts::bls12_381_fq>;
+using Bls381Fr = Fp<consts::bls12_381_fr>;
+using Bn254Fq2 = Fp2<Bn254Fq>;
+using Bls381Fq2 = Fp2<Bls381Fq>;
+
+}  // namespace tachyon_amd

@@ -1,0 +1,91 @@
+// Variable-base MSM on MI355X: host driver interface.
+//
+// Drop-in for tachyon::math::VariableBaseMSMGpu<Point> (variable_base_msm_gpu.h:11-30)
+// whose GPU work the reference delegates to icicle (icicle_msm.h:19-100).
+// Pipeline (one HIP stream, no host sync until the final window sums):
+//   recode   scalars (Montgomery -> canonical -> signed c-bit digits), one key
+//            per (window, point): |digit| and point index | sign<<31
+//   sort     per-window radix sort of the (bucket, point) pairs (rocPRIM)
+//   bounds   bucket [start, end) from the sorted keys
+//   acc      bucket sums as XYZZ, split into chunks of <= K entries so that a
+//            skewed bucket (NonUniform test set) is spread over many threads
+//   levels   tree-reduce per-bucket chunk partials (K2-ary) until one per bucket
+//   window   sum_b b * B_b per window via per-segment running sums
+//   host     Horner over windows (c doublings each) -> one point
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "../common/hip_util.h"
+#include "../ec/point.h"
+
+namespace tachyon_amd::msm {
+
+struct MsmPlan {
+  unsigned c = 0;        // window bits
+  unsigned windows = 0;  // W
+  unsigned buckets = 0;  // B = 2^(c-1) buckets per window (|digit| in [1, B])
+  unsigned K = 0;        // entries per accumulation chunk
+  unsigned K2 = 16;      // fan-in of the partial-reduction levels
+  unsigned levels = 0;   // number of K2 levels
+  unsigned seg = 0;      // buckets per running-sum segment
+  static MsmPlan make(size_t n, unsigned scalar_bits, unsigned force_c = 0);
+};
+
+// Per-phase device timings of the last run (ms), filled when profiling is on.
+struct MsmTimings {
+  float h2d = 0, recode = 0, sort = 0, acc = 0, reduce = 0, total = 0;
+};
+
+template <class Curve>
+class MsmGpu {
+ public:
+  using F = typename Curve::F;
+  using Fr = typename Curve::Fr;
+  using Point = XYZZ<F>;
+  using Aff = Affine<F>;
+
+  explicit MsmGpu(hipStream_t stream = nullptr);
+  ~MsmGpu();
+  MsmGpu(const MsmGpu&) = delete;
+  MsmGpu& operator=(const MsmGpu&) = delete;
+
+  // bases: n affine points (Montgomery, (0,0) = identity); scalars: n Fr in
+  // Montgomery form.  Either may live on the host or on the current device.
+  // Returns the MSM as an XYZZ point (host memory).
+  Point run(const void* bases, const void* scalars, size_t n);
+
+  // Window sums only (for multi-GPU: each rank ships W points) -- device work
+  // identical to run(); `out` gets plan.windows points.
+  void run_windows(const void* bases, const void* scalars, size_t n, std::vector<Point>* out,
+                   MsmPlan* plan_out);
+
+  static Point combine_windows(const std::vector<Point>& window_sums, unsigned c);
+
+  void set_force_window_bits(unsigned c) { force_c_ = c; }
+  void set_profile(bool on) { profile_ = on; }
+  const MsmTimings& timings() const { return timings_; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
+
+  hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
+  bool profile_ = false;
+  unsigned force_c_ = 0;
+  MsmTimings timings_;
+  DeviceBuffer bases_, scalars_, keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_;
+  DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_;
+  hipEvent_t ev_[8] = {};
+};
+
+extern template class MsmGpu<Bn254G1>;
+extern template class MsmGpu<Bn254G2>;
+extern template class MsmGpu<Bls381G1>;
+extern template class MsmGpu<Bls381G2>;
+
+}  // namespace tachyon_amd::msm

@@ -1,0 +1,96 @@
+// Radix-2 NTT over a two-adic prime field on MI355X: host driver interface.
+//
+// Drop-in for the GPU hook of tachyon::math::UnivariateEvaluationDomain
+// (set_icicle / IcicleNTT::Run, univariate_evaluation_domain.h:99,169-178,
+// icicle_ntt_bn254.cc:68-101): natural-order input and output, Montgomery form
+// end to end, optional coset offset h (GetCoset, univariate_evaluation_domain.h:102-117).
+//
+//   forward:  e_i = sum_j c_j (h w^i)^j
+//   inverse:  c_j = n^-1 h^-j sum_i e_i w^-ij
+//
+// Both run the decimation-in-frequency network (the reference's
+// ButterflyFnInOut form, univariate_evaluation_domain.h:518-524) in passes of
+// up to 8 stages held in LDS, with the bit-reversal permutation and the
+// n^-1 / coset scaling fused into the last pass.  Results are canonical field
+// elements, so they equal the reference's DIT (FFT) / DIF (IFFT) CPU output
+// byte for byte.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <vector>
+
+#include "../common/hip_util.h"
+#include "../field/ff.h"
+
+namespace tachyon_amd::ntt {
+
+struct NttTimings {
+  float total = 0;
+  std::vector<float> passes;
+};
+
+template <class Fr>
+class NttDomain {
+ public:
+  // size = bit_ceil(num_coeffs) (Radix2EvaluationDomain::Create, radix2_evaluation_domain.h:83-89)
+  explicit NttDomain(size_t num_coeffs, hipStream_t stream = nullptr);
+  ~NttDomain();
+  NttDomain(const NttDomain&) = delete;
+  NttDomain& operator=(const NttDomain&) = delete;
+
+  size_t size() const { return n_; }
+  uint32_t log_size() const { return log_n_; }
+  const Fr& group_gen() const { return omega_; }
+  const Fr& group_gen_inv() const { return omega_inv_; }
+  const Fr& size_inv() const { return size_inv_; }
+  hipStream_t stream() const { return stream_; }
+
+  // Coset offset h (Montgomery).  h == 1 restores the plain domain.
+  void set_offset(const Fr& h);
+  const Fr& offset() const { return offset_; }
+
+  // In-place transform of n device-resident elements (d_data), enqueued on
+  // stream(); scratch is owned by the domain.  Not synchronised.
+  void forward_device(Fr* d_data);
+  void inverse_device(Fr* d_data);
+
+  // Host vector in/out: `len` <= n input elements, zero-padded to n; writes n
+  // outputs to `out` (may alias `in`).  Synchronises.
+  void forward_host(const Fr* in, size_t len, Fr* out);
+  void inverse_host(const Fr* in, size_t len, Fr* out);
+
+  void set_profile(bool on) { profile_ = on; }
+  const NttTimings& timings() const { return timings_; }
+
+  struct Pass {
+    uint32_t s0, k, log_m;
+    bool final_pass;
+  };
+  const std::vector<Pass>& plan() const { return plan_; }
+
+ private:
+  void run(Fr* d_data, bool inverse);
+  void build_twiddles();
+  void build_powers(const Fr& base, const Fr& scale, Fr* d_lo, Fr* d_hi);
+
+  size_t n_ = 0;
+  uint32_t log_n_ = 0;
+  Fr omega_, omega_inv_, size_inv_, offset_, offset_inv_;
+  bool has_offset_ = false;
+  hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
+  bool profile_ = false;
+  std::vector<Pass> plan_;
+  uint32_t pow_bits_ = 0;  // split point of the two-level power tables
+  DeviceBuffer tw_fwd_, tw_inv_, scratch_, io_;
+  DeviceBuffer coset_lo_, coset_hi_, icoset_lo_, icoset_hi_;
+  NttTimings timings_;
+  std::vector<hipEvent_t> ev_;
+};
+
+extern template class NttDomain<Bn254Fr>;
+extern template class NttDomain<Bls381Fr>;
+
+}  // namespace tachyon_amd::ntt

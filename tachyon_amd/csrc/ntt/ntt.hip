@@ -1,0 +1,363 @@
+// Radix-2 NTT kernels for MI355X (gfx950) and the NttDomain host driver.
+// Reference semantics: radix2_evaluation_domain.h:213-333,
+// univariate_evaluation_domain.h:141-232,464-489,518-566, radix2_twiddle_cache.h:57-121.
+#include "ntt.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace tachyon_amd::ntt {
+
+namespace {
+
+constexpr unsigned kBlock = 256;
+constexpr uint32_t kMaxPassStages = 8;
+constexpr uint32_t kMaxLdsElems = 2048;  // 64 KiB of 32-byte elements: 2 workgroups / CU
+
+enum : uint32_t { kLoadCoset = 1, kStoreScale = 2, kStoreCoset = 4 };
+
+template <class Fr>
+struct PassArgs {
+  uint32_t L, s0, k, log_m, final_pass, mode, pow_bits;
+  const Fr* load_lo;
+  const Fr* load_hi;
+  const Fr* store_lo;
+  const Fr* store_hi;
+  Fr scale;
+};
+
+__device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
+  return bits == 0 ? 0u : (__brev(x) >> (32 - bits));
+}
+
+// One pass of k DIF stages (s0 .. s0+k-1) over M sets of 2^k elements held in
+// LDS.  Non-final passes are in place (each workgroup reads and writes the
+// same positions); the final pass (s0 + k == L) writes natural order through
+// the bit-reversal permutation, M bit-reversed-consecutive sets per workgroup
+// so every store row is M contiguous elements.
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__ in, Fr* __restrict__ out,
+                                                          const Fr* __restrict__ tw, PassArgs<Fr> a) {
+  extern __shared__ uint4 smem_raw[];
+  Fr* lds = reinterpret_cast<Fr*>(smem_raw);
+  const uint32_t L = a.L, k = a.k, log_m = a.log_m;
+  const uint32_t M = 1u << log_m;
+  const uint32_t elems = M << k;
+  const uint32_t n = 1u << L;
+  const uint32_t b = blockIdx.x;
+
+  // index(mid, m) of element m of the block's set, position mid in the set
+  uint32_t hi_shift = L - a.s0;            // set stride in the hi dimension
+  uint32_t mid_shift = L - a.s0 - k;       // stride between set members
+  uint32_t hi = 0, lo_base = 0, r0 = 0;
+  if (!a.final_pass) {
+    uint32_t lo_blocks = (1u << mid_shift) >> log_m;
+    hi = b / lo_blocks;
+    lo_base = (b - hi * lo_blocks) << log_m;
+  } else {
+    r0 = b << log_m;
+  }
+  auto index = [&](uint32_t mid, uint32_t m) -> uint32_t {
+    if (!a.final_pass) return (hi << hi_shift) + (mid << mid_shift) + lo_base + m;
+    uint32_t h = bitrev(r0 + m, L - k);
+    return (h << k) + mid;
+  };
+
+  // ---- load ----
+  for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
+    uint32_t mid = e >> log_m, m = e & (M - 1);
+    uint32_t i = index(mid, m);
+    Fr v = in[i];
+    if (a.mode & kLoadCoset) v = v * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
+    lds[e] = v;
+  }
+  __syncthreads();
+
+  // ---- k butterfly stages ----
+  for (uint32_t t = 0; t < k; ++t) {
+    const uint32_t s = a.s0 + t;
+    const uint32_t half_log = k - 1 - t;
+    const uint32_t half = 1u << half_log;
+    const uint32_t gap = 1u << (L - s - 1);
+    const Fr* tws = tw + (n - (n >> s));
+    for (uint32_t u = threadIdx.x; u < (elems >> 1); u += kBlock) {
+      uint32_t m = u & (M - 1);
+      uint32_t r = u >> log_m;
+      uint32_t blk = r >> half_log, off = r & (half - 1);
+      uint32_t mid_lo = (blk << (half_log + 1)) + off;
+      uint32_t mid_hi = mid_lo + half;
+      uint32_t i_lo = index(mid_lo, m);
+      Fr w = tws[i_lo & (gap - 1)];
+      Fr x = lds[(mid_lo << log_m) + m];
+      Fr y = lds[(mid_hi << log_m) + m];
+      // ButterflyFnInOut: lo = lo + hi; hi = (lo - hi) * w
+      lds[(mid_lo << log_m) + m] = x + y;
+      lds[(mid_hi << log_m) + m] = (x - y) * w;
+    }
+    __syncthreads();
+  }
+
+  // ---- store ----
+  if (!a.final_pass) {
+    for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
+      uint32_t mid = e >> log_m, m = e & (M - 1);
+      out[index(mid, m)] = lds[e];
+    }
+  } else {
+    for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
+      uint32_t q = e >> log_m, m = e & (M - 1);
+      uint32_t mid = bitrev(q, k);
+      Fr v = lds[(mid << log_m) + m];
+      uint32_t o = (q << (L - k)) + r0 + m;
+      if (a.mode & kStoreCoset) v = v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits]);
+      else if (a.mode & kStoreScale) v = v * a.scale;
+      out[o] = v;
+    }
+  }
+}
+
+// T0[j] = w^j for j < n/2 from two small power tables: lo[j & mask] * hi[j >> bits]
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void twiddle_base_kernel(Fr* __restrict__ t0, uint32_t count,
+                                                              const Fr* __restrict__ lo, const Fr* __restrict__ hi,
+                                                              uint32_t bits) {
+  uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= count) return;
+  t0[j] = lo[j & ((1u << bits) - 1)] * hi[j >> bits];
+}
+
+// T_s[j] = T_0[j << s]  (the strided sub-sampling of radix2_twiddle_cache.h:105-117)
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void twiddle_stage_kernel(Fr* __restrict__ ts, const Fr* __restrict__ t0,
+                                                               uint32_t count, uint32_t s) {
+  uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= count) return;
+  ts[j] = t0[(size_t)j << s];
+}
+
+template <class Fr>
+Fr fr_from_u64(uint64_t v) {
+  Fr x = Fr::zero();
+  x.v[0] = (uint32_t)v;
+  x.v[1] = (uint32_t)(v >> 32);
+  return x.to_mont();
+}
+
+template <class Fr>
+Fr two_adic_root() {
+  Fr r;
+  const uint64_t* src = Fr::Config::kTwoAdicRootMont64;
+  for (int i = 0; i < Fr::N / 2; ++i) {
+    r.v[2 * i] = (uint32_t)src[i];
+    r.v[2 * i + 1] = (uint32_t)(src[i] >> 32);
+  }
+  return r;
+}
+
+template <class Fr>
+std::vector<Fr> host_powers(const Fr& base, const Fr& scale, size_t count) {
+  std::vector<Fr> out(count);
+  Fr p = scale;
+  for (size_t i = 0; i < count; ++i) {
+    out[i] = p;
+    p = p * base;
+  }
+  return out;
+}
+
+}  // namespace
+
+template <class Fr>
+NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream) {
+  require_gpu();
+  log_n_ = 0;
+  while ((size_t(1) << log_n_) < std::max<size_t>(num_coeffs, 1)) ++log_n_;
+  if (log_n_ > (uint32_t)Fr::Config::kTwoAdicity || log_n_ > 30)
+    throw std::runtime_error("tachyon_mi355x: NTT size exceeds the field's two-adicity");
+  n_ = size_t(1) << log_n_;
+  if (!stream_) {
+    TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    own_stream_ = true;
+  }
+  // w_n = root^(2^(s - log n))  (PrimeFieldBase::GetRootOfUnity, prime_field_base.h:90-130)
+  omega_ = two_adic_root<Fr>();
+  for (uint32_t i = log_n_; i < (uint32_t)Fr::Config::kTwoAdicity; ++i) omega_ = omega_.sqr();
+  omega_inv_ = omega_.inverse();
+  size_inv_ = fr_from_u64<Fr>(n_).inverse();
+  offset_ = Fr::one();
+  offset_inv_ = Fr::one();
+
+  // pass plan: ceil(L / 8) passes, stages split evenly
+  if (log_n_ > 0) {
+    uint32_t P = (log_n_ + kMaxPassStages - 1) / kMaxPassStages;
+    uint32_t s0 = 0;
+    for (uint32_t p = 0; p < P; ++p) {
+      uint32_t k = (log_n_ - s0) / (P - p);
+      Pass ps;
+      ps.s0 = s0;
+      ps.k = k;
+      ps.final_pass = (s0 + k == log_n_);
+      uint32_t avail = ps.final_pass ? (log_n_ - k) : (log_n_ - s0 - k);  // log2 of sets available
+      uint32_t log_m = 0;
+      while (log_m < avail && ((2u << log_m) << k) <= kMaxLdsElems) ++log_m;
+      ps.log_m = log_m;
+      plan_.push_back(ps);
+      s0 += k;
+    }
+  }
+  pow_bits_ = (log_n_ + 1) / 2;
+  ev_.resize(plan_.size() + 1);
+  for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
+  build_twiddles();
+}
+
+template <class Fr>
+NttDomain<Fr>::~NttDomain() {
+  for (auto& e : ev_) (void)hipEventDestroy(e);
+  if (own_stream_) (void)hipStreamDestroy(stream_);
+}
+
+template <class Fr>
+void NttDomain<Fr>::build_twiddles() {
+  if (log_n_ == 0) return;
+  const uint32_t half = (uint32_t)(n_ / 2);
+  const uint32_t lb = (log_n_ - 1 + 1) / 2;  // lo bits of the base table split
+  const size_t lo_cnt = size_t(1) << lb;
+  const size_t hi_cnt = std::max<size_t>(1, half >> lb);
+  Fr* tw[2] = {static_cast<Fr*>(tw_fwd_.ensure(n_ * sizeof(Fr))), static_cast<Fr*>(tw_inv_.ensure(n_ * sizeof(Fr)))};
+  DeviceBuffer lo_d, hi_d;
+  Fr* lo = static_cast<Fr*>(lo_d.ensure(lo_cnt * sizeof(Fr)));
+  Fr* hi = static_cast<Fr*>(hi_d.ensure(hi_cnt * sizeof(Fr)));
+  for (int dir = 0; dir < 2; ++dir) {
+    Fr w = dir == 0 ? omega_ : omega_inv_;
+    std::vector<Fr> lo_h = host_powers(w, Fr::one(), lo_cnt);
+    Fr w_step = w;
+    for (uint32_t i = 0; i < lb; ++i) w_step = w_step.sqr();
+    std::vector<Fr> hi_h = host_powers(w_step, Fr::one(), hi_cnt);
+    TA_HIP(hipMemcpyAsync(lo, lo_h.data(), lo_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+    TA_HIP(hipMemcpyAsync(hi, hi_h.data(), hi_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+    hipLaunchKernelGGL(twiddle_base_kernel<Fr>, dim3(ceil_div(half, kBlock)), dim3(kBlock), 0, stream_, tw[dir], half,
+                       lo, hi, lb);
+    for (uint32_t s = 1; s < log_n_; ++s) {
+      uint32_t cnt = (uint32_t)(n_ >> (s + 1));
+      Fr* ts = tw[dir] + (n_ - (n_ >> s));
+      hipLaunchKernelGGL(twiddle_stage_kernel<Fr>, dim3(ceil_div(cnt, kBlock)), dim3(kBlock), 0, stream_, ts, tw[dir],
+                         cnt, s);
+    }
+    TA_HIP(hipGetLastError());
+    TA_HIP(hipStreamSynchronize(stream_));  // host vectors go out of scope
+  }
+}
+
+template <class Fr>
+void NttDomain<Fr>::build_powers(const Fr& base, const Fr& scale, Fr* d_lo, Fr* d_hi) {
+  const size_t lo_cnt = size_t(1) << pow_bits_;
+  const size_t hi_cnt = std::max<size_t>(1, n_ >> pow_bits_);
+  std::vector<Fr> lo_h = host_powers(base, scale, lo_cnt);
+  Fr step = base;
+  for (uint32_t i = 0; i < pow_bits_; ++i) step = step.sqr();
+  std::vector<Fr> hi_h = host_powers(step, Fr::one(), hi_cnt);
+  TA_HIP(hipMemcpyAsync(d_lo, lo_h.data(), lo_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+  TA_HIP(hipMemcpyAsync(d_hi, hi_h.data(), hi_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+  TA_HIP(hipStreamSynchronize(stream_));
+}
+
+template <class Fr>
+void NttDomain<Fr>::set_offset(const Fr& h) {
+  offset_ = h;
+  has_offset_ = !h.is_one();
+  offset_inv_ = has_offset_ ? h.inverse() : Fr::one();
+  if (!has_offset_) return;
+  const size_t lo_cnt = size_t(1) << pow_bits_;
+  const size_t hi_cnt = std::max<size_t>(1, n_ >> pow_bits_);
+  // forward: multiply input i by h^i ; inverse: output i by n^-1 h^-i
+  build_powers(h, Fr::one(), static_cast<Fr*>(coset_lo_.ensure(lo_cnt * sizeof(Fr))),
+               static_cast<Fr*>(coset_hi_.ensure(hi_cnt * sizeof(Fr))));
+  build_powers(offset_inv_, size_inv_, static_cast<Fr*>(icoset_lo_.ensure(lo_cnt * sizeof(Fr))),
+               static_cast<Fr*>(icoset_hi_.ensure(hi_cnt * sizeof(Fr))));
+}
+
+template <class Fr>
+void NttDomain<Fr>::run(Fr* d_data, bool inverse) {
+  if (log_n_ == 0) {
+    // size-1 domain: forward is the identity (h^0 = 1); inverse scales by n^-1 = 1
+    return;
+  }
+  const Fr* tw = inverse ? tw_inv_.as<Fr>() : tw_fwd_.as<Fr>();
+  Fr* scratch = plan_.size() > 1 ? static_cast<Fr*>(scratch_.ensure(n_ * sizeof(Fr))) : d_data;
+  if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
+  for (size_t p = 0; p < plan_.size(); ++p) {
+    const Pass& ps = plan_[p];
+    PassArgs<Fr> a{};
+    a.L = log_n_;
+    a.s0 = ps.s0;
+    a.k = ps.k;
+    a.log_m = ps.log_m;
+    a.final_pass = ps.final_pass ? 1u : 0u;
+    a.pow_bits = pow_bits_;
+    a.mode = 0;
+    if (p == 0 && !inverse && has_offset_) {
+      a.mode |= kLoadCoset;
+      a.load_lo = coset_lo_.as<Fr>();
+      a.load_hi = coset_hi_.as<Fr>();
+    }
+    if (ps.final_pass && inverse) {
+      if (has_offset_) {
+        a.mode |= kStoreCoset;
+        a.store_lo = icoset_lo_.as<Fr>();
+        a.store_hi = icoset_hi_.as<Fr>();
+      } else {
+        a.mode |= kStoreScale;
+        a.scale = size_inv_;
+      }
+    }
+    // first pass: data -> scratch; middle: scratch in place; last: scratch -> data
+    const Fr* src = (p == 0) ? d_data : scratch;
+    Fr* dst = ps.final_pass ? d_data : scratch;
+    uint32_t elems = (1u << ps.log_m) << ps.k;
+    uint32_t blocks = (uint32_t)(n_ / elems);
+    size_t lds = (size_t)elems * sizeof(Fr);
+    hipLaunchKernelGGL(dif_pass_kernel<Fr>, dim3(blocks), dim3(kBlock), lds, stream_, src, dst, tw, a);
+    TA_HIP(hipGetLastError());
+    if (profile_) TA_HIP(hipEventRecord(ev_[p + 1], stream_));
+  }
+  if (profile_) {
+    TA_HIP(hipEventSynchronize(ev_[plan_.size()]));
+    timings_.passes.assign(plan_.size(), 0.f);
+    for (size_t p = 0; p < plan_.size(); ++p) TA_HIP(hipEventElapsedTime(&timings_.passes[p], ev_[p], ev_[p + 1]));
+    TA_HIP(hipEventElapsedTime(&timings_.total, ev_[0], ev_[plan_.size()]));
+  }
+}
+
+template <class Fr>
+void NttDomain<Fr>::forward_device(Fr* d_data) { run(d_data, false); }
+
+template <class Fr>
+void NttDomain<Fr>::inverse_device(Fr* d_data) { run(d_data, true); }
+
+template <class Fr>
+void NttDomain<Fr>::forward_host(const Fr* in, size_t len, Fr* out) {
+  if (len > n_) throw std::runtime_error("tachyon_mi355x: FFT input longer than the domain");
+  Fr* d = static_cast<Fr*>(io_.ensure(n_ * sizeof(Fr)));
+  TA_HIP(hipMemcpyAsync(d, in, len * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+  if (len < n_) TA_HIP(hipMemsetAsync(d + len, 0, (n_ - len) * sizeof(Fr), stream_));
+  run(d, false);
+  TA_HIP(hipMemcpyAsync(out, d, n_ * sizeof(Fr), hipMemcpyDeviceToHost, stream_));
+  TA_HIP(hipStreamSynchronize(stream_));
+}
+
+template <class Fr>
+void NttDomain<Fr>::inverse_host(const Fr* in, size_t len, Fr* out) {
+  if (len > n_) throw std::runtime_error("tachyon_mi355x: IFFT input longer than the domain");
+  Fr* d = static_cast<Fr*>(io_.ensure(n_ * sizeof(Fr)));
+  TA_HIP(hipMemcpyAsync(d, in, len * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+  if (len < n_) TA_HIP(hipMemsetAsync(d + len, 0, (n_ - len) * sizeof(Fr), stream_));
+  run(d, true);
+  TA_HIP(hipMemcpyAsync(out, d, n_ * sizeof(Fr), hipMemcpyDeviceToHost, stream_));
+  TA_HIP(hipStreamSynchronize(stream_));
+}
+
+template class NttDomain<Bn254Fr>;
+template class NttDomain<Bls381Fr>;
+
+}  // namespace tachyon_amd::ntt
