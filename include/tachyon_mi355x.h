@@ -214,8 +214,9 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const 
                                                     size_t size, void* out_affine);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
-/* ms: h2d, recode, sort, acc, reduce, total (6 floats) */
-TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out6);
+/* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
+ * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total, 0 (8 floats) */
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8);
 /* window bits / windows the planner picks for `size` points */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows);
 /* Host-side group arithmetic on affine points (multi-GPU partial sums):
@@ -242,6 +243,9 @@ TACHYON_C_EXPORT void tachyon_mi355x_field_op(int field, int op, const void* a, 
 /* point op: 0 add (affine + affine), 1 double, 2 add-mixed into xyzz of a. Affine in/out. */
 TACHYON_C_EXPORT void tachyon_mi355x_ec_op(int curve, int op, const void* a, const void* b, void* out, size_t count);
 
+/* delete a Jacobian returned by an *_msm / *_msm_gpu entry point (for callers
+ * that cannot use C++ delete, e.g. ctypes). */
+TACHYON_C_EXPORT void tachyon_mi355x_jacobian_destroy(int curve, void* jacobian);
 TACHYON_C_EXPORT const char* tachyon_mi355x_version(void);
 TACHYON_C_EXPORT int tachyon_mi355x_device_count(void);
 

@@ -1,0 +1,130 @@
+"""ctypes binding of libtachyon_mi355x.so (the C-ABI in include/tachyon_mi355x.h).
+
+The library is built in-tree by `tachyon_amd.build.build()` (hipcc, gfx950).
+There is no CPU fallback: if the shared library is missing this module raises,
+and every compute entry point of the library aborts without a HIP device.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtachyon_mi355x.so")
+
+CURVES = {"bn254_g1": 0, "bn254_g2": 1, "bls12_381_g1": 2, "bls12_381_g2": 3}
+FIELDS = {"bn254_fq": 0, "bn254_fr": 1, "bls12_381_fq": 2, "bls12_381_fr": 3}
+FIELD_BYTES = {"bn254_fq": 32, "bn254_fr": 32, "bls12_381_fq": 48, "bls12_381_fr": 32}
+# curve -> (affine point bytes, scalar field)
+CURVE_INFO = {
+    "bn254_g1": (64, "bn254_fr"),
+    "bn254_g2": (128, "bn254_fr"),
+    "bls12_381_g1": (96, "bls12_381_fr"),
+    "bls12_381_g2": (192, "bls12_381_fr"),
+}
+
+_lib = None
+
+# (name, restype, argtypes) of every entry point declared in include/tachyon_mi355x.h
+vp, sz, i32, u8, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint64
+fp = ctypes.POINTER(ctypes.c_float)
+SIGNATURES = [
+    # reference C-ABI: MSM
+    ("tachyon_bn254_g1_init", None, []),
+    ("tachyon_bls12_381_g1_init", None, []),
+    ("tachyon_bn254_g2_init", None, []),
+    ("tachyon_bls12_381_g2_init", None, []),
+    ("tachyon_bn254_g1_create_msm", vp, [u8]),
+    ("tachyon_bn254_g1_destroy_msm", None, [vp]),
+    ("tachyon_bn254_g1_point2_msm", vp, [vp, vp, vp, sz]),
+    ("tachyon_bn254_g1_affine_msm", vp, [vp, vp, vp, sz]),
+    ("tachyon_bn254_g1_create_msm_gpu", vp, [u8]),
+    ("tachyon_bn254_g1_destroy_msm_gpu", None, [vp]),
+    ("tachyon_bn254_g1_point2_msm_gpu", vp, [vp, vp, vp, sz]),
+    ("tachyon_bn254_g1_affine_msm_gpu", vp, [vp, vp, vp, sz]),
+    ("tachyon_bls12_381_g1_create_msm", vp, [u8]),
+    ("tachyon_bls12_381_g1_destroy_msm", None, [vp]),
+    ("tachyon_bls12_381_g1_point2_msm", vp, [vp, vp, vp, sz]),
+    ("tachyon_bls12_381_g1_affine_msm", vp, [vp, vp, vp, sz]),
+    ("tachyon_bls12_381_g1_create_msm_gpu", vp, [u8]),
+    ("tachyon_bls12_381_g1_destroy_msm_gpu", None, [vp]),
+    ("tachyon_bls12_381_g1_point2_msm_gpu", vp, [vp, vp, vp, sz]),
+    ("tachyon_bls12_381_g1_affine_msm_gpu", vp, [vp, vp, vp, sz]),
+    # reference C-ABI: univariate domain / containers
+    ("tachyon_bn254_univariate_evaluation_domain_create", vp, [sz]),
+    ("tachyon_bn254_univariate_evaluation_domain_destroy", None, [vp]),
+    ("tachyon_bn254_univariate_evaluation_domain_empty_evals", vp, [vp]),
+    ("tachyon_bn254_univariate_evaluation_domain_empty_poly", vp, [vp]),
+    ("tachyon_bn254_univariate_evaluation_domain_fft", vp, [vp, vp]),
+    ("tachyon_bn254_univariate_evaluation_domain_fft_inplace", vp, [vp, vp]),
+    ("tachyon_bn254_univariate_evaluation_domain_ifft", vp, [vp, vp]),
+    ("tachyon_bn254_univariate_evaluation_domain_ifft_inplace", vp, [vp, vp]),
+    ("tachyon_bn254_univariate_evaluations_create", vp, []),
+    ("tachyon_bn254_univariate_evaluations_clone", vp, [vp]),
+    ("tachyon_bn254_univariate_evaluations_destroy", None, [vp]),
+    ("tachyon_bn254_univariate_evaluations_len", sz, [vp]),
+    ("tachyon_bn254_univariate_evaluations_set_value", None, [vp, sz, vp]),
+    ("tachyon_bn254_univariate_dense_polynomial_create", vp, []),
+    ("tachyon_bn254_univariate_dense_polynomial_clone", vp, [vp]),
+    ("tachyon_bn254_univariate_dense_polynomial_destroy", None, [vp]),
+    # extensions
+    ("tachyon_mi355x_bn254_univariate_evaluations_get_value", None, [vp, sz, vp]),
+    ("tachyon_mi355x_bn254_univariate_evaluations_data", vp, [vp]),
+    ("tachyon_mi355x_bn254_univariate_evaluations_resize", None, [vp, sz]),
+    ("tachyon_mi355x_bn254_univariate_dense_polynomial_len", sz, [vp]),
+    ("tachyon_mi355x_bn254_univariate_dense_polynomial_resize", None, [vp, sz]),
+    ("tachyon_mi355x_bn254_univariate_dense_polynomial_set_value", None, [vp, sz, vp]),
+    ("tachyon_mi355x_bn254_univariate_dense_polynomial_get_value", None, [vp, sz, vp]),
+    ("tachyon_mi355x_bn254_univariate_dense_polynomial_data", vp, [vp]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_size", sz, [vp]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_group_gen", None, [vp, vp]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset", None, [vp, vp]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device", None, [vp, vp, i32]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_stream", vp, [vp]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile", None, [vp, i32]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings", i32, [vp, fp, fp, i32]),
+    ("tachyon_bn254_g2_create_msm_gpu", vp, [u8]),
+    ("tachyon_bn254_g2_destroy_msm_gpu", None, [vp]),
+    ("tachyon_bn254_g2_affine_msm_gpu", vp, [vp, vp, vp, sz]),
+    ("tachyon_bls12_381_g2_create_msm_gpu", vp, [u8]),
+    ("tachyon_bls12_381_g2_destroy_msm_gpu", None, [vp]),
+    ("tachyon_bls12_381_g2_affine_msm_gpu", vp, [vp, vp, vp, sz]),
+    ("tachyon_mi355x_msm_gpu_affine", None, [i32, vp, vp, vp, sz, vp]),
+    ("tachyon_mi355x_msm_gpu_set_window_bits", None, [i32, vp, ctypes.c_uint]),
+    ("tachyon_mi355x_msm_gpu_set_profile", None, [i32, vp, i32]),
+    ("tachyon_mi355x_msm_gpu_last_timings", None, [i32, vp, fp]),
+    ("tachyon_mi355x_msm_plan", None, [i32, sz, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]),
+    ("tachyon_mi355x_affine_sum", None, [i32, vp, sz, vp]),
+    ("tachyon_mi355x_jacobian_to_affine", None, [i32, vp, vp]),
+    ("tachyon_mi355x_gen_scalars", None, [i32, u64, sz, sz, vp, vp]),
+    ("tachyon_mi355x_gen_bases", None, [i32, u64, sz, sz, vp, vp]),
+    ("tachyon_mi355x_field_op", None, [i32, i32, vp, vp, vp, sz]),
+    ("tachyon_mi355x_ec_op", None, [i32, i32, vp, vp, vp, sz]),
+    ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
+    ("tachyon_mi355x_version", ctypes.c_char_p, []),
+    ("tachyon_mi355x_device_count", i32, []),
+]
+
+
+def lib():
+    """Load the in-tree HIP library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        # One HIP runtime per process: PyTorch-ROCm bundles its own
+        # libamdhip64 (SONAME libamdhip64.so.7) and cannot initialise the GPU
+        # once /opt/rocm's copy is loaded.  Importing torch first makes this
+        # library bind to the runtime torch already loaded, so HBM buffers,
+        # streams and RCCL from torch interoperate with the C-ABI.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(the MI355X backend has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib

@@ -291,10 +291,11 @@ void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c) {
 void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on) {
   GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_profile(on != 0)) GUARD_END
 }
-void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out6) {
+void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8) {
   GUARD_BEGIN CURVE_DISPATCH(curve, {
     const msm::MsmTimings& t = static_cast<const MsmCtx<C>*>(ctx)->impl.timings();
-    out6[0] = t.h2d; out6[1] = t.recode; out6[2] = t.sort; out6[3] = t.acc; out6[4] = t.reduce; out6[5] = t.total;
+    out8[0] = t.h2d; out8[1] = t.recode; out8[2] = t.sort; out8[3] = t.prep; out8[4] = t.acc; out8[5] = t.reduce;
+    out8[6] = t.total; out8[7] = 0.f;
   }) GUARD_END
 }
 void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows) {
@@ -322,6 +323,15 @@ void tachyon_mi355x_field_op(int field, int op, const void* a, const void* b, vo
 }
 void tachyon_mi355x_ec_op(int curve, int op, const void* a, const void* b, void* out, size_t count) {
   GUARD_BEGIN util::ec_op(curve, op, a, b, out, count); GUARD_END
+}
+
+void tachyon_mi355x_jacobian_destroy(int curve, void* jac) {
+  switch (curve) {
+    case 0: delete static_cast<tachyon_bn254_g1_jacobian*>(jac); break;
+    case 1: delete static_cast<tachyon_bn254_g2_jacobian*>(jac); break;
+    case 2: delete static_cast<tachyon_bls12_381_g1_jacobian*>(jac); break;
+    case 3: delete static_cast<tachyon_bls12_381_g2_jacobian*>(jac); break;
+  }
 }
 
 const char* tachyon_mi355x_version(void) { return "tachyon_mi355x 0.1 (gfx950)"; }

@@ -38,6 +38,9 @@ struct XYZZ {
   }
   TA_HD XYZZ neg() const { return {x, -y, zz, zzz}; }
 
+  // out-of-line doubling for the exceptional P == Q branch of the adds
+  TA_HD_NOINLINE XYZZ dbl_outline() const { return dbl(); }
+
   // dbl-2008-s-1 (a = 0)
   TA_HD XYZZ dbl() const {
     if (is_zero()) return *this;
@@ -61,7 +64,7 @@ struct XYZZ {
     if (is_zero()) return from_affine(b);
     F p = b.x * zz - x;
     F r = b.y * zzz - y;
-    if (p.is_zero() && r.is_zero()) return dbl();
+    if (p.is_zero() && r.is_zero()) return dbl_outline();
     F pp = p.sqr();
     F ppp = p * pp;
     F q = x * pp;
@@ -81,7 +84,7 @@ struct XYZZ {
     F s1 = y * b.zzz;
     F p = b.x * zz - u1;
     F r = b.y * zzz - s1;
-    if (p.is_zero() && r.is_zero()) return dbl();
+    if (p.is_zero() && r.is_zero()) return dbl_outline();
     F pp = p.sqr();
     F ppp = p * pp;
     F q = u1 * pp;
@@ -94,7 +97,7 @@ struct XYZZ {
   }
 
   // point_xyzz.h:199-212
-  TA_HD Affine<F> to_affine() const {
+  TA_HD_NOINLINE Affine<F> to_affine() const {
     if (is_zero()) return Affine<F>::zero();
     if (zz.is_one()) return {x, y};
     F zinv3 = zzz.inverse();
@@ -103,7 +106,7 @@ struct XYZZ {
   }
 
   // point_xyzz.h:228-237
-  TA_HD Jacobian<F> to_jacobian() const {
+  TA_HD_NOINLINE Jacobian<F> to_jacobian() const {
     if (is_zero()) return Jacobian<F>::zero();
     if (zz.is_one()) return {x, y, F::one()};
     F z = zz * zzz;

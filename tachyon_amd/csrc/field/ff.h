@@ -18,6 +18,11 @@
 #include "constants.h"
 
 #define TA_HD __host__ __device__ __forceinline__
+// Rarely-executed or very large bodies stay out of line: inlining every
+// 12-limb (BLS12-381 Fq) product and every exceptional-case doubling made
+// single kernels tens of thousands of instructions long and compile for
+// minutes.
+#define TA_HD_NOINLINE __host__ __device__ __noinline__
 
 namespace tachyon_amd {
 
@@ -108,8 +113,14 @@ struct Fp {
   }
   TA_HD Fp operator-() const { return zero() - *this; }
 
-  // CIOS no-carry Montgomery product (DoFastMul, prime_field_fallback.h:331-355).
   TA_HD Fp operator*(const Fp& b) const {
+    if constexpr (N <= 8) return mul_inline(b);
+    else return mul_outline(b);
+  }
+  TA_HD_NOINLINE Fp mul_outline(const Fp& b) const { return mul_inline(b); }
+
+  // CIOS no-carry Montgomery product (DoFastMul, prime_field_fallback.h:331-355).
+  TA_HD Fp mul_inline(const Fp& b) const {
     uint32_t t[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) t[i] = 0;
@@ -155,7 +166,7 @@ struct Fp {
     return (*this) * r2;
   }
 
-  TA_HD Fp pow(const uint32_t* e, int nlimbs) const {
+  TA_HD_NOINLINE Fp pow(const uint32_t* e, int nlimbs) const {
     Fp r = one();
     for (int i = nlimbs - 1; i >= 0; --i)
       for (int bit = 31; bit >= 0; --bit) {
@@ -165,11 +176,12 @@ struct Fp {
     return r;
   }
   // Fermat inverse (same canonical value as the reference's BY inverter).
-  TA_HD Fp inverse() const {
+  TA_HD_NOINLINE Fp inverse() const {
+    // e = p - 2 with borrow (BLS12-381 Fr's low 32-bit limb is 1)
     uint32_t e[N];
+    uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < N; ++i) e[i] = Cfg::kP32[i];
-    e[0] -= 2;
+    for (int i = 0; i < N; ++i) e[i] = subb(Cfg::kP32[i], i == 0 ? 2u : 0u, br, &br);
     return pow(e, N);
   }
 };
@@ -191,6 +203,11 @@ struct Fp2 {
   TA_HD Fp2 operator-() const { return {-c0, -c1}; }
   TA_HD Fp2 dbl() const { return {c0.dbl(), c1.dbl()}; }
   TA_HD Fp2 operator*(const Fp2& o) const {
+    if constexpr (F::N <= 8) return mul_inline(o);
+    else return mul_outline(o);
+  }
+  TA_HD_NOINLINE Fp2 mul_outline(const Fp2& o) const { return mul_inline(o); }
+  TA_HD Fp2 mul_inline(const Fp2& o) const {
     F v0 = c0 * o.c0;
     F v1 = c1 * o.c1;
     F m = (c0 + c1) * (o.c0 + o.c1);
@@ -200,7 +217,7 @@ struct Fp2 {
     F ab = c0 * c1;
     return {(c0 + c1) * (c0 - c1), ab.dbl()};
   }
-  TA_HD Fp2 inverse() const {
+  TA_HD_NOINLINE Fp2 inverse() const {
     F t = (c0.sqr() + c1.sqr()).inverse();
     return {c0 * t, -(c1 * t)};
   }

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <algorithm>
 #include <cstdint>
 #include <vector>
 
@@ -32,12 +33,38 @@ struct MsmPlan {
   unsigned K2 = 16;      // fan-in of the partial-reduction levels
   unsigned levels = 0;   // number of K2 levels
   unsigned seg = 0;      // buckets per running-sum segment
-  static MsmPlan make(size_t n, unsigned scalar_bits, unsigned force_c = 0);
+  static inline MsmPlan make(size_t n, unsigned scalar_bits, unsigned force_c = 0);
 };
+
+// Window size: more bits -> fewer windows (fewer madds, fewer sort passes)
+// but more buckets to reduce.  n*W madds dominate; bucket reduction costs
+// ~2*W*2^(c-1) adds.  Tuned on MI355X.
+inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
+  MsmPlan p;
+  unsigned lg = 1;
+  while ((size_t(1) << lg) < n) ++lg;
+  unsigned c = force_c ? force_c : (unsigned)std::clamp<int>((int)lg - 6, 4, 20);
+  p.c = c;
+  p.windows = (scalar_bits + 1 + c - 1) / c;  // W*c >= bits+1
+  p.buckets = 1u << (c - 1);
+  size_t entries = (size_t)n * p.windows;
+  // aim for ~2^20 accumulation threads; K in [8, 512]
+  size_t k = entries >> 20;
+  p.K = (unsigned)std::clamp<size_t>(k, 8, 512);
+  p.K2 = 16;
+  size_t maxchunks = (n + p.K - 1) / p.K;  // worst case: all entries of a window in one bucket
+  p.levels = 0;
+  while (maxchunks > 1) {
+    maxchunks = (maxchunks + p.K2 - 1) / p.K2;
+    ++p.levels;
+  }
+  p.seg = std::min<unsigned>(p.buckets, 64);
+  return p;
+}
 
 // Per-phase device timings of the last run (ms), filled when profiling is on.
 struct MsmTimings {
-  float h2d = 0, recode = 0, sort = 0, acc = 0, reduce = 0, total = 0;
+  float h2d = 0, recode = 0, sort = 0, prep = 0, acc = 0, reduce = 0, total = 0;
 };
 
 template <class Curve>

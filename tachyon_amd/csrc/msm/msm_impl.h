@@ -1,7 +1,10 @@
-// Variable-base MSM kernels for MI355X (gfx950) and their host driver.
+// Variable-base MSM kernels for MI355X (gfx950) and their host driver
+// (template definitions; one translation unit per curve instantiates them:
+// msm_bn254_g1.hip, msm_bn254_g2.hip, msm_bls12_381_g1.hip, msm_bls12_381_g2.hip).
 // See msm.h for the pipeline; reference semantics: pippenger.h:28-170,
 // pippenger_base.h:36-77 (the answer is the same group element; the parity
 // tests compare affine coordinates bytewise).
+#pragma once
 #include "msm.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -12,7 +15,8 @@
 
 namespace tachyon_amd::msm {
 
-namespace {
+namespace detail {
+namespace {  // internal linkage: every per-curve TU gets its own copy
 
 constexpr unsigned kBlock = 256;
 constexpr uint32_t kSignBit = 0x80000000u;
@@ -222,35 +226,11 @@ __global__ __launch_bounds__(kBlock) void reduce_uniform_kernel(const XYZZ<typen
   out[t] = acc;
 }
 
-unsigned grid_for(size_t threads) { return (unsigned)std::max<size_t>(1, (threads + kBlock - 1) / kBlock); }
+inline unsigned grid_for(size_t threads) { return (unsigned)std::max<size_t>(1, (threads + kBlock - 1) / kBlock); }
 
 }  // namespace
-
-// Window size: more bits -> fewer windows (fewer madds, fewer sort passes)
-// but more buckets to reduce.  n*W madds dominate; bucket reduction costs
-// ~2*W*2^(c-1) adds.  Tuned on MI355X.
-MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
-  MsmPlan p;
-  unsigned lg = 1;
-  while ((size_t(1) << lg) < n) ++lg;
-  unsigned c = force_c ? force_c : (unsigned)std::clamp<int>((int)lg - 6, 4, 20);
-  p.c = c;
-  p.windows = (scalar_bits + 1 + c - 1) / c;  // W*c >= bits+1
-  p.buckets = 1u << (c - 1);
-  size_t entries = (size_t)n * p.windows;
-  // aim for ~2^20 accumulation threads; K in [8, 512]
-  size_t k = entries >> 20;
-  p.K = (unsigned)std::clamp<size_t>(k, 8, 512);
-  p.K2 = 16;
-  size_t maxchunks = (n + p.K - 1) / p.K;  // worst case: all entries of a window in one bucket
-  p.levels = 0;
-  while (maxchunks > 1) {
-    maxchunks = (maxchunks + p.K2 - 1) / p.K2;
-    ++p.levels;
-  }
-  p.seg = std::min<unsigned>(p.buckets, 64);
-  return p;
-}
+}  // namespace detail
+using namespace detail;
 
 template <class Curve>
 MsmGpu<Curve>::MsmGpu(hipStream_t stream) : stream_(stream) {
@@ -316,6 +296,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   TA_HIP(rocprim::exclusive_scan(scan_tmp, scan_bytes, cnt, off_a, 0u, nb + 1, rocprim::plus<uint32_t>(), stream_));
 
   // ---- accumulation ----
+  if (profile_) TA_HIP(hipEventRecord(ev_[6], stream_));
   size_t max_chunks = entries / plan.K + nb + 1;
   // size both ping-pong buffers up front: nothing may be freed while queued
   // kernels still read it
@@ -398,7 +379,8 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
     TA_HIP(hipEventElapsedTime(&timings_.h2d, ev_[0], ev_[1]));
     TA_HIP(hipEventElapsedTime(&timings_.recode, ev_[1], ev_[2]));
     TA_HIP(hipEventElapsedTime(&timings_.sort, ev_[2], ev_[3]));
-    TA_HIP(hipEventElapsedTime(&timings_.acc, ev_[3], ev_[4]));
+    TA_HIP(hipEventElapsedTime(&timings_.prep, ev_[3], ev_[6]));
+    TA_HIP(hipEventElapsedTime(&timings_.acc, ev_[6], ev_[4]));
     TA_HIP(hipEventElapsedTime(&timings_.reduce, ev_[4], ev_[5]));
     TA_HIP(hipEventElapsedTime(&timings_.total, ev_[0], ev_[5]));
   }
@@ -426,9 +408,5 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* 
   return combine_windows(ws, plan.c);
 }
 
-template class MsmGpu<Bn254G1>;
-template class MsmGpu<Bn254G2>;
-template class MsmGpu<Bls381G1>;
-template class MsmGpu<Bls381G2>;
 
 }  // namespace tachyon_amd::msm

@@ -1,0 +1,137 @@
+"""Host mirror of tachyon::math::VariableBaseMSMGpu<Point> over the C-ABI.
+
+Reference: tachyon/math/elliptic_curves/msm/variable_base_msm_gpu.h:11-30
+(ctor(mem_pool, stream); Run(bases, scalars, &ret) -> bool) and the C-ABI
+tachyon_<curve>_g1_{create,destroy}_msm_gpu / _affine_msm_gpu
+(tachyon/c/math/elliptic_curves/generator/msm_gpu.h.tpl:26-54).
+
+Inputs may be `bytes`, contiguous numpy arrays (host memory) or torch CUDA
+tensors (device memory, used in place -- the analogue of the reference's
+device-pointer detection, icicle_msm_bn254_g1.cc:37-45).
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import CURVE_INFO, CURVES, FIELD_BYTES, lib
+
+_CREATE = {
+    "bn254_g1": ("tachyon_bn254_g1_create_msm_gpu", "tachyon_bn254_g1_destroy_msm_gpu", "tachyon_bn254_g1_affine_msm_gpu"),
+    "bn254_g2": ("tachyon_bn254_g2_create_msm_gpu", "tachyon_bn254_g2_destroy_msm_gpu", "tachyon_bn254_g2_affine_msm_gpu"),
+    "bls12_381_g1": ("tachyon_bls12_381_g1_create_msm_gpu", "tachyon_bls12_381_g1_destroy_msm_gpu",
+                     "tachyon_bls12_381_g1_affine_msm_gpu"),
+    "bls12_381_g2": ("tachyon_bls12_381_g2_create_msm_gpu", "tachyon_bls12_381_g2_destroy_msm_gpu",
+                     "tachyon_bls12_381_g2_affine_msm_gpu"),
+}
+
+
+def _ptr(x):
+    """(pointer, nbytes, keepalive) of bytes / numpy / torch tensor."""
+    if isinstance(x, (bytes, bytearray)):
+        buf = ctypes.create_string_buffer(bytes(x), max(1, len(x)))
+        return ctypes.addressof(buf), len(x), buf
+    if isinstance(x, np.ndarray):
+        if not x.flags["C_CONTIGUOUS"]:
+            x = np.ascontiguousarray(x)
+        return x.ctypes.data, x.nbytes, x
+    if hasattr(x, "data_ptr"):  # torch tensor (host or device)
+        if not x.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return x.data_ptr(), x.numel() * x.element_size(), x
+    raise TypeError(f"unsupported buffer type {type(x)}")
+
+
+class VariableBaseMSMGpu:
+    def __init__(self, curve: str = "bn254_g1", degree: int = 0):
+        if curve not in CURVES:
+            raise ValueError(f"unknown curve {curve}")
+        self.curve = curve
+        self.curve_id = CURVES[curve]
+        self.point_bytes, self.scalar_field = CURVE_INFO[curve]
+        self.scalar_bytes = FIELD_BYTES[self.scalar_field]
+        create, self._destroy, self._affine_msm = _CREATE[curve]
+        self._ctx = getattr(lib(), create)(degree)
+        if not self._ctx:
+            raise RuntimeError("failed to create MSM context")
+
+    def close(self):
+        if self._ctx:
+            getattr(lib(), self._destroy)(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _args(self, bases, scalars, n):
+        pb, bn, kb = _ptr(bases)
+        ps, sn, ks = _ptr(scalars)
+        if n is None:
+            n = bn // self.point_bytes
+        if bn < n * self.point_bytes or sn < n * self.scalar_bytes:
+            raise ValueError("bases/scalars shorter than n")
+        return pb, ps, n, (kb, ks)
+
+    def run(self, bases, scalars, n=None) -> bytes:
+        """MSM sum_i scalars[i] * bases[i]; returns affine (x, y) Montgomery bytes."""
+        pb, ps, n, keep = self._args(bases, scalars, n)
+        out = ctypes.create_string_buffer(self.point_bytes)
+        lib().tachyon_mi355x_msm_gpu_affine(self.curve_id, self._ctx, pb, ps, n, out)
+        del keep
+        return out.raw
+
+    def run_jacobian(self, bases, scalars, n=None) -> bytes:
+        """Through the reference entry point (*_affine_msm_gpu): returns the
+        Jacobian the C-ABI allocates (copied, then freed)."""
+        pb, ps, n, keep = self._args(bases, scalars, n)
+        p = getattr(lib(), self._affine_msm)(self._ctx, pb, ps, n)
+        nbytes = self.point_bytes // 2 * 3
+        data = ctypes.string_at(p, nbytes)
+        lib().tachyon_mi355x_jacobian_destroy(self.curve_id, p)
+        del keep
+        return data
+
+    def set_window_bits(self, c: int):
+        lib().tachyon_mi355x_msm_gpu_set_window_bits(self.curve_id, self._ctx, c)
+
+    def set_profile(self, on: bool):
+        lib().tachyon_mi355x_msm_gpu_set_profile(self.curve_id, self._ctx, 1 if on else 0)
+
+    def last_timings(self) -> dict:
+        out = (ctypes.c_float * 8)()
+        lib().tachyon_mi355x_msm_gpu_last_timings(self.curve_id, self._ctx, out)
+        return dict(zip(("h2d", "recode", "sort", "prep", "acc", "reduce", "total"), list(out)))
+
+
+def plan(curve: str, n: int):
+    c, w = ctypes.c_uint(), ctypes.c_uint()
+    lib().tachyon_mi355x_msm_plan(CURVES[curve], n, ctypes.byref(c), ctypes.byref(w))
+    return c.value, w.value
+
+
+def affine_sum(curve: str, points: bytes) -> bytes:
+    """Group sum of affine points on the host (combines per-GPU partial MSMs)."""
+    pbytes = CURVE_INFO[curve][0]
+    n = len(points) // pbytes
+    src = ctypes.create_string_buffer(points, max(1, len(points)))
+    out = ctypes.create_string_buffer(pbytes)
+    lib().tachyon_mi355x_affine_sum(CURVES[curve], src, n, out)
+    return out.raw
+
+
+def jacobian_to_affine(curve: str, jac: bytes) -> bytes:
+    pbytes = CURVE_INFO[curve][0]
+    src = ctypes.create_string_buffer(jac, len(jac))
+    out = ctypes.create_string_buffer(pbytes)
+    lib().tachyon_mi355x_jacobian_to_affine(CURVES[curve], src, out)
+    return out.raw
+
+
+def gen_scalars(field: str, seed: int, n: int, d_out_ptr: int, start: int = 0, stream=None):
+    lib().tachyon_mi355x_gen_scalars({"bn254_fr": 1, "bls12_381_fr": 3}[field], seed, start, n, d_out_ptr, stream)
+
+
+def gen_bases(curve: str, seed: int, n: int, chunk: int, d_out_ptr: int, stream=None):
+    lib().tachyon_mi355x_gen_bases(CURVES[curve], seed, n, chunk, d_out_ptr, stream)

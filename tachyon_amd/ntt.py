@@ -1,0 +1,110 @@
+"""Host mirror of tachyon::math::Radix2EvaluationDomain<bn254::Fr> over the C-ABI.
+
+Reference: tachyon/c/math/polynomials/univariate/bn254_univariate_evaluation_domain.h:38-136
+(create / fft / ifft returning new containers) and
+tachyon/math/polynomials/univariate/univariate_evaluation_domain.h
+(FFT/IFFT semantics, GetCoset :102-117).
+Elements are BN254 Fr in Montgomery form, 32 bytes each.
+"""
+import ctypes
+
+from ._lib import lib
+
+FR_BYTES = 32
+
+
+class Radix2EvaluationDomain:
+    def __init__(self, num_coeffs: int, _handle=None):
+        L = lib()
+        self._d = _handle or L.tachyon_bn254_univariate_evaluation_domain_create(num_coeffs)
+        if not self._d:
+            raise RuntimeError("domain creation failed")
+        self.size = L.tachyon_mi355x_bn254_univariate_evaluation_domain_size(self._d)
+        self.log_size_of_group = self.size.bit_length() - 1
+        self.offset = None
+
+    @classmethod
+    def create(cls, num_coeffs: int):
+        return cls(num_coeffs)
+
+    def close(self):
+        if self._d:
+            lib().tachyon_bn254_univariate_evaluation_domain_destroy(self._d)
+            self._d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def group_gen(self) -> bytes:
+        out = ctypes.create_string_buffer(FR_BYTES)
+        lib().tachyon_mi355x_bn254_univariate_evaluation_domain_group_gen(self._d, out)
+        return out.raw
+
+    def set_offset(self, offset_mont: bytes):
+        """Coset h*<w> (GetCoset); offset = Montgomery bytes of h."""
+        buf = ctypes.create_string_buffer(offset_mont, FR_BYTES)
+        lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset(self._d, buf)
+        self.offset = offset_mont
+
+    def _poly(self, coeffs: bytes):
+        L = lib()
+        p = L.tachyon_bn254_univariate_dense_polynomial_create()
+        n = len(coeffs) // FR_BYTES
+        L.tachyon_mi355x_bn254_univariate_dense_polynomial_resize(p, n)
+        if n:
+            ctypes.memmove(L.tachyon_mi355x_bn254_univariate_dense_polynomial_data(p), coeffs, n * FR_BYTES)
+        return p
+
+    def _evals(self, evals: bytes):
+        L = lib()
+        e = L.tachyon_bn254_univariate_evaluations_create()
+        n = len(evals) // FR_BYTES
+        L.tachyon_mi355x_bn254_univariate_evaluations_resize(e, n)
+        if n:
+            ctypes.memmove(L.tachyon_mi355x_bn254_univariate_evaluations_data(e), evals, n * FR_BYTES)
+        return e
+
+    def fft(self, coeffs: bytes) -> bytes:
+        """tachyon_bn254_univariate_evaluation_domain_fft: coefficients -> evaluations."""
+        L = lib()
+        p = self._poly(coeffs)
+        e = L.tachyon_bn254_univariate_evaluation_domain_fft(self._d, p)
+        n = L.tachyon_bn254_univariate_evaluations_len(e)
+        out = ctypes.string_at(L.tachyon_mi355x_bn254_univariate_evaluations_data(e), n * FR_BYTES) if n else b""
+        L.tachyon_bn254_univariate_evaluations_destroy(e)
+        L.tachyon_bn254_univariate_dense_polynomial_destroy(p)
+        return out
+
+    def ifft(self, evals: bytes) -> bytes:
+        """tachyon_bn254_univariate_evaluation_domain_ifft: evaluations -> coefficients
+        (trailing zero coefficients removed, like the reference CPU path)."""
+        L = lib()
+        e = self._evals(evals)
+        p = L.tachyon_bn254_univariate_evaluation_domain_ifft(self._d, e)
+        n = L.tachyon_mi355x_bn254_univariate_dense_polynomial_len(p)
+        out = ctypes.string_at(L.tachyon_mi355x_bn254_univariate_dense_polynomial_data(p), n * FR_BYTES) if n else b""
+        L.tachyon_bn254_univariate_dense_polynomial_destroy(p)
+        L.tachyon_bn254_univariate_evaluations_destroy(e)
+        return out
+
+    def transform_device(self, d_ptr: int, inverse: bool = False):
+        """In-place transform of `size` elements already in HBM (not synchronised;
+        runs on self.stream)."""
+        lib().tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(self._d, d_ptr, 1 if inverse else 0)
+
+    @property
+    def stream(self) -> int:
+        return lib().tachyon_mi355x_bn254_univariate_evaluation_domain_stream(self._d)
+
+    def set_profile(self, on: bool):
+        lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(self._d, 1 if on else 0)
+
+    def last_timings(self):
+        total = ctypes.c_float()
+        passes = (ctypes.c_float * 16)()
+        k = lib().tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(self._d, ctypes.byref(total), passes, 16)
+        return total.value, list(passes)[:k]

@@ -1,0 +1,67 @@
+"""CPU-side checks of the product library: it was built for gfx950, loads
+without a GPU, and exports every symbol include/tachyon_mi355x.h declares
+(no compute calls here)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "tachyon_mi355x.h")
+LIB = os.path.join(ROOT, "tachyon_amd", "libtachyon_mi355x.so")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"TACHYON_C_EXPORT[^;(]*?\b(tachyon_\w+)\s*\(", text, re.S)))
+
+
+@pytest.fixture(scope="module")
+def libpath():
+    if not os.path.exists(LIB):
+        pytest.skip("libtachyon_mi355x.so not built (run __graft_entry__.build())")
+    return LIB
+
+
+def test_header_declares_reference_abi():
+    syms = declared_symbols()
+    for s in ("tachyon_bn254_g1_create_msm_gpu", "tachyon_bn254_g1_affine_msm_gpu", "tachyon_bn254_g1_point2_msm_gpu",
+              "tachyon_bn254_g1_destroy_msm_gpu", "tachyon_bn254_g1_affine_msm", "tachyon_bls12_381_g1_affine_msm_gpu",
+              "tachyon_bn254_univariate_evaluation_domain_create", "tachyon_bn254_univariate_evaluation_domain_fft",
+              "tachyon_bn254_univariate_evaluation_domain_ifft_inplace", "tachyon_bn254_univariate_evaluations_set_value"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(libpath):
+    out = subprocess.run(["nm", "-D", "--defined-only", libpath], capture_output=True, text=True, check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if " T " in line)
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+
+
+def test_library_loads_and_binds_signatures(libpath):
+    from tachyon_amd._lib import SIGNATURES, lib
+    L = lib()
+    names = {n for n, _, _ in SIGNATURES}
+    assert set(declared_symbols()) == names
+    assert b"gfx950" in L.tachyon_mi355x_version()
+
+
+def test_code_object_targets_gfx950(libpath):
+    # the fat binary carries one code object, for gfx950 only
+    data = open(libpath, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx\w+)", data))
+    assert targets == {b"gfx950"}, targets
+
+
+def test_no_oracle_in_product():
+    """The product path never imports / links the oracle."""
+    bad = re.compile(r"^\s*(import\s+oracle|from\s+oracle)|#\s*include\s*[\"<][^\">]*oracle|liboracle", re.M)
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "tachyon_amd")):
+        for f in files:
+            if f.endswith((".py", ".h", ".hip", ".cc", "Makefile")) and f != "build.py":
+                text = open(os.path.join(dirpath, f), errors="ignore").read()
+                assert not bad.search(text), f
+    out = subprocess.run(["nm", "-D", LIB], capture_output=True, text=True).stdout if os.path.exists(LIB) else ""
+    assert "oracle_" not in out

@@ -1,0 +1,153 @@
+"""GPU MSM parity through the C-ABI (the reference's variable_base_msm_gpu_unittest.cc,
+msm_gpu_unittest.cc and msm_benchmark_gpu.cc --check_results): results must be
+bit-exact (affine coordinates) against the CPU oracle on the same inputs."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+CURVES = ["bn254_g1", "bn254_g2", "bls12_381_g1", "bls12_381_g2"]
+_ctx = {}
+
+
+def ctx(curve):
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    if curve not in _ctx:
+        _ctx[curve] = VariableBaseMSMGpu(curve)
+    return _ctx[curve]
+
+
+@pytest.mark.parametrize("curve", CURVES)
+def test_msm_golden(curve):
+    """Golden vectors of the independent Python restatement, incl. edge cases
+    (zero scalars, identity bases, P + (-P), r-1) and the Easy KAT."""
+    g = json.load(open(os.path.join(GOLDEN, "msm.json")))[curve]
+    for c in g["cases"]:
+        bases = b"".join(bytes.fromhex(x) for x in c["bases"])
+        scalars = b"".join(bytes.fromhex(x) for x in c["scalars"])
+        assert ctx(curve).run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
+
+
+def test_msm_zkey_points():
+    z = json.load(open(os.path.join(GOLDEN, "zkey_multiplier_3.json")))
+    for key, curve in (("g1", "bn254_g1"), ("g2", "bn254_g2")):
+        bases = b"".join(bytes.fromhex(x) for x in z[f"{key}_points"])
+        scalars = b"".join(bytes.fromhex(x) for x in z[f"msm_{key}"]["scalars"])
+        assert ctx(curve).run(bases, scalars).hex() == z[f"msm_{key}"]["expected"]
+
+
+def test_reference_entry_points_bn254():
+    """tachyon_bn254_g1_{affine,point2}_msm{,_gpu}: Jacobian result, caller-owned."""
+    import ctypes
+    from tachyon_amd._lib import lib
+    L = lib()
+    for n in (32, 2, 5):  # sizes of msm_gpu_unittest.cc:13-66
+        bases = O.gen_bases("bn254_g1", 100 + n, n, 3).tobytes()
+        scalars = O.gen_scalars("bn254_fr", 100 + n, n).tobytes()
+        expect, _ = O.msm("bn254_g1", bases, scalars, method="naive")
+        for create, run, destroy in (("tachyon_bn254_g1_create_msm_gpu", "tachyon_bn254_g1_affine_msm_gpu",
+                                      "tachyon_bn254_g1_destroy_msm_gpu"),
+                                     ("tachyon_bn254_g1_create_msm_gpu", "tachyon_bn254_g1_point2_msm_gpu",
+                                      "tachyon_bn254_g1_destroy_msm_gpu"),
+                                     ("tachyon_bn254_g1_create_msm", "tachyon_bn254_g1_affine_msm",
+                                      "tachyon_bn254_g1_destroy_msm")):
+            c = getattr(L, create)(0)
+            p = getattr(L, run)(c, bases, scalars, n)
+            jac = ctypes.string_at(p, 96)
+            L.tachyon_mi355x_jacobian_destroy(0, p)
+            getattr(L, destroy)(c)
+            from tachyon_amd.msm import jacobian_to_affine
+            assert jacobian_to_affine("bn254_g1", jac) == expect, (n, run)
+
+
+@pytest.mark.parametrize("logn", [10, 13, 16])
+def test_msm_random_bn254_vs_oracle(logn):
+    n = 1 << logn
+    bases = O.gen_bases("bn254_g1", logn, n, 64).tobytes()
+    scalars = O.gen_scalars("bn254_fr", logn, n).tobytes()
+    expect, _ = O.msm("bn254_g1", bases, scalars)
+    assert ctx("bn254_g1").run(bases, scalars) == expect
+
+
+@pytest.mark.parametrize("curve", ["bn254_g2", "bls12_381_g1", "bls12_381_g2"])
+def test_msm_random_other_curves_vs_oracle(curve):
+    n = 1 << 10  # variable_base_msm_gpu_unittest.cc:25-78 uses 2^10 on all four groups
+    bases = O.gen_bases(curve, 77, n, 32).tobytes()
+    scalars = O.gen_scalars(O.CURVE_INFO[curve][1], 77, n).tobytes()
+    expect, _ = O.msm(curve, bases, scalars)
+    assert ctx(curve).run(bases, scalars) == expect
+
+
+def test_msm_non_uniform_all_equal_scalars():
+    """benchmark --test_set non_uniform = NonUniform(n, 1): every scalar equal, so
+    every window puts all n points in ONE bucket (the skew path)."""
+    n = 1 << 14
+    bases = O.gen_bases("bn254_g1", 9, n, 64).tobytes()
+    one = O.gen_scalars("bn254_fr", 9, 1).tobytes()
+    scalars = one * n
+    expect, _ = O.msm("bn254_g1", bases, scalars)
+    assert ctx("bn254_g1").run(bases, scalars) == expect
+
+
+def test_msm_window_sizes_agree():
+    """Any window size gives the same point (MSMCtx only changes the schedule)."""
+    n = 3000
+    bases = O.gen_bases("bn254_g1", 4, n, 10).tobytes()
+    scalars = O.gen_scalars("bn254_fr", 4, n).tobytes()
+    expect, _ = O.msm("bn254_g1", bases, scalars)
+    m = ctx("bn254_g1")
+    try:
+        for c in (4, 7, 11, 16, 21):
+            m.set_window_bits(c)
+            assert m.run(bases, scalars) == expect, c
+    finally:
+        m.set_window_bits(0)
+
+
+def test_msm_empty_and_single():
+    m = ctx("bn254_g1")
+    assert m.run(b"", b"", n=0) == b"\x00" * 64
+    b1 = O.gen_bases("bn254_g1", 1, 1, 1).tobytes()
+    s1 = O.gen_scalars("bn254_fr", 1, 1).tobytes()
+    assert m.run(b1, s1) == O.msm("bn254_g1", b1, s1)[0]
+
+
+def test_device_generator_matches_oracle():
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    for curve in CURVES:
+        pb, sf = O.CURVE_INFO[curve]
+        n, chunk = 300, 7
+        d_b = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
+        d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+        M.gen_bases(curve, 31, n, chunk, d_b.data_ptr())
+        M.gen_scalars(sf, 31, n, d_s.data_ptr())
+        torch.cuda.synchronize()
+        assert d_b.cpu().numpy().tobytes() == O.gen_bases(curve, 31, n, chunk).tobytes(), curve
+        assert d_s.cpu().numpy().tobytes() == O.gen_scalars(sf, 31, n).tobytes(), curve
+
+
+def test_device_resident_inputs_and_shard_sum():
+    """Device pointers are used in place; MSM(A||B) == MSM(A) + MSM(B) (the
+    kParallelTerm / multi-GPU sharding contract, pippenger_adapter_unittest.cc)."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    n = 1 << 18
+    d_b = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    M.gen_bases("bn254_g1", 5, n, 256, d_b.data_ptr())
+    M.gen_scalars("bn254_fr", 5, n, d_s.data_ptr())
+    torch.cuda.synchronize()
+    m = ctx("bn254_g1")
+    whole = m.run(d_b, d_s)
+    h = n // 2
+    a = m.run(d_b[:h * 64], d_s[:h * 32])
+    b = m.run(d_b[h * 64:], d_s[h * 32:])
+    assert M.affine_sum("bn254_g1", a + b) == whole
+    hb, hs = d_b.cpu().numpy(), d_s.cpu().numpy()
+    assert O.msm_np("bn254_g1", hb, hs) == whole
