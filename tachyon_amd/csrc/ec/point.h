@@ -38,7 +38,15 @@ struct XYZZ {
   }
   TA_HD XYZZ neg() const { return {x, -y, zz, zzz}; }
 
-  // out-of-line doubling for the exceptional P == Q branch of the adds
+  // Doubling for the exceptional P == Q branch of the adds.  For one-word
+  // (32-byte) fields it stays inline: an out-of-line call there makes the
+  // compiler keep the accumulator in scratch (the sret / `this` slots are
+  // addressable), which cost a 272-byte scratch round trip per madd on
+  // MI355X.  Wider fields (Fq2, BLS12-381 Fq) take the call to bound code size.
+  TA_HD XYZZ dbl_slowpath() const {
+    if constexpr (sizeof(F) <= 32) return dbl();
+    else return dbl_outline();
+  }
   TA_HD_NOINLINE XYZZ dbl_outline() const { return dbl(); }
 
   // dbl-2008-s-1 (a = 0)
@@ -64,7 +72,7 @@ struct XYZZ {
     if (is_zero()) return from_affine(b);
     F p = b.x * zz - x;
     F r = b.y * zzz - y;
-    if (p.is_zero() && r.is_zero()) return dbl_outline();
+    if (p.is_zero() && r.is_zero()) return dbl_slowpath();
     F pp = p.sqr();
     F ppp = p * pp;
     F q = x * pp;
@@ -84,7 +92,7 @@ struct XYZZ {
     F s1 = y * b.zzz;
     F p = b.x * zz - u1;
     F r = b.y * zzz - s1;
-    if (p.is_zero() && r.is_zero()) return dbl_outline();
+    if (p.is_zero() && r.is_zero()) return dbl_slowpath();
     F pp = p.sqr();
     F ppp = p * pp;
     F q = u1 * pp;

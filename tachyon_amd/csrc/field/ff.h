@@ -16,6 +16,7 @@
 #include <cstdint>
 
 #include "constants.h"
+#include "mont_asm.h"
 
 #define TA_HD __host__ __device__ __forceinline__
 // Rarely-executed or very large bodies stay out of line: inlining every
@@ -119,8 +120,22 @@ struct Fp {
   }
   TA_HD_NOINLINE Fp mul_outline(const Fp& b) const { return mul_inline(b); }
 
-  // CIOS no-carry Montgomery product (DoFastMul, prime_field_fallback.h:331-355).
   TA_HD Fp mul_inline(const Fp& b) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // device: FIPS with hand-scheduled v_mad_u64_u32 carry chains (mont_asm.h)
+    Fp r;
+    if constexpr (N == 8) detail::mont_mul_fips_8<Cfg>(r.v, v, b.v);
+    else detail::mont_mul_fips_12<Cfg>(r.v, v, b.v);
+    reduce_once(r.v);
+    return r;
+#else
+    return mul_cios(b);
+#endif
+  }
+
+  // CIOS no-carry Montgomery product (DoFastMul, prime_field_fallback.h:331-355);
+  // the host path (final Horner step, conversions).
+  TA_HD Fp mul_cios(const Fp& b) const {
     uint32_t t[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) t[i] = 0;
