@@ -96,6 +96,7 @@ class MsmGpu {
   void set_profile(bool on) { profile_ = on; }
   const MsmTimings& timings() const { return timings_; }
   hipStream_t stream() const { return stream_; }
+  unsigned last_levels() const { return last_levels_; }
 
  private:
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
@@ -108,6 +109,9 @@ class MsmGpu {
   DeviceBuffer bases_, scalars_, keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_;
   DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_;
   hipEvent_t ev_[8] = {};
+  DeviceBuffer maxlen_;
+  uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
+  unsigned last_levels_ = 0;
 };
 
 extern template class MsmGpu<Bn254G1>;

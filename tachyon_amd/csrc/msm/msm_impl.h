@@ -85,12 +85,27 @@ __global__ __launch_bounds__(kBlock) void bounds_kernel(const uint32_t* __restri
 __global__ __launch_bounds__(kBlock) void chunk_count_kernel(const uint32_t* __restrict__ start,
                                                              const uint32_t* __restrict__ end,
                                                              size_t nb, unsigned K,
-                                                             uint32_t* __restrict__ cnt) {
+                                                             uint32_t* __restrict__ cnt,
+                                                             uint32_t* __restrict__ max_len) {
   size_t b = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  if (b > nb) return;
-  if (b == nb) { cnt[b] = 0; return; }
-  uint32_t len = end[b] - start[b];
-  cnt[b] = (len + K - 1) / K;
+  uint32_t len = 0;
+  if (b < nb) {
+    len = end[b] - start[b];
+    cnt[b] = (len + K - 1) / K;
+  } else if (b == nb) {
+    cnt[b] = 0;
+  }
+  // largest bucket -> the host sizes the partial-reduction tree (one 4-byte
+  // read-back instead of a worst-case tree for every input)
+  __shared__ uint32_t red[kBlock / 64];
+  for (int o = 32; o > 0; o >>= 1) len = max(len, (uint32_t)__shfl_xor(len, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = len;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t m = red[0];
+    for (unsigned w = 1; w < kBlock / 64; ++w) m = max(m, red[w]);
+    if (m) atomicMax(max_len, m);
+  }
 }
 
 // chunk counts of the next reduction level from the current offsets
@@ -240,11 +255,13 @@ MsmGpu<Curve>::MsmGpu(hipStream_t stream) : stream_(stream) {
     own_stream_ = true;
   }
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
+  TA_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_max_), 4, hipHostMallocDefault));
 }
 
 template <class Curve>
 MsmGpu<Curve>::~MsmGpu() {
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+  if (h_max_) (void)hipHostFree(h_max_);
   if (own_stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -286,10 +303,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // ---- bucket bounds and chunking ----
   TA_HIP(hipMemsetAsync(start, 0, nb * 4, stream_));
   TA_HIP(hipMemsetAsync(end, 0, nb * 4, stream_));
+  uint32_t* d_max = static_cast<uint32_t*>(maxlen_.ensure(4));
+  TA_HIP(hipMemsetAsync(d_max, 0, 4, stream_));
   hipLaunchKernelGGL(bounds_kernel, dim3(grid_for(entries)), dim3(kBlock), 0, stream_, keys2, (uint32_t)n, W, B,
                      start, end);
   hipLaunchKernelGGL(chunk_count_kernel, dim3(grid_for(nb + 1)), dim3(kBlock), 0, stream_, start, end, nb, plan.K,
-                     cnt);
+                     cnt, d_max);
+  TA_HIP(hipMemcpyAsync(h_max_, d_max, 4, hipMemcpyDeviceToHost, stream_));
   size_t scan_bytes = 0;
   TA_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, cnt, off_a, 0u, nb + 1, rocprim::plus<uint32_t>(), stream_));
   void* scan_tmp = scan_tmp_.ensure(scan_bytes);
@@ -308,10 +328,16 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));
 
   // ---- reduce chunk partials per bucket ----
+  // levels needed for the largest bucket (the sync overlaps the acc kernel)
+  TA_HIP(hipStreamSynchronize(stream_));
+  unsigned levels = 0;
+  for (size_t chunks = (*h_max_ + plan.K - 1) / plan.K; chunks > 1; chunks = (chunks + plan.K2 - 1) / plan.K2)
+    ++levels;
+  last_levels_ = levels;
   Point* cur = part_a;
   uint32_t* cur_off = off_a;
   size_t cur_max = max_chunks;
-  for (unsigned l = 0; l < plan.levels; ++l) {
+  for (unsigned l = 0; l < levels; ++l) {
     uint32_t* nxt_off = (cur_off == off_a) ? off_b : off_a;
     hipLaunchKernelGGL(level_count_kernel, dim3(grid_for(nb + 1)), dim3(kBlock), 0, stream_, cur_off, nb, plan.K2,
                        cnt);

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_round.sh output directory into markdown:
+kernel-trace stats (top kernels) and per-kernel PMC averages with the gfx950
+FETCH_SIZE correction (x2 for wide coalesced streams, MI355X_MICROARCH.md §HBM)."""
+import collections
+import csv
+import os
+import sys
+
+
+def short(name):
+    base = name.replace("(anonymous namespace)", "anon").split("(")[0]
+    for key in ("acc_kernel", "dif_pass_kernel", "reduce_level_kernel", "window_segment_kernel", "bounds_kernel",
+                "recode_kernel", "reduce_uniform_kernel", "gen_bases_kernel", "gen_scalars_kernel",
+                "chunk_count_kernel", "level_count_kernel", "twiddle_stage_kernel", "twiddle_base_kernel",
+                "segmented_acc_kernel", "fixup_kernel"):
+        if key in base:
+            return key
+    if "rocprim" in base:
+        for key in ("onesweep_histograms", "onesweep_iteration", "radix_sort", "lookback_scan", "scan"):
+            if key in name:
+                return "rocprim::" + key
+        return "rocprim::other"
+    return base.split("::")[-1][:60]
+
+
+def main(d):
+    print(f"# rocprofv3 summary: {d}\n")
+    stats = os.path.join(d, "trace", "run_kernel_stats.csv")
+    if os.path.exists(stats):
+        rows = list(csv.DictReader(open(stats)))
+        print("## Kernel trace (--kernel-trace --stats)\n")
+        print("| kernel | calls | total ms | avg ms | % |")
+        print("|---|---|---|---|---|")
+        for r in rows[:20]:
+            print(f"| {short(r['Name'])} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
+                  f"{float(r['AverageNs']) / 1e6:.4f} | {float(r['Percentage']):.2f} |")
+        print()
+    agg = collections.defaultdict(list)
+    meta = {}
+    for sub in ("fetch", "write", "valu"):
+        p = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        for r in csv.DictReader(open(p)):
+            k = short(r["Kernel_Name"])
+            agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+            meta[k] = (r["VGPR_Count"], r["SGPR_Count"], r["Scratch_Size"], r["LDS_Block_Size"])
+    if agg:
+        print("## PMC (per dispatch averages; separate passes)\n")
+        print("| kernel | VGPR | scratch | LDS | FETCH_SIZE KB (x2 corr.) | WRITE_SIZE KB | SQ_INSTS_VALU | "
+              "VALU busy % | eff. clock GHz |")
+        print("|---|---|---|---|---|---|---|---|---|")
+        for k in sorted({k for k, _ in agg}):
+            def avg(c):
+                v = agg.get((k, c))
+                return sum(v) / len(v) if v else None
+            fetch, write, insts = avg("FETCH_SIZE"), avg("WRITE_SIZE"), avg("SQ_INSTS_VALU")
+            act, busy, grbm = avg("SQ_ACTIVE_INST_VALU"), avg("SQ_BUSY_CYCLES"), avg("GRBM_GUI_ACTIVE")
+            wave = avg("SQ_WAVE_CYCLES")
+            valu = f"{100.0 * act / wave:.1f}" if act and wave else "-"
+            fmt = (lambda x: f"{x:.4g}" if x is not None else "-")
+            v, s, sc, l = meta[k]
+            print(f"| {k} | {v} | {sc} | {l} | {fmt(fetch * 2 if fetch else None)} | {fmt(write)} | {fmt(insts)} | "
+                  f"{valu} | - |")
+        print("\nVALU busy % = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of wave-cycles issuing VALU).")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
