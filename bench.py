@@ -112,10 +112,9 @@ def main():
         torch.cuda.synchronize()
 
     # ---- MSM inputs (device-resident, this rank's shard) ----
+    from tachyon_amd import dist as D
     n_total = 1 << args.log_n
-    shard = (n_total + world - 1) // world
-    start = rank * shard
-    n = max(0, min(shard, n_total - start))
+    start, n = D.shard_range(n_total, rank, world)
     d_bases = torch.empty(max(1, n) * 64, dtype=torch.uint8, device="cuda")
     d_scalars = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
     chunk = 1 << 10
@@ -128,13 +127,7 @@ def main():
         msm.set_window_bits(args.window_bits)
 
     def step():
-        part = msm.run(d_bases, d_scalars, n)
-        if dist is None:
-            return part
-        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda()
-        g = torch.empty(world * 64, dtype=torch.uint8, device="cuda")
-        dist.all_gather_into_tensor(g, t)
-        return M.affine_sum("bn254_g1", g.cpu().numpy().tobytes())
+        return D.sharded_msm("bn254_g1", lambda: msm.run(d_bases, d_scalars, n), device="cuda")
 
     for _ in range(args.warmup):
         ref = step()

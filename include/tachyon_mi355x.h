@@ -214,6 +214,8 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const 
                                                     size_t size, void* out_affine);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
+/* kernel-variant bits for A/B tuning in one process (0 = default schedule) */
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
  * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total, 0 (8 floats) */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8);

@@ -291,6 +291,9 @@ void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c) {
 void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on) {
   GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_profile(on != 0)) GUARD_END
 }
+void tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_variant(variant)) GUARD_END
+}
 void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8) {
   GUARD_BEGIN CURVE_DISPATCH(curve, {
     const msm::MsmTimings& t = static_cast<const MsmCtx<C>*>(ctx)->impl.timings();

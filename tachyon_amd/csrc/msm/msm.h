@@ -93,6 +93,8 @@ class MsmGpu {
   static Point combine_windows(const std::vector<Point>& window_sums, unsigned c);
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
+  // kernel-variant bits for in-process A/B tuning (0 = default)
+  void set_variant(int v) { variant_ = v; }
   void set_profile(bool on) { profile_ = on; }
   const MsmTimings& timings() const { return timings_; }
   hipStream_t stream() const { return stream_; }
@@ -105,6 +107,7 @@ class MsmGpu {
   bool own_stream_ = false;
   bool profile_ = false;
   unsigned force_c_ = 0;
+  int variant_ = 0;
   MsmTimings timings_;
   DeviceBuffer bases_, scalars_, keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_;
   DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_;

@@ -130,8 +130,8 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ of
 
 // Bucket accumulation: thread t owns chunk t of bucket b = find_segment(off, t)
 // and sums up to K signed affine bases into an XYZZ partial with madd-2008-s.
-template <class Curve>
-__global__ __launch_bounds__(kBlock) void acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
+template <class Curve, int kMinWaves>
+__global__ __launch_bounds__(kBlock, kMinWaves) void acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
                                                      const uint32_t* __restrict__ vals, uint32_t n,
                                                      unsigned B, const uint32_t* __restrict__ start,
                                                      const uint32_t* __restrict__ end,
@@ -148,16 +148,19 @@ __global__ __launch_bounds__(kBlock) void acc_kernel(const Affine<typename Curve
   uint32_t e0 = start[b] + q * K;
   uint32_t e1 = min(end[b], e0 + K);
   XYZZ<F> acc = XYZZ<F>::zero();
+  // Two-deep software pipeline: the point index for e+2 and the base for e+1
+  // are in flight while the madd for e runs, so neither the (L2-served) index
+  // load nor the (HBM) 64-byte base gather sits on the critical path.
   uint32_t v = wv[e0];
+  uint32_t v1 = (e0 + 1 < e1) ? wv[e0 + 1] : v;
   Affine<F> P = bases[v & ~kSignBit];
   for (uint32_t e = e0; e < e1; ++e) {
-    // software prefetch of the next base while this madd runs
-    uint32_t vn = (e + 1 < e1) ? wv[e + 1] : v;
-    Affine<F> Pn = bases[vn & ~kSignBit];
-    Affine<F> Q = P;
-    if ((v & kSignBit) && !Q.is_zero()) Q.y = -Q.y;
-    acc = acc.madd(Q);
-    v = vn;
+    uint32_t v2 = (e + 2 < e1) ? wv[e + 2] : v1;
+    Affine<F> Pn = bases[v1 & ~kSignBit];
+    if ((v & kSignBit) && !P.is_zero()) P.y = -P.y;
+    acc = acc.madd(P);
+    v = v1;
+    v1 = v2;
     P = Pn;
   }
   out[t] = acc;
@@ -322,7 +325,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // kernels still read it
   Point* part_a = static_cast<Point*>(part_a_.ensure(max_chunks * sizeof(Point)));
   Point* part_b = static_cast<Point*>(part_b_.ensure((max_chunks / plan.K2 + nb + 1) * sizeof(Point)));
-  hipLaunchKernelGGL(acc_kernel<Curve>, dim3(grid_for(max_chunks)), dim3(kBlock), 0, stream_, d_bases, vals2,
+  auto acc_fn = (variant_ & 1) ? acc_kernel<Curve, 4> : acc_kernel<Curve, 1>;
+  hipLaunchKernelGGL(acc_fn, dim3(grid_for(max_chunks)), dim3(kBlock), 0, stream_, d_bases, vals2,
                      (uint32_t)n, B, start, end, off_a, (uint32_t)nb, plan.K, part_a);
   TA_HIP(hipGetLastError());
   if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));

@@ -1,0 +1,51 @@
+"""One-process-per-GPU sharding of the MSM (torch.distributed; backend "nccl" = RCCL).
+
+The reference's kParallelTerm strategy (pippenger_adapter.h:82-113) splits the
+points into contiguous chunks, runs one Pippenger per chunk and adds the chunk
+results; the multi-GPU MSM is the same decomposition with one chunk per rank.
+The only exchange is one all-gather of the per-rank partial points (affine,
+64 B for BN254 G1) followed by a group sum on every rank -- elliptic-curve
+addition is not an RCCL reduction operator.
+"""
+from typing import Callable
+
+import numpy as np
+
+from ._lib import CURVE_INFO
+from .msm import affine_sum
+
+
+def shard_range(n_total: int, rank: int, world: int):
+    """Contiguous shard [start, start + n) of rank (ceil split, like
+    base::ParallelizeMap's ceil(n / T) chunking)."""
+    chunk = (n_total + world - 1) // world
+    start = min(rank * chunk, n_total)
+    return start, max(0, min(chunk, n_total - start))
+
+
+def combine_partials(curve: str, partials: bytes) -> bytes:
+    """Sum of the per-rank affine partials (host group arithmetic of the product library)."""
+    return affine_sum(curve, partials)
+
+
+def all_gather_partials(curve: str, partial: bytes, group=None, device=None) -> bytes:
+    """All-gather every rank's affine partial; returns the concatenation in rank order."""
+    import torch
+    import torch.distributed as dist
+    pb = CURVE_INFO[curve][0]
+    world = dist.get_world_size(group)
+    t = torch.frombuffer(bytearray(partial), dtype=torch.uint8)
+    if device is not None:
+        t = t.to(device)
+    out = torch.empty(world * pb, dtype=torch.uint8, device=t.device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return out.cpu().numpy().tobytes()
+
+
+def sharded_msm(curve: str, local_msm: Callable[[], bytes], group=None, device=None) -> bytes:
+    """Run `local_msm()` (this rank's shard -> affine partial) and combine across ranks."""
+    import torch.distributed as dist
+    part = local_msm()
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return part
+    return combine_partials(curve, all_gather_partials(curve, part, group, device))

@@ -99,6 +99,9 @@ class VariableBaseMSMGpu:
     def set_profile(self, on: bool):
         lib().tachyon_mi355x_msm_gpu_set_profile(self.curve_id, self._ctx, 1 if on else 0)
 
+    def set_variant(self, variant: int):
+        lib().tachyon_mi355x_msm_gpu_set_variant(self.curve_id, self._ctx, variant)
+
     def last_timings(self) -> dict:
         out = (ctypes.c_float * 8)()
         lib().tachyon_mi355x_msm_gpu_last_timings(self.curve_id, self._ctx, out)

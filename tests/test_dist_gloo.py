@@ -1,0 +1,71 @@
+"""Multi-rank MSM sharding on CPU (gloo, world_size 2): the shard split, the
+all-gather of per-rank partial points and the product's host-side group sum
+(tachyon_mi355x_affine_sum, no GPU needed) reproduce the single-process MSM.
+The per-rank local MSM is the oracle here (the CPU box has no GPU); on the GPU
+box bench.py runs the same code with the HIP MSM and RCCL."""
+import os
+import socket
+
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tachyon_amd",
+                   "libtachyon_mi355x.so")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, curve, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from tachyon_amd import dist as D
+        pb, sf = O.CURVE_INFO[curve]
+        bases = O.gen_bases(curve, 99, n, 16).tobytes()
+        scalars = O.gen_scalars(sf, 99, n).tobytes()
+        start, m = D.shard_range(n, rank, world)
+        local = lambda: O.msm(curve, bases[start * pb:(start + m) * pb], scalars[start * 32:(start + m) * 32])[0]
+        got = D.sharded_msm(curve, local)
+        if rank == 0:
+            q.put((got, O.msm(curve, bases, scalars)[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libtachyon_mi355x.so not built")
+@pytest.mark.parametrize("curve,n", [("bn254_g1", 301), ("bls12_381_g1", 64)])
+def test_sharded_msm_world2(curve, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, curve, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, expect = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == expect
+
+
+def test_shard_range_covers():
+    from tachyon_amd.dist import shard_range
+    for n in (0, 1, 7, 64, 1 << 26):
+        for world in (1, 2, 3, 4, 8):
+            spans = [shard_range(n, r, world) for r in range(world)]
+            assert sum(m for _, m in spans) == n
+            pos = 0
+            for s, m in spans:
+                if m:
+                    assert s == pos
+                pos = s + m if m else pos

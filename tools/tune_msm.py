@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--c", type=int, nargs="+", default=[0])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--non-uniform", action="store_true")
+    ap.add_argument("--variants", type=int, nargs="+", default=[0])
+    ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
     import torch
     from tachyon_amd import msm as M
@@ -35,8 +37,9 @@ def main():
         torch.cuda.synchronize()
         m = M.VariableBaseMSMGpu("bn254_g1")
         ref = None
-        for c in args.c:
+        for c, var in [(c, v) for _ in range(args.rounds) for c in args.c for v in args.variants]:
             m.set_window_bits(c)
+            m.set_variant(var)
             m.set_profile(True)
             res = m.run(d_b, d_s)
             ref = ref or res
@@ -48,7 +51,7 @@ def main():
                 times.append(m.last_timings())
                 assert r == ref
             best = min(range(args.reps), key=lambda i: walls[i])
-            print(json.dumps({"log_n": lg, "c": c or M.plan("bn254_g1", n)[0], "wall_ms": round(walls[best], 3),
+            print(json.dumps({"log_n": lg, "c": c or M.plan("bn254_g1", n)[0], "variant": var, "wall_ms": round(walls[best], 3),
                               **{k: round(v, 3) for k, v in times[best].items()}}), flush=True)
         m.close()
 
