@@ -20,6 +20,8 @@ namespace {  // internal linkage: every per-curve TU gets its own copy
 
 constexpr unsigned kBlock = 256;
 constexpr uint32_t kSignBit = 0x80000000u;
+constexpr uint32_t kNoBucket = 0xFFFFFFFFu;
+enum : uint32_t { kHead = 1, kTail = 2, kSingle = 4 };
 
 // ---------------------------------------------------------------------------
 // recode: Montgomery scalar -> canonical -> signed base-2^c digits
@@ -63,64 +65,156 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
   }
 }
 
-// bucket [start, end) per (window, |digit|) from the sorted keys
-__global__ __launch_bounds__(kBlock) void bounds_kernel(const uint32_t* __restrict__ keys, uint32_t n,
-                                                        unsigned W, unsigned B,
-                                                        uint32_t* __restrict__ start,
-                                                        uint32_t* __restrict__ end) {
-  size_t p = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  size_t total = (size_t)n * W;
-  if (p >= total) return;
-  uint32_t w = (uint32_t)(p / n);
-  uint32_t q = (uint32_t)(p - (size_t)w * n);
-  uint32_t k = keys[p];
-  if (k == 0) return;
-  size_t b = (size_t)w * B + (k - 1);
-  // positions are stored window-relative offsets into the window's slice
-  if (q == 0 || keys[p - 1] != k) start[b] = (uint32_t)q;
-  if (q == n - 1 || keys[p + 1] != k) end[b] = (uint32_t)q + 1;
+// ---------------------------------------------------------------------------
+// Load-balanced bucket accumulation.
+//
+// The per-window sorted (bucket, point) lists are one array of W*n entries,
+// ordered by (window, bucket).  Thread t owns entries [t*K, (t+1)*K) -- every
+// lane runs exactly K mixed additions whatever the bucket sizes (a bucket per
+// lane left lanes idle for the longest bucket of their wave).  A run of equal
+// buckets inside the range is summed with madd-2008-s (XYZZ += +-affine):
+//   * a run that starts and ends inside the range is that bucket's whole sum
+//     -> stored straight to bucket_sum[b] (the only writer);
+//   * the first run, if the bucket started in an earlier thread ("head"), and
+//     the last run, if it continues into the next thread ("tail"), go to
+//     pieces[2t] / pieces[2t+1] and are joined by the chain kernels below.
+template <class Curve>
+__global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
+                                                         const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ vals, uint32_t n, uint32_t B,
+                                                         uint64_t total, uint32_t K,
+                                                         XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+                                                         XYZZ<typename Curve::F>* __restrict__ pieces,
+                                                         uint32_t* __restrict__ tflags,
+                                                         uint32_t* __restrict__ tlast) {
+  using F = typename Curve::F;
+  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t g0 = t * K;
+  if (g0 >= total) return;
+  const uint64_t g1 = min(g0 + K, total);
+  auto bucket_of = [&](uint64_t g) -> uint32_t {
+    uint32_t k = keys[g];
+    return k ? (uint32_t)(g / n) * B + (k - 1) : kNoBucket;
+  };
+  const uint32_t prev_b = g0 ? bucket_of(g0 - 1) : kNoBucket;
+  const uint32_t next_b = (g1 < total) ? bucket_of(g1) : kNoBucket;
+  uint32_t w = (uint32_t)(g0 / n);
+  uint64_t wend = (uint64_t)(w + 1) * n;
+
+  uint32_t flags = 0, runs = 0, cur = kNoBucket;
+  XYZZ<F> acc = XYZZ<F>::zero();
+  // two-deep software pipeline: (key, val) for g+2 and the base for g+1 are
+  // in flight while the madd for g runs
+  uint32_t k0 = keys[g0], v0 = vals[g0];
+  uint32_t k1 = 0, v1 = 0;
+  if (g0 + 1 < g1) { k1 = keys[g0 + 1]; v1 = vals[g0 + 1]; }
+  Affine<F> P = bases[v0 & ~kSignBit];
+  for (uint64_t g = g0; g < g1; ++g) {
+    uint32_t k2 = 0, v2 = 0;
+    if (g + 2 < g1) { k2 = keys[g + 2]; v2 = vals[g + 2]; }
+    Affine<F> Pn = bases[v1 & ~kSignBit];
+    if (g == wend) { ++w; wend += n; }
+    if (k0 != 0) {
+      const uint32_t b = w * B + (k0 - 1);
+      if (b != cur) {
+        if (cur != kNoBucket) {  // close a run that is not the last one
+          if (runs == 1 && cur == prev_b) { pieces[2 * t] = acc; flags |= kHead; }
+          else bucket_sum[cur] = acc;
+        }
+        cur = b;
+        ++runs;
+        acc = XYZZ<F>::zero();
+      }
+      if ((v0 & kSignBit) && !P.is_zero()) P.y = -P.y;
+      acc = acc.madd(P);
+    }
+    k0 = k1; v0 = v1; k1 = k2; v1 = v2;
+    P = Pn;
+  }
+  if (cur != kNoBucket) {  // the last run
+    const bool head = runs == 1 && cur == prev_b;
+    const bool tail = cur == next_b;
+    if (head) { pieces[2 * t] = acc; flags |= kHead; }
+    if (tail) flags |= kTail;
+    if (tail && !head) pieces[2 * t + 1] = acc;
+    if (!head && !tail) bucket_sum[cur] = acc;
+  }
+  if (runs <= 1) flags |= kSingle;
+  // absent pieces are the identity so every chain sums a contiguous range
+  if (!(flags & kHead)) pieces[2 * t] = XYZZ<F>::zero();
+  const bool through = (flags & kHead) && (flags & kTail) && (flags & kSingle);
+  if (!(flags & kTail) || through) pieces[2 * t + 1] = XYZZ<F>::zero();
+  tflags[t] = flags;
+  tlast[t] = cur;
 }
 
-// number of accumulation chunks per bucket
-__global__ __launch_bounds__(kBlock) void chunk_count_kernel(const uint32_t* __restrict__ start,
-                                                             const uint32_t* __restrict__ end,
-                                                             size_t nb, unsigned K,
-                                                             uint32_t* __restrict__ cnt,
-                                                             uint32_t* __restrict__ max_len) {
-  size_t b = (size_t)blockIdx.x * kBlock + threadIdx.x;
+// A bucket that crosses thread boundaries forms a chain t0 < ... < t1: the
+// tail of t0, the whole-range heads of the "through" threads in between and
+// the head of t1 -- i.e. pieces[2*t0+1 .. 2*t1] (absent tails are identity).
+__device__ __forceinline__ bool chain_start(uint32_t f) {
+  const bool through = (f & kHead) && (f & kTail) && (f & kSingle);
+  return (f & kTail) && !through;
+}
+__device__ __forceinline__ bool chain_end(uint32_t f) {
+  const bool through = (f & kHead) && (f & kTail) && (f & kSingle);
+  return (f & kHead) && !through;
+}
+
+__global__ __launch_bounds__(kBlock) void chain_mark_kernel(const uint32_t* __restrict__ tflags, uint32_t T,
+                                                            uint32_t* __restrict__ is_start) {
+  uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t > T) return;
+  is_start[t] = (t < T && chain_start(tflags[t])) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void chain_build_kernel(const uint32_t* __restrict__ tflags,
+                                                             const uint32_t* __restrict__ tlast,
+                                                             const uint32_t* __restrict__ cid, uint32_t T,
+                                                             uint32_t* __restrict__ cbeg, uint32_t* __restrict__ cend,
+                                                             uint32_t* __restrict__ cbucket,
+                                                             uint32_t* __restrict__ nchains) {
+  uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= T) return;
+  uint32_t f = tflags[t];
+  if (chain_end(f)) cend[cid[t] - 1] = 2 * t + 1;  // the chain opened by the last start before t
+  if (chain_start(f)) {
+    cbeg[cid[t]] = 2 * t + 1;
+    cbucket[cid[t]] = tlast[t];
+  }
+  if (t == T - 1) nchains[0] = cid[t] + (chain_start(f) ? 1u : 0u);
+}
+
+// per-chain piece count for the first reduction level, and the longest chain
+__global__ __launch_bounds__(kBlock) void seg_count_kernel(const uint32_t* __restrict__ beg,
+                                                           const uint32_t* __restrict__ end,
+                                                           const uint32_t* __restrict__ nseg_ptr, uint32_t nseg_cap,
+                                                           unsigned K2, uint32_t* __restrict__ cnt,
+                                                           uint32_t* __restrict__ max_len) {
+  uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+  const uint32_t nseg = nseg_ptr ? *nseg_ptr : nseg_cap;
   uint32_t len = 0;
-  if (b < nb) {
-    len = end[b] - start[b];
-    cnt[b] = (len + K - 1) / K;
-  } else if (b == nb) {
-    cnt[b] = 0;
+  if (s < nseg) {
+    len = end[s] - beg[s];
+    cnt[s] = (len + K2 - 1) / K2;
+  } else if (s <= nseg_cap) {
+    cnt[s] = 0;
   }
-  // largest bucket -> the host sizes the partial-reduction tree (one 4-byte
-  // read-back instead of a worst-case tree for every input)
-  __shared__ uint32_t red[kBlock / 64];
-  for (int o = 32; o > 0; o >>= 1) len = max(len, (uint32_t)__shfl_xor(len, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = len;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t m = red[0];
-    for (unsigned w = 1; w < kBlock / 64; ++w) m = max(m, red[w]);
-    if (m) atomicMax(max_len, m);
+  if (max_len) {
+    __shared__ uint32_t red[kBlock / 64];
+    for (int o = 32; o > 0; o >>= 1) len = max(len, (uint32_t)__shfl_xor(len, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = len;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t m = red[0];
+      for (unsigned i = 1; i < kBlock / 64; ++i) m = max(m, red[i]);
+      if (m) atomicMax(max_len, m);
+    }
   }
 }
 
-// chunk counts of the next reduction level from the current offsets
-__global__ __launch_bounds__(kBlock) void level_count_kernel(const uint32_t* __restrict__ off, size_t nb,
-                                                             unsigned K2, uint32_t* __restrict__ cnt) {
-  size_t b = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  if (b > nb) return;
-  if (b == nb) { cnt[b] = 0; return; }
-  uint32_t len = off[b + 1] - off[b];
-  cnt[b] = (len + K2 - 1) / K2;
-}
-
-// largest b in [0, nb) with off[b] <= t  (off is non-decreasing, off[nb] = total)
-__device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ off, uint32_t nb, uint32_t t) {
-  uint32_t lo = 0, hi = nb;  // invariant: off[lo] <= t < off[hi]
+// largest s in [0, nseg) with off[s] <= t  (off non-decreasing)
+__device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ off, uint32_t nseg, uint32_t t) {
+  uint32_t lo = 0, hi = nseg;
   while (hi - lo > 1) {
     uint32_t mid = (lo + hi) >> 1;
     if (off[mid] <= t) lo = mid; else hi = mid;
@@ -128,62 +222,28 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ of
   return lo;
 }
 
-// Bucket accumulation: thread t owns chunk t of bucket b = find_segment(off, t)
-// and sums up to K signed affine bases into an XYZZ partial with madd-2008-s.
-template <class Curve, int kMinWaves>
-__global__ __launch_bounds__(kBlock, kMinWaves) void acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
-                                                     const uint32_t* __restrict__ vals, uint32_t n,
-                                                     unsigned B, const uint32_t* __restrict__ start,
-                                                     const uint32_t* __restrict__ end,
-                                                     const uint32_t* __restrict__ off, uint32_t nb,
-                                                     unsigned K, XYZZ<typename Curve::F>* __restrict__ out) {
-  using F = typename Curve::F;
-  uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t total = off[nb];
-  if (t >= total) return;
-  uint32_t b = find_segment(off, nb, t);
-  uint32_t q = t - off[b];
-  uint32_t w = b / B;
-  const uint32_t* wv = vals + (size_t)w * n;
-  uint32_t e0 = start[b] + q * K;
-  uint32_t e1 = min(end[b], e0 + K);
-  XYZZ<F> acc = XYZZ<F>::zero();
-  // Two-deep software pipeline: the point index for e+2 and the base for e+1
-  // are in flight while the madd for e runs, so neither the (L2-served) index
-  // load nor the (HBM) 64-byte base gather sits on the critical path.
-  uint32_t v = wv[e0];
-  uint32_t v1 = (e0 + 1 < e1) ? wv[e0 + 1] : v;
-  Affine<F> P = bases[v & ~kSignBit];
-  for (uint32_t e = e0; e < e1; ++e) {
-    uint32_t v2 = (e + 2 < e1) ? wv[e + 2] : v1;
-    Affine<F> Pn = bases[v1 & ~kSignBit];
-    if ((v & kSignBit) && !P.is_zero()) P.y = -P.y;
-    acc = acc.madd(P);
-    v = v1;
-    v1 = v2;
-    P = Pn;
-  }
-  out[t] = acc;
-}
-
-// One K2-ary reduction level over per-bucket partial lists.
+// One K2-ary level of the segmented tree: output q of segment s is the sum of
+// in[beg[s] + q*K2 .. min(end[s], +K2)).  On the last level every segment has
+// one output, which goes to bucket_sum[bucket[s]].
 template <class Curve>
-__global__ __launch_bounds__(kBlock) void reduce_level_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
-                                                              const uint32_t* __restrict__ in_off,
-                                                              const uint32_t* __restrict__ out_off,
-                                                              uint32_t nb, unsigned K2,
-                                                              XYZZ<typename Curve::F>* __restrict__ out) {
+__global__ __launch_bounds__(kBlock) void seg_reduce_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
+                                                            const uint32_t* __restrict__ beg,
+                                                            const uint32_t* __restrict__ end,
+                                                            const uint32_t* __restrict__ out_off, uint32_t nseg,
+                                                            unsigned K2, XYZZ<typename Curve::F>* __restrict__ out,
+                                                            const uint32_t* __restrict__ bucket,
+                                                            XYZZ<typename Curve::F>* __restrict__ bucket_sum) {
   using F = typename Curve::F;
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t total = out_off[nb];
-  if (t >= total) return;
-  uint32_t b = find_segment(out_off, nb, t);
-  uint32_t q = t - out_off[b];
-  uint32_t e0 = in_off[b] + q * K2;
-  uint32_t e1 = min(in_off[b + 1], e0 + K2);
+  if (t >= out_off[nseg]) return;
+  uint32_t s = find_segment(out_off, nseg, t);
+  uint32_t q = t - out_off[s];
+  uint32_t e0 = beg[s] + q * K2;
+  uint32_t e1 = min(end[s], e0 + K2);
   XYZZ<F> acc = in[e0];
   for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc + in[e];
-  out[t] = acc;
+  if (bucket) bucket_sum[bucket[s]] = acc;
+  else out[t] = acc;
 }
 
 // m * P for a small non-negative integer m (double-and-add, high bit first)
@@ -206,8 +266,7 @@ __device__ XYZZ<F> small_mul(const XYZZ<F>& P, uint32_t m) {
 // sum_b (b+1) B_b is S + jL * R  (PippengerBase::AccumulateBuckets,
 // pippenger_base.h:36-57, split across threads).
 template <class Curve>
-__global__ __launch_bounds__(kBlock) void window_segment_kernel(const XYZZ<typename Curve::F>* __restrict__ pts,
-                                                                const uint32_t* __restrict__ off,
+__global__ __launch_bounds__(kBlock) void window_segment_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                                 unsigned W, unsigned B, unsigned L,
                                                                 XYZZ<typename Curve::F>* __restrict__ out) {
   using F = typename Curve::F;
@@ -215,12 +274,10 @@ __global__ __launch_bounds__(kBlock) void window_segment_kernel(const XYZZ<typen
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= W * S) return;
   uint32_t w = t / S, j = t - w * S;
-  uint32_t base = w * B + j * L;
+  const XYZZ<F>* bs = bucket_sum + (size_t)w * B + (size_t)j * L;
   XYZZ<F> R = XYZZ<F>::zero(), acc = XYZZ<F>::zero();
   for (int k = (int)L - 1; k >= 0; --k) {
-    uint32_t b = base + k;
-    uint32_t o0 = off[b], o1 = off[b + 1];
-    if (o1 > o0) R = R + pts[o0];
+    R = R + bs[k];
     acc = acc + R;
   }
   acc = acc + small_mul(R, j * L);
@@ -258,7 +315,7 @@ MsmGpu<Curve>::MsmGpu(hipStream_t stream) : stream_(stream) {
     own_stream_ = true;
   }
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
-  TA_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_max_), 4, hipHostMallocDefault));
+  TA_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_max_), 2 * sizeof(uint32_t), hipHostMallocDefault));
 }
 
 template <class Curve>
@@ -275,16 +332,29 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   const size_t entries = n * W;
   const size_t nb = (size_t)W * B;
   if (n >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM size must be < 2^31 per device");
+  const uint32_t K = plan.K;
+  const size_t T = (entries + K - 1) / K;  // accumulation threads
+  if (T >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM too large for the chunking");
 
   uint32_t* keys = static_cast<uint32_t*>(keys_.ensure(entries * 4));
   uint32_t* vals = static_cast<uint32_t*>(vals_.ensure(entries * 4));
   uint32_t* keys2 = static_cast<uint32_t*>(keys2_.ensure(entries * 4));
   uint32_t* vals2 = static_cast<uint32_t*>(vals2_.ensure(entries * 4));
-  uint32_t* start = static_cast<uint32_t*>(start_.ensure(nb * 4));
-  uint32_t* end = static_cast<uint32_t*>(end_.ensure(nb * 4));
-  uint32_t* cnt = static_cast<uint32_t*>(cnt_.ensure((nb + 1) * 4));
-  uint32_t* off_a = static_cast<uint32_t*>(off_a_.ensure((nb + 1) * 4));
-  uint32_t* off_b = static_cast<uint32_t*>(off_b_.ensure((nb + 1) * 4));
+  Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * sizeof(Point)));
+  Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * sizeof(Point)));
+  Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / plan.K2 + T + 2) * sizeof(Point)));
+  uint32_t* tflags = static_cast<uint32_t*>(start_.ensure(T * 4));
+  uint32_t* tlast = static_cast<uint32_t*>(end_.ensure(T * 4));
+  uint32_t* is_start = static_cast<uint32_t*>(cnt_.ensure((T + 1) * 4));
+  uint32_t* cid = static_cast<uint32_t*>(off_a_.ensure((T + 1) * 4));
+  // chain tables: beg, end, bucket, level counts/offsets (<= T chains)
+  uint32_t* ctab = static_cast<uint32_t*>(off_b_.ensure((5 * (T + 2) + 4) * 4));
+  uint32_t* cbeg = ctab;
+  uint32_t* cend = ctab + (T + 2);
+  uint32_t* cbucket = ctab + 2 * (T + 2);
+  uint32_t* lcnt = ctab + 3 * (T + 2);
+  uint32_t* loff = ctab + 4 * (T + 2);
+  uint32_t* dscal = ctab + 5 * (T + 2);  // [0] nchains, [1] max chain length
 
   if (profile_) TA_HIP(hipEventRecord(ev_[1], stream_));
   hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
@@ -303,66 +373,73 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   }
   if (profile_) TA_HIP(hipEventRecord(ev_[3], stream_));
 
-  // ---- bucket bounds and chunking ----
-  TA_HIP(hipMemsetAsync(start, 0, nb * 4, stream_));
-  TA_HIP(hipMemsetAsync(end, 0, nb * 4, stream_));
-  uint32_t* d_max = static_cast<uint32_t*>(maxlen_.ensure(4));
-  TA_HIP(hipMemsetAsync(d_max, 0, 4, stream_));
-  hipLaunchKernelGGL(bounds_kernel, dim3(grid_for(entries)), dim3(kBlock), 0, stream_, keys2, (uint32_t)n, W, B,
-                     start, end);
-  hipLaunchKernelGGL(chunk_count_kernel, dim3(grid_for(nb + 1)), dim3(kBlock), 0, stream_, start, end, nb, plan.K,
-                     cnt, d_max);
-  TA_HIP(hipMemcpyAsync(h_max_, d_max, 4, hipMemcpyDeviceToHost, stream_));
-  size_t scan_bytes = 0;
-  TA_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, cnt, off_a, 0u, nb + 1, rocprim::plus<uint32_t>(), stream_));
-  void* scan_tmp = scan_tmp_.ensure(scan_bytes);
-  TA_HIP(rocprim::exclusive_scan(scan_tmp, scan_bytes, cnt, off_a, 0u, nb + 1, rocprim::plus<uint32_t>(), stream_));
-
-  // ---- accumulation ----
+  // ---- accumulation (every bucket without an entry stays the identity) ----
+  TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * sizeof(Point), stream_));
+  TA_HIP(hipMemsetAsync(dscal, 0, 2 * sizeof(uint32_t), stream_));
   if (profile_) TA_HIP(hipEventRecord(ev_[6], stream_));
-  size_t max_chunks = entries / plan.K + nb + 1;
-  // size both ping-pong buffers up front: nothing may be freed while queued
-  // kernels still read it
-  Point* part_a = static_cast<Point*>(part_a_.ensure(max_chunks * sizeof(Point)));
-  Point* part_b = static_cast<Point*>(part_b_.ensure((max_chunks / plan.K2 + nb + 1) * sizeof(Point)));
-  auto acc_fn = (variant_ & 1) ? acc_kernel<Curve, 4> : acc_kernel<Curve, 1>;
-  hipLaunchKernelGGL(acc_fn, dim3(grid_for(max_chunks)), dim3(kBlock), 0, stream_, d_bases, vals2,
-                     (uint32_t)n, B, start, end, off_a, (uint32_t)nb, plan.K, part_a);
+  hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(T)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2,
+                     (uint32_t)n, B, (uint64_t)entries, K, bucket_sum, pieces, tflags, tlast);
   TA_HIP(hipGetLastError());
   if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));
 
-  // ---- reduce chunk partials per bucket ----
-  // levels needed for the largest bucket (the sync overlaps the acc kernel)
+  // ---- join buckets that cross thread boundaries ----
+  hipLaunchKernelGGL(chain_mark_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, stream_, tflags, (uint32_t)T,
+                     is_start);
+  size_t scan_bytes = 0;
+  TA_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, is_start, cid, 0u, T + 1, rocprim::plus<uint32_t>(), stream_));
+  void* scan_tmp = scan_tmp_.ensure(scan_bytes);
+  TA_HIP(rocprim::exclusive_scan(scan_tmp, scan_bytes, is_start, cid, 0u, T + 1, rocprim::plus<uint32_t>(), stream_));
+  hipLaunchKernelGGL(chain_build_kernel, dim3(grid_for(T)), dim3(kBlock), 0, stream_, tflags, tlast, cid,
+                     (uint32_t)T, cbeg, cend, cbucket, dscal);
+  hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, stream_, cbeg, cend, dscal,
+                     (uint32_t)T, plan.K2, lcnt, dscal + 1);
+  TA_HIP(hipMemcpyAsync(h_max_, dscal, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   TA_HIP(hipStreamSynchronize(stream_));
+  const uint32_t nchains = h_max_[0], max_len = h_max_[1];
   unsigned levels = 0;
-  for (size_t chunks = (*h_max_ + plan.K - 1) / plan.K; chunks > 1; chunks = (chunks + plan.K2 - 1) / plan.K2)
-    ++levels;
+  for (size_t len = max_len; len > 1; len = (len + plan.K2 - 1) / plan.K2) ++levels;
   last_levels_ = levels;
-  Point* cur = part_a;
-  uint32_t* cur_off = off_a;
-  size_t cur_max = max_chunks;
-  for (unsigned l = 0; l < levels; ++l) {
-    uint32_t* nxt_off = (cur_off == off_a) ? off_b : off_a;
-    hipLaunchKernelGGL(level_count_kernel, dim3(grid_for(nb + 1)), dim3(kBlock), 0, stream_, cur_off, nb, plan.K2,
-                       cnt);
-    TA_HIP(rocprim::exclusive_scan(scan_tmp, scan_bytes, cnt, nxt_off, 0u, nb + 1, rocprim::plus<uint32_t>(),
-                                   stream_));
-    size_t nxt_max = cur_max / plan.K2 + nb + 1;
-    Point* nxt = (cur == part_a) ? part_b : part_a;
-    hipLaunchKernelGGL(reduce_level_kernel<Curve>, dim3(grid_for(nxt_max)), dim3(kBlock), 0, stream_, cur, cur_off,
-                       nxt_off, (uint32_t)nb, plan.K2, nxt);
-    TA_HIP(hipGetLastError());
-    cur = nxt;
-    cur_off = nxt_off;
-    cur_max = nxt_max;
+  if (nchains > 0) {
+    size_t scan2_bytes = 0;
+    TA_HIP(rocprim::exclusive_scan(nullptr, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
+                                   rocprim::plus<uint32_t>(), stream_));
+    if (scan2_bytes > scan_bytes) scan_tmp = scan_tmp_.ensure(scan2_bytes);  // (nchains <= T: never grows)
+    const Point* cur = pieces;
+    const uint32_t* cur_beg = cbeg;
+    const uint32_t* cur_end = cend;
+    size_t cur_items = 2 * T;
+    Point* dst_bufs[2] = {lvl_buf, pieces};  // pieces is free once level 0 has read it
+    for (unsigned l = 0; l < levels; ++l) {
+      const bool last = (l + 1 == levels);
+      if (l > 0)
+        hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, stream_, cur_beg,
+                           cur_end, nullptr, nchains, plan.K2, lcnt, nullptr);
+      TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
+                                     rocprim::plus<uint32_t>(), stream_));
+      size_t out_items = cur_items / plan.K2 + nchains + 1;
+      Point* dst = dst_bufs[l & 1];
+      hipLaunchKernelGGL(seg_reduce_kernel<Curve>, dim3(grid_for(out_items)), dim3(kBlock), 0, stream_, cur, cur_beg,
+                         cur_end, loff, nchains, plan.K2, dst, last ? cbucket : nullptr, bucket_sum);
+      TA_HIP(hipGetLastError());
+      if (!last) {
+        // next level reads this level's compact output: segment s = [loff[s], loff[s+1])
+        // (copy the offsets: lcnt/loff are rewritten by the next level)
+        uint32_t* nbeg = cbeg;  // the chain begin/end tables are no longer needed after level 0
+        TA_HIP(hipMemcpyAsync(nbeg, loff, ((size_t)nchains + 1) * 4, hipMemcpyDeviceToDevice, stream_));
+        cur_beg = nbeg;
+        cur_end = nbeg + 1;
+        cur = dst;
+        cur_items = out_items;
+      }
+    }
   }
 
   // ---- window sums ----
   unsigned S = B / plan.seg;
   Point* seg_a = static_cast<Point*>(seg_a_.ensure((size_t)W * S * sizeof(Point)));
   Point* seg_b = static_cast<Point*>(seg_b_.ensure((size_t)W * S * sizeof(Point)));
-  hipLaunchKernelGGL(window_segment_kernel<Curve>, dim3(grid_for((size_t)W * S)), dim3(kBlock), 0, stream_, cur,
-                     cur_off, W, B, plan.seg, seg_a);
+  hipLaunchKernelGGL(window_segment_kernel<Curve>, dim3(grid_for((size_t)W * S)), dim3(kBlock), 0, stream_,
+                     bucket_sum, W, B, plan.seg, seg_a);
   TA_HIP(hipGetLastError());
   Point* s_cur = seg_a;
   Point* s_nxt = seg_b;
@@ -375,7 +452,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     std::swap(s_cur, s_nxt);
     S = S_out;
   }
-  if (s_cur == seg_a && S == 1 && B / plan.seg == 1) {
+  if (B / plan.seg == 1) {
     TA_HIP(hipMemcpyAsync(d_windows, seg_a, W * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
   }
   if (profile_) TA_HIP(hipEventRecord(ev_[5], stream_));
@@ -437,6 +514,5 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* 
   if (n == 0) return Point::zero();
   return combine_windows(ws, plan.c);
 }
-
 
 }  // namespace tachyon_amd::msm
