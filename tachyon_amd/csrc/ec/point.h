@@ -17,6 +17,7 @@ struct Affine {
   TA_HD bool is_zero() const { return x.is_zero() && y.is_zero(); }
   TA_HD static Affine zero() { return {F::zero(), F::zero()}; }
   TA_HD Affine neg() const { return is_zero() ? *this : Affine{x, -y}; }
+  TA_HD Affine canonical() const { return {x.canonical(), y.canonical()}; }
 };
 
 template <class F>
@@ -24,6 +25,7 @@ struct Jacobian {
   F x, y, z;
   TA_HD bool is_zero() const { return z.is_zero(); }
   TA_HD static Jacobian zero() { return {F::one(), F::one(), F::zero()}; }
+  TA_HD Jacobian canonical() const { return {x.canonical(), y.canonical(), z.canonical()}; }
 };
 
 template <class F>
@@ -37,6 +39,7 @@ struct XYZZ {
     return {a.x, a.y, F::one(), F::one()};
   }
   TA_HD XYZZ neg() const { return {x, -y, zz, zzz}; }
+  TA_HD XYZZ canonical() const { return {x.canonical(), y.canonical(), zz.canonical(), zzz.canonical()}; }
 
   // Doubling for the exceptional P == Q branch of the adds.  For one-word
   // (32-byte) fields it stays inline: an out-of-line call there makes the
@@ -107,10 +110,10 @@ struct XYZZ {
   // point_xyzz.h:199-212
   TA_HD_NOINLINE Affine<F> to_affine() const {
     if (is_zero()) return Affine<F>::zero();
-    if (zz.is_one()) return {x, y};
+    if (zz.is_one()) return Affine<F>{x, y}.canonical();
     F zinv3 = zzz.inverse();
     F zinv2 = (zinv3 * zz).sqr();
-    return {x * zinv2, y * zinv3};
+    return Affine<F>{x * zinv2, y * zinv3}.canonical();
   }
 
   // point_xyzz.h:228-237

@@ -5,12 +5,17 @@
 // [0, p), little-endian limbs -- so a tachyon_bn254_fq {uint64_t limbs[4]} is
 // bit-identical to an Fp<bn254_fq> {uint32_t v[8]}.
 //
-// Multiplication is the CIOS "no-carry" variant (the reference's DoFastMul,
-// prime_field_fallback.h:331-355) restated on 32-bit limbs, because gfx950 has
-// no 64x64 multiplier: every partial product is one v_mad_u64_u32
-// (32x32+64 -> 64, measured at ~1/2 of the full VALU rate on MI355X), carries
-// ride v_add_co/v_addc chains.  All moduli here leave the top limb < 2^31 - 1,
-// which is the condition for the no-carry trick.
+// Device multiplication is Finely Integrated Product Scanning with generated
+// v_mad_u64_u32 carry chains (mont_asm.h, tools/gen_mont_asm.py); the host
+// keeps the reference's CIOS "no-carry" DoFastMul (prime_field_fallback.h:331-355)
+// restated on 32-bit limbs.
+//
+// Lazy reduction (device only): when 4p < 2^(32N) (BN254 Fq/Fr, BLS12-381 Fq)
+// device values live in [0, 2p): the FIPS product of two such values is < 2p
+// without the final conditional subtraction, add/sub/neg wrap by 2p, and
+// zero/equality tests compare canonical forms.  Every value that leaves a
+// kernel as a result is canonicalised (canonical()); host code always works
+// on canonical values.  BLS12-381 Fr (1 spare bit) stays canonical.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -43,6 +48,13 @@ template <class Cfg>
 struct Fp {
   static constexpr int N = Cfg::N32;
   using Config = Cfg;
+  // [0, 2p) representation is sound when 4p < 2^(32N)
+  static constexpr bool kLazyCapable = Cfg::kModulusBits <= 32 * N - 2;
+#if defined(__HIP_DEVICE_COMPILE__)
+  static constexpr bool kLazy = kLazyCapable;
+#else
+  static constexpr bool kLazy = false;
+#endif
   uint32_t v[N];
 
   TA_HD static Fp zero() {
@@ -63,44 +75,62 @@ struct Fp {
     for (int i = 0; i < N; ++i) r.v[i] = Cfg::kP32[i];
     return r;
   }
+
+  // r = a - m if a >= m else a, with m = p or 2p given as limbs
+  TA_HD static void cond_sub(uint32_t* a, const uint32_t* m) {
+    uint32_t t[N];
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = subb(a[i], m[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < N; ++i) a[i] = br ? a[i] : t[i];
+  }
+  TA_HD static void reduce_once(uint32_t* a) { cond_sub(a, Cfg::kP32); }
+
+  // canonical representative in [0, p); also applied on the host to values
+  // copied back from the device
+  TA_HD Fp canonical() const {
+    Fp r = *this;
+    if constexpr (kLazyCapable) reduce_once(r.v);
+    return r;
+  }
+
   TA_HD bool is_zero() const {
     uint32_t acc = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i) acc |= v[i];
+    if constexpr (kLazy) {
+      uint32_t accp = 0;  // x == p is the other representative of zero
+#pragma unroll
+      for (int i = 0; i < N; ++i) accp |= v[i] ^ Cfg::kP32[i];
+      return acc == 0 || accp == 0;
+    }
     return acc == 0;
   }
   TA_HD bool operator==(const Fp& o) const {
+    Fp a = canonical(), b = o.canonical();
     uint32_t acc = 0;
 #pragma unroll
-    for (int i = 0; i < N; ++i) acc |= v[i] ^ o.v[i];
+    for (int i = 0; i < N; ++i) acc |= a.v[i] ^ b.v[i];
     return acc == 0;
   }
   TA_HD bool operator!=(const Fp& o) const { return !(*this == o); }
   TA_HD bool is_one() const { return *this == one(); }
 
-  // r = a - p if a >= p else a   (a < 2p, no overflow past N limbs)
-  TA_HD static void reduce_once(uint32_t* a) {
-    uint32_t t[N];
-    uint32_t br = 0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) t[i] = subb(a[i], Cfg::kP32[i], br, &br);
-    // br == 1  <=>  a < p  -> keep a
-#pragma unroll
-    for (int i = 0; i < N; ++i) a[i] = br ? a[i] : t[i];
-  }
-
-  // prime_field_fallback.h:199-214 (Add + Clamp)
+  // prime_field_fallback.h:199-214 (Add + Clamp); lazy: wrap at 2p
   TA_HD Fp operator+(const Fp& o) const {
     Fp r;
     uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i) r.v[i] = addc(v[i], o.v[i], c, &c);
-    reduce_once(r.v);  // spare top bit: no carry out of the top limb
+    // spare top bits: no carry out of the top limb
+    if constexpr (kLazy) cond_sub(r.v, Cfg::kP232);
+    else reduce_once(r.v);
     return r;
   }
   TA_HD Fp dbl() const { return *this + *this; }
 
-  // prime_field_fallback.h:234-251 (Sub: add p back on borrow)
+  // prime_field_fallback.h:234-251 (Sub: add p back on borrow); lazy: add 2p
   TA_HD Fp operator-(const Fp& o) const {
     Fp r;
     uint32_t br = 0;
@@ -109,7 +139,10 @@ struct Fp {
     uint32_t mask = 0u - br;
     uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < N; ++i) r.v[i] = addc(r.v[i], Cfg::kP32[i] & mask, c, &c);
+    for (int i = 0; i < N; ++i) {
+      const uint32_t m = kLazy ? Cfg::kP232[i] : Cfg::kP32[i];
+      r.v[i] = addc(r.v[i], m & mask, c, &c);
+    }
     return r;
   }
   TA_HD Fp operator-() const { return zero() - *this; }
@@ -122,11 +155,12 @@ struct Fp {
 
   TA_HD Fp mul_inline(const Fp& b) const {
 #if defined(__HIP_DEVICE_COMPILE__)
-    // device: FIPS with hand-scheduled v_mad_u64_u32 carry chains (mont_asm.h)
+    // device: FIPS with hand-scheduled v_mad_u64_u32 carry chains (mont_asm.h);
+    // the product is < 2p for inputs < 2p (4p < R)
     Fp r;
     if constexpr (N == 8) detail::mont_mul_fips_8<Cfg>(r.v, v, b.v);
     else detail::mont_mul_fips_12<Cfg>(r.v, v, b.v);
-    reduce_once(r.v);
+    if constexpr (!kLazy) reduce_once(r.v);
     return r;
 #else
     return mul_cios(b);
@@ -167,13 +201,13 @@ struct Fp {
   }
   TA_HD Fp sqr() const { return (*this) * (*this); }
 
-  // Montgomery -> canonical (ToBigInt, prime_field_fallback.h:166-169).
+  // Montgomery -> canonical integer (ToBigInt, prime_field_fallback.h:166-169)
   TA_HD Fp from_mont() const {
     Fp one_plain = zero();
     one_plain.v[0] = 1;
-    return (*this) * one_plain;
+    return ((*this) * one_plain).canonical();
   }
-  // canonical (< p) -> Montgomery
+  // canonical integer (< p) -> Montgomery (lazy on device)
   TA_HD Fp to_mont() const {
     Fp r2;
 #pragma unroll
@@ -190,7 +224,7 @@ struct Fp {
       }
     return r;
   }
-  // Fermat inverse (same canonical value as the reference's BY inverter).
+  // Fermat inverse (same canonical value as the reference's BY inverter)
   TA_HD_NOINLINE Fp inverse() const {
     // e = p - 2 with borrow (BLS12-381 Fr's low 32-bit limb is 1)
     uint32_t e[N];
@@ -209,6 +243,7 @@ struct Fp2 {
   F c0, c1;
   TA_HD static Fp2 zero() { return {F::zero(), F::zero()}; }
   TA_HD static Fp2 one() { return {F::one(), F::zero()}; }
+  TA_HD Fp2 canonical() const { return {c0.canonical(), c1.canonical()}; }
   TA_HD bool is_zero() const { return c0.is_zero() && c1.is_zero(); }
   TA_HD bool is_one() const { return c0.is_one() && c1.is_zero(); }
   TA_HD bool operator==(const Fp2& o) const { return c0 == o.c0 && c1 == o.c1; }

@@ -58,7 +58,13 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
     maxchunks = (maxchunks + p.K2 - 1) / p.K2;
     ++p.levels;
   }
-  p.seg = std::min<unsigned>(p.buckets, 64);
+  // running-sum segment length: long segments amortise the (jL)*R fix-up, but
+  // small MSMs need >= ~64K segment threads to fill the chip (a 2^16 MSM with
+  // 64-bucket segments ran 208 threads of ~2000 serial mulmods each)
+  size_t nb = (size_t)p.windows * p.buckets;
+  unsigned seg = 2;
+  while (seg < 64 && ((nb / (seg * 2)) >= 65536)) seg *= 2;
+  p.seg = std::min<unsigned>(p.buckets, seg);
   return p;
 }
 

@@ -27,7 +27,9 @@ enum : uint32_t { kHead = 1, kTail = 2, kSingle = 4 };
 // recode: Montgomery scalar -> canonical -> signed base-2^c digits
 // (FillDigits, pippenger.h:28-51: digits in [-2^(c-1), 2^(c-1)), carry into
 // the top digit; W*c >= bits+1 keeps the top digit in [0, 2^(c-1)]).
-// key = |digit| (0 = no contribution), val = point index | sign << 31.
+// key = window << c | |digit| (digit 0 = no contribution), so one radix sort
+// over all windows orders the entries by (window, bucket) and every window
+// keeps its slice [w*n, (w+1)*n); val = point index | sign << 31.
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
                                                         unsigned c, unsigned W,
@@ -60,7 +62,7 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
       sign = 0;
     }
     size_t o = (size_t)w * n + i;
-    keys[o] = key;
+    keys[o] = (w << c) | key;
     vals[o] = i | sign;
   }
 }
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 template <class Curve>
 __global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
                                                          const uint32_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ vals, uint32_t n, uint32_t B,
+                                                         const uint32_t* __restrict__ vals, uint32_t c,
                                                          uint64_t total, uint32_t K,
                                                          XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                          XYZZ<typename Curve::F>* __restrict__ pieces,
@@ -92,14 +94,14 @@ __global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename C
   const uint64_t g0 = t * K;
   if (g0 >= total) return;
   const uint64_t g1 = min(g0 + K, total);
-  auto bucket_of = [&](uint64_t g) -> uint32_t {
-    uint32_t k = keys[g];
-    return k ? (uint32_t)(g / n) * B + (k - 1) : kNoBucket;
+  const uint32_t dmask = (1u << c) - 1;
+  // bucket id (w * 2^(c-1) + |digit| - 1) of a combined key, or none for digit 0
+  auto bucket_of_key = [&](uint32_t key) -> uint32_t {
+    uint32_t d = key & dmask;
+    return d ? ((key >> c) << (c - 1)) + (d - 1) : kNoBucket;
   };
-  const uint32_t prev_b = g0 ? bucket_of(g0 - 1) : kNoBucket;
-  const uint32_t next_b = (g1 < total) ? bucket_of(g1) : kNoBucket;
-  uint32_t w = (uint32_t)(g0 / n);
-  uint64_t wend = (uint64_t)(w + 1) * n;
+  const uint32_t prev_b = g0 ? bucket_of_key(keys[g0 - 1]) : kNoBucket;
+  const uint32_t next_b = (g1 < total) ? bucket_of_key(keys[g1]) : kNoBucket;
 
   uint32_t flags = 0, runs = 0, cur = kNoBucket;
   XYZZ<F> acc = XYZZ<F>::zero();
@@ -113,9 +115,8 @@ __global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename C
     uint32_t k2 = 0, v2 = 0;
     if (g + 2 < g1) { k2 = keys[g + 2]; v2 = vals[g + 2]; }
     Affine<F> Pn = bases[v1 & ~kSignBit];
-    if (g == wend) { ++w; wend += n; }
-    if (k0 != 0) {
-      const uint32_t b = w * B + (k0 - 1);
+    const uint32_t b = bucket_of_key(k0);
+    if (b != kNoBucket) {
       if (b != cur) {
         if (cur != kNoBucket) {  // close a run that is not the last one
           if (runs == 1 && cur == prev_b) { pieces[2 * t] = acc; flags |= kHead; }
@@ -362,23 +363,22 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   TA_HIP(hipGetLastError());
   if (profile_) TA_HIP(hipEventRecord(ev_[2], stream_));
 
-  // ---- sort each window's (bucket, point) pairs ----
+  // ---- one radix sort of all (window, bucket, point) entries ----
+  unsigned wbits = 0;
+  while ((1u << wbits) < W) ++wbits;
+  const unsigned key_bits = c + wbits;
   size_t sort_bytes = 0;
-  TA_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, (uint32_t)n, 0, c, stream_));
+  TA_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, entries, 0, key_bits, stream_));
   void* sort_tmp = sort_tmp_.ensure(sort_bytes);
-  for (unsigned w = 0; w < W; ++w) {
-    size_t o = (size_t)w * n;
-    TA_HIP(rocprim::radix_sort_pairs(sort_tmp, sort_bytes, keys + o, keys2 + o, vals + o, vals2 + o, (uint32_t)n,
-                                     0, c, stream_));
-  }
+  TA_HIP(rocprim::radix_sort_pairs(sort_tmp, sort_bytes, keys, keys2, vals, vals2, entries, 0, key_bits, stream_));
   if (profile_) TA_HIP(hipEventRecord(ev_[3], stream_));
 
   // ---- accumulation (every bucket without an entry stays the identity) ----
   TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * sizeof(Point), stream_));
   TA_HIP(hipMemsetAsync(dscal, 0, 2 * sizeof(uint32_t), stream_));
   if (profile_) TA_HIP(hipEventRecord(ev_[6], stream_));
-  hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(T)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2,
-                     (uint32_t)n, B, (uint64_t)entries, K, bucket_sum, pieces, tflags, tlast);
+  hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(T)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2, c,
+                     (uint64_t)entries, K, bucket_sum, pieces, tflags, tlast);
   TA_HIP(hipGetLastError());
   if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));
 
@@ -482,6 +482,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   enqueue(d_bases, d_scalars, n, plan, d_windows);
   TA_HIP(hipMemcpyAsync(out->data(), d_windows, plan.windows * sizeof(Point), hipMemcpyDeviceToHost, stream_));
   TA_HIP(hipStreamSynchronize(stream_));
+  for (auto& p : *out) p = p.canonical();  // device values live in [0, 2p)
   if (profile_) {
     TA_HIP(hipEventElapsedTime(&timings_.h2d, ev_[0], ev_[1]));
     TA_HIP(hipEventElapsedTime(&timings_.recode, ev_[1], ev_[2]));

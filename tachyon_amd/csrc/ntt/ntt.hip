@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__
       uint32_t o = (q << (L - k)) + r0 + m;
       if (a.mode & kStoreCoset) v = v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits]);
       else if (a.mode & kStoreScale) v = v * a.scale;
-      out[o] = v;
+      out[o] = v.canonical();
     }
   }
 }

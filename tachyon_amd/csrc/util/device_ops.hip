@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kBlock) void gen_scalars_kernel(uint64_t seed, uint
   if (i >= n) return;
   uint64_t c[4];
   rand_scalar<Fr>(seed, start + i, c);
-  out[i] = limbs_to_fr<Fr>(c).to_mont();
+  out[i] = limbs_to_fr<Fr>(c).to_mont().canonical();
 }
 
 template <class F>
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void field_op_kernel(int op, const F* a, co
     case 8: r = x.dbl(); break;
     default: r = F::zero();
   }
-  out[i] = r;
+  out[i] = r.canonical();
 }
 
 template <class F>
