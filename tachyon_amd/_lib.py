@@ -8,7 +8,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtachyon_mi355x.so")
+# TACHYON_MI355X_LIB: alternative build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("TACHYON_MI355X_LIB") or os.path.join(HERE, "libtachyon_mi355x.so")
 
 CURVES = {"bn254_g1": 0, "bn254_g2": 1, "bls12_381_g1": 2, "bls12_381_g2": 3}
 FIELDS = {"bn254_fq": 0, "bn254_fr": 1, "bls12_381_fq": 2, "bls12_381_fr": 3}

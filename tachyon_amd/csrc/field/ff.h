@@ -29,6 +29,11 @@
 // single kernels tens of thousands of instructions long and compile for
 // minutes.
 #define TA_HD_NOINLINE __host__ __device__ __noinline__
+// device add/sub/conditional-subtract as hand-written VCC carry chains
+// (mont_asm.h); 0 = hipcc's code from the portable C below
+#ifndef TA_FIELD_ASM
+#define TA_FIELD_ASM 1
+#endif
 
 namespace tachyon_amd {
 
@@ -85,7 +90,13 @@ struct Fp {
 #pragma unroll
     for (int i = 0; i < N; ++i) a[i] = br ? a[i] : t[i];
   }
-  TA_HD static void reduce_once(uint32_t* a) { cond_sub(a, Cfg::kP32); }
+  TA_HD static void reduce_once(uint32_t* a) {
+#if defined(__HIP_DEVICE_COMPILE__) && TA_FIELD_ASM
+    if constexpr (N == 8) return detail::cond_sub_8<Cfg, false>(a);
+    else if constexpr (N == 12) return detail::cond_sub_12<Cfg, false>(a);
+#endif
+    cond_sub(a, Cfg::kP32);
+  }
 
   // canonical representative in [0, p); also applied on the host to values
   // copied back from the device
@@ -120,6 +131,10 @@ struct Fp {
   // prime_field_fallback.h:199-214 (Add + Clamp); lazy: wrap at 2p
   TA_HD Fp operator+(const Fp& o) const {
     Fp r;
+#if defined(__HIP_DEVICE_COMPILE__) && TA_FIELD_ASM
+    if constexpr (N == 8) { detail::add_mod_8<Cfg, kLazy>(r.v, v, o.v); return r; }
+    else if constexpr (N == 12) { detail::add_mod_12<Cfg, kLazy>(r.v, v, o.v); return r; }
+#endif
     uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i) r.v[i] = addc(v[i], o.v[i], c, &c);
@@ -133,6 +148,10 @@ struct Fp {
   // prime_field_fallback.h:234-251 (Sub: add p back on borrow); lazy: add 2p
   TA_HD Fp operator-(const Fp& o) const {
     Fp r;
+#if defined(__HIP_DEVICE_COMPILE__) && TA_FIELD_ASM
+    if constexpr (N == 8) { detail::sub_mod_8<Cfg, kLazy>(r.v, v, o.v); return r; }
+    else if constexpr (N == 12) { detail::sub_mod_12<Cfg, kLazy>(r.v, v, o.v); return r; }
+#endif
     uint32_t br = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i) r.v[i] = subb(v[i], o.v[i], br, &br);

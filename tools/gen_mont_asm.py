@@ -23,22 +23,46 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tachyon_amd", "csrc", "field", "mont_asm.h")
 
 
-def mac_lines(pairs):
-    """pairs: list of (x_operand, y_operand) names -> asm text lines."""
+# Carry-out SGPR pairs rotate over three registers and each v_addc_co_u32 that
+# collects a carry trails its v_mad_u64_u32 by two instructions: gfx940-family
+# parts need two wait states between a VALU write of an SGPR (the carry mask)
+# and a VALU read of it (hipcc pads its own carry chains with s_nop 1), and the
+# rotation meets that without nops wherever a statement has >= 3 products.
+NCARRY = 3
+
+
+def mac_lines(pairs, fresh_c2):
+    """pairs: list of (x_operand, y_operand) names -> asm text lines.
+    fresh_c2: the first collected carry defines c2 (v_addc_co_u32 c2, .., 0, zero)
+    instead of a separate zeroing move."""
     out = []
-    for x, y in pairs:
-        out.append(f"v_mad_u64_u32 %[acc], vcc, %[{x}], %[{y}], %[acc]")
-        out.append("v_addc_co_u32 %[c2], vcc, 0, %[c2], vcc")
+    pos = {}  # product index -> position of its mad in `out`
+
+    def collect(j):
+        dist = len(out) - pos[j] - 1  # instructions between the mad and this addc
+        if dist < 2:
+            out.append(f"s_nop {1 - dist}")
+        src = "%[z]" if (fresh_c2 and j == 0) else "%[c2]"
+        out.append(f"v_addc_co_u32 %[c2], vcc, 0, {src}, %[s{j % NCARRY}]")
+
+    for k, (x, y) in enumerate(pairs):
+        pos[k] = len(out)
+        out.append(f"v_mad_u64_u32 %[acc], %[s{k % NCARRY}], %[{x}], %[{y}], %[acc]")
+        if k >= 2:
+            collect(k - 2)
+    for j in range(max(0, len(pairs) - 2), len(pairs)):
+        collect(j)
     return out
 
 
-def asm_stmt(pairs):
+def asm_stmt(pairs, fresh_c2=False):
     names = []
     for x, y in pairs:
         for v in (x, y):
             if v not in names:
                 names.append(v)
-    text = "\\n\\t".join(mac_lines(pairs))
+    lines = mac_lines(pairs, fresh_c2)
+    text = "\\n\\t".join(lines)
     ins = []
     for v in names:
         kind, idx = v[0], int(v[1:])
@@ -50,8 +74,13 @@ def asm_stmt(pairs):
             ins.append(f'[{v}] "v"(m[{idx}])')
         elif kind == "p":
             ins.append(f'[{v}] "s"(Cfg::kP32[{idx}])')
+    if fresh_c2:
+        ins.append('[z] "v"(0u)')
+    c2 = '[c2] "=&v"(c2)' if fresh_c2 else '[c2] "+&v"(c2)'
+    nsg = min(NCARRY, len(pairs))
+    sg = ", ".join(f'[s{i}] "=&s"(sc[{i}])' for i in range(nsg))
     return (f'    asm volatile("{text}"\n'
-            f'                 : [acc] "+&v"(acc), [c2] "+&v"(c2)\n'
+            f'                 : [acc] "+&v"(acc), {c2}, {sg}\n'
             f'                 : {", ".join(ins)}\n'
             f'                 : "vcc");\n')
 
@@ -63,7 +92,8 @@ def gen(N):
              f"                                                  const uint32_t* __restrict__ b) {{",
              f"  uint32_t m[{N}];",
              "  uint64_t acc = 0;",
-             "  uint32_t c2 = 0;"]
+             f"  uint64_t sc[{NCARRY}];  // carry-out lane masks (SGPR pairs)",
+             "  uint32_t c2;"]
     for k in range(N):
         pairs = []
         for j in range(k):
@@ -71,11 +101,16 @@ def gen(N):
             pairs.append((f"m{j}", f"p{k - j}"))
         pairs.append((f"a{k}", "b0"))
         lines.append(f"  {{  // column {k}")
-        lines.append(asm_stmt(pairs).rstrip("\n"))
+        if k == 0:  # a0*b0 + 0 cannot carry out
+            lines.append('    asm volatile("v_mad_u64_u32 %[acc], %[s0], %[a0], %[b0], %[acc]"\n'
+                         '                 : [acc] "+&v"(acc), [s0] "=&s"(sc[0])\n'
+                         '                 : [a0] "v"(a[0]), [b0] "v"(b[0]));')
+            lines.append("    c2 = 0;")
+        else:
+            lines.append(asm_stmt(pairs, fresh_c2=True).rstrip("\n"))
         lines.append(f"    m[{k}] = (uint32_t)acc * Cfg::kInv32;")
         lines.append(asm_stmt([(f"m{k}", "p0")]).rstrip("\n"))
         lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
-        lines.append("    c2 = 0;")
         lines.append("  }")
     for k in range(N, 2 * N - 1):
         pairs = []
@@ -83,23 +118,141 @@ def gen(N):
             pairs.append((f"a{j}", f"b{k - j}"))
             pairs.append((f"m{j}", f"p{k - j}"))
         lines.append(f"  {{  // column {k}")
-        lines.append(asm_stmt(pairs).rstrip("\n"))
+        lines.append(asm_stmt(pairs, fresh_c2=True).rstrip("\n"))
         lines.append(f"    r[{k - N}] = (uint32_t)acc;")
         lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
-        lines.append("    c2 = 0;")
         lines.append("  }")
     lines.append(f"  r[{N - 1}] = (uint32_t)acc;  // < 2p < 2^{32 * N}: the top word is the last one")
     lines.append("}")
     return "\n".join(lines) + "\n"
 
 
+def operand_list(spec):
+    return ", ".join(spec)
+
+
+def asm_block(lines, outs, ins, volatile=False):
+    text = "\\n\\t".join(x for x in lines if x)
+    kw = "asm volatile" if volatile else "asm"
+    return (f'  {kw}("{text}"\n'
+            f'      : {operand_list(outs)}\n'
+            f'      : {operand_list(ins)}\n'
+            f'      : "vcc");\n')
+
+
+def interleave_select(N, chain_a, chain_b_name, out_sel):
+    """Two dependent carry chains, hazard-free without nops: chain A (VCC)
+    produces limb i, chain B (SGPR pair %[sb], e64 forms) consumes it one step
+    behind, and the N moves of the modulus limbs fill the remaining slot, so
+    consecutive links of either chain are two instructions apart.  Finally
+    out_sel selects limbwise on B's (or A's) last carry."""
+    L = ["v_mov_b32 %[t0], %[m0]"]
+    L.append(chain_a(0))
+    L.append("v_mov_b32 %[t1], %[m1]")
+    for i in range(1, N):
+        L.append(chain_b_name(i - 1))
+        L.append(chain_a(i))
+        if i + 1 < N:
+            L.append(f"v_mov_b32 %[t{i + 1}], %[m{i + 1}]")
+        else:
+            L.append("s_nop 0")
+    L.append(chain_b_name(N - 1))
+    L.append("s_nop 1")
+    L += out_sel
+    return L
+
+
+def gen_addsub(N):
+    """add_mod / sub_mod / cond_sub for N 32-bit limbs with the modulus M
+    (p or 2p) as 32-bit literals ("i" operands): VCC carry chains instead of
+    hipcc's 64-bit emulation (v_lshl_add_u64 + v_ashrrev per limb)."""
+    m_in = [f'[m{i}] "i"(ModLimb<Cfg, k2p>::get({i}))' for i in range(N)]
+    a_in = [f'[a{i}] "v"(a[{i}])' for i in range(N)]
+    b_in = [f'[b{i}] "v"(b[{i}])' for i in range(N)]
+    r_out = [f'[r{i}] "=&v"(r[{i}])' for i in range(N)]
+    t_out = [f'[t{i}] "=&v"(t[{i}])' for i in range(N)]
+    sb_out = ['[sb] "=&s"(sb)']
+    out = []
+
+    # ---- add: r = a + b (VCC chain); t = r - M (sb chain); r = borrow(sb) ? r : t
+    def add_a(i):
+        return ("v_add_co_u32 %[r0], vcc, %[a0], %[b0]" if i == 0
+                else f"v_addc_co_u32 %[r{i}], vcc, %[a{i}], %[b{i}], vcc")
+
+    def add_b(i):
+        return ("v_sub_co_u32_e64 %[t0], %[sb], %[r0], %[t0]" if i == 0
+                else f"v_subb_co_u32_e64 %[t{i}], %[sb], %[r{i}], %[t{i}], %[sb]")
+    L = interleave_select(N, add_a, add_b,
+                          [f"v_cndmask_b32_e64 %[r{i}], %[t{i}], %[r{i}], %[sb]" for i in range(N)])
+    # single-chain form: one VCC chain at a time, s_nop 1 between links
+    L1 = [add_a(0)]
+    for i in range(1, N):
+        L1 += ["s_nop 1", add_a(i)]
+    L1 += [f"v_mov_b32 %[t{i}], %[m{i}]" for i in range(1, N)]
+    L1 += ["v_subrev_co_u32 %[t0], vcc, %[m0], %[r0]"]
+    for i in range(1, N):
+        L1 += ["s_nop 1", f"v_subb_co_u32 %[t{i}], vcc, %[r{i}], %[t{i}], vcc"]
+    L1 += ["s_nop 1"] + [f"v_cndmask_b32 %[r{i}], %[t{i}], %[r{i}], vcc" for i in range(N)]
+    out.append(f"// r = a + b mod M, M = k2p ? 2p : p; a, b < M and 2M < 2^{32 * N}\n"
+               f"template <class Cfg, bool k2p>\n"
+               f"__device__ __forceinline__ void add_mod_{N}(uint32_t* r, const uint32_t* a, const uint32_t* b) {{\n"
+               f"  uint32_t t[{N}];\n  uint64_t sb;\n#if TA_ADDSUB_INTERLEAVE\n"
+               + asm_block(L, r_out + t_out + sb_out, a_in + b_in + m_in) + "#else\n  (void)sb;\n"
+               + asm_block(L1, r_out + t_out, a_in + b_in + m_in) + "#endif\n}\n")
+
+    # ---- sub: r = a - b (VCC chain); t = r + M (sb chain); r = borrow(vcc) ? t : r
+    def sub_a(i):
+        return ("v_sub_co_u32 %[r0], vcc, %[a0], %[b0]" if i == 0
+                else f"v_subb_co_u32 %[r{i}], vcc, %[a{i}], %[b{i}], vcc")
+
+    def sub_b(i):
+        return ("v_add_co_u32_e64 %[t0], %[sb], %[r0], %[t0]" if i == 0
+                else f"v_addc_co_u32_e64 %[t{i}], %[sb], %[r{i}], %[t{i}], %[sb]")
+    L = interleave_select(N, sub_a, sub_b,
+                          [f"v_cndmask_b32 %[r{i}], %[r{i}], %[t{i}], vcc" for i in range(N)])
+    L1 = [sub_a(0)]
+    for i in range(1, N):
+        L1 += ["s_nop 1", sub_a(i)]
+    L1 += ["s_nop 1", f"v_subb_co_u32 %[t0], vcc, %[r{N - 1}], %[r{N - 1}], vcc"]  # t0 = -borrow
+    L1 += [f"v_and_b32 %[t{i}], %[m{i}], %[t0]" for i in range(N - 1, -1, -1)]
+    L1 += ["v_add_co_u32 %[r0], vcc, %[r0], %[t0]"]
+    for i in range(1, N):
+        L1 += ["s_nop 1", f"v_addc_co_u32 %[r{i}], vcc, %[r{i}], %[t{i}], vcc"]
+    out.append(f"// r = a - b mod M (a - b + M selected on borrow)\n"
+               f"template <class Cfg, bool k2p>\n"
+               f"__device__ __forceinline__ void sub_mod_{N}(uint32_t* r, const uint32_t* a, const uint32_t* b) {{\n"
+               f"  uint32_t t[{N}];\n  uint64_t sb;\n#if TA_ADDSUB_INTERLEAVE\n"
+               + asm_block(L, r_out + t_out + sb_out, a_in + b_in + m_in) + "#else\n  (void)sb;\n"
+               + asm_block(L1, r_out + t_out, a_in + b_in + m_in) + "#endif\n}\n")
+
+    # ---- cond_sub: r = r >= M ? r - M : r  (in place; off the hot path)
+    rio = [f'[r{i}] "+v"(r[{i}])' for i in range(N)]
+    L = [f"v_mov_b32 %[t{i}], %[m{i}]" for i in range(1, N)]
+    L += ["v_subrev_co_u32 %[t0], vcc, %[m0], %[r0]"]
+    for i in range(1, N):
+        L += ["s_nop 1", f"v_subb_co_u32 %[t{i}], vcc, %[r{i}], %[t{i}], vcc"]
+    L += ["s_nop 1"]
+    L += [f"v_cndmask_b32 %[r{i}], %[t{i}], %[r{i}], vcc" for i in range(N)]
+    out.append(f"// r = r - M if r >= M  (r < 2^{32 * N})\n"
+               f"template <class Cfg, bool k2p>\n"
+               f"__device__ __forceinline__ void cond_sub_{N}(uint32_t* r) {{\n"
+               f"  uint32_t t[{N}];\n" + asm_block(L, rio + t_out, m_in) + "}\n")
+    return "\n".join(out)
+
+
 def main():
     text = ["// GENERATED by tools/gen_mont_asm.py -- do not edit.",
             "// FIPS Montgomery product for gfx950 (see the generator for the rationale).",
             "// Output is < 2p (the caller applies the final conditional subtraction).",
-            "#pragma once", "#include <cstdint>", "", "namespace tachyon_amd::detail {", ""]
+            "#pragma once", "#include <cstdint>", "",
+            "// add/sub: 1 = two interleaved carry chains (no nops), 0 = one chain with s_nop 1 per link\n// (0 measured ~1% faster in the MSM accumulation: fewer VGPRs, shorter encodings)",
+            "#ifndef TA_ADDSUB_INTERLEAVE", "#define TA_ADDSUB_INTERLEAVE 0", "#endif", "",
+            "namespace tachyon_amd::detail {", ""]
+    text.append("template <class Cfg, bool k2p>\nstruct ModLimb {\n"
+                "  static constexpr uint32_t get(int i) { return k2p ? Cfg::kP232[i] : Cfg::kP32[i]; }\n};\n")
     for N in (8, 12):
         text.append(gen(N))
+        text.append(gen_addsub(N))
     text.append("}  // namespace tachyon_amd::detail")
     with open(OUT, "w") as f:
         f.write("\n".join(text) + "\n")
