@@ -179,10 +179,13 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_group_ge
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset(
     tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_fr* offset);
 /* Device-resident in-place transform of size() elements at d_data (HBM),
- * enqueued on `stream` (hipStream_t, NULL = the domain's own stream).
- * inverse = 0: FFT, 1: IFFT (no trimming).  Not synchronised. */
+ * enqueued on the domain's stream (see _stream).  inverse = 0: FFT,
+ * 1: IFFT (no trimming).  Not synchronised.  _batch_device transforms `batch`
+ * consecutive arrays of size() elements. */
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(
     tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_fr* d_data, int inverse);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device(
+    tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_fr* d_data, size_t batch, int inverse);
 TACHYON_C_EXPORT void* tachyon_mi355x_bn254_univariate_evaluation_domain_stream(
     tachyon_bn254_univariate_evaluation_domain* domain);
 /* per-pass device time (ms) of the last transform when profiling is on;
@@ -191,6 +194,25 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_prof
     tachyon_bn254_univariate_evaluation_domain* domain, int on);
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(
     const tachyon_bn254_univariate_evaluation_domain* domain, float* total_ms, float* pass_ms, int max_passes);
+
+/* Distributed four-step NTT over 2^log_world ranks (no
+ * reference counterpart -- icicle's NTT is single-GPU).  One plan per rank;
+ * rank r holds the columns c in [r C/G, (r+1) C/G) of the R x C view of the
+ * input (R = 2^floor(log_n/2)), column-major: in[c_l R + r'] = x[C r' + c],
+ * and produces rows k1 in [r R/G, (r+1) R/G) of the output, row-major:
+ * out[k1_l C + k2] = X[k1 + R k2].  A transform is
+ *   stage(1, in -> send); all-to-all(send -> recv) by the caller; stage(2, recv -> out)
+ * with send/recv = G chunks of local_size/G elements (chunk h to/from rank h).
+ * The inverse maps the output layout back to the input layout (n^-1 included).
+ * Work is enqueued on `stream` (hipStream_t; NULL = a stream owned by the plan). */
+typedef struct tachyon_mi355x_bn254_ntt4 tachyon_mi355x_bn254_ntt4;
+TACHYON_C_EXPORT tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create(uint32_t log_n, uint32_t log_world,
+                                                                            uint32_t rank, void* stream);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_destroy(tachyon_mi355x_bn254_ntt4* plan);
+TACHYON_C_EXPORT size_t tachyon_mi355x_bn254_ntt4_local_size(const tachyon_mi355x_bn254_ntt4* plan);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4* plan, int stage, int inverse,
+                                                      const tachyon_bn254_fr* d_in, tachyon_bn254_fr* d_out);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_synchronize(tachyon_mi355x_bn254_ntt4* plan);
 
 /* G2 MSM contexts (Groth16's B-in-G2, BLS12-381 config 4); same semantics as
  * the G1 *_msm_gpu entry points. */

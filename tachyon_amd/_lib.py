@@ -79,9 +79,15 @@ SIGNATURES = [
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_group_gen", None, [vp, vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset", None, [vp, vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device", None, [vp, vp, i32]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device", None, [vp, vp, sz, i32]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_stream", vp, [vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile", None, [vp, i32]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings", i32, [vp, fp, fp, i32]),
+    ("tachyon_mi355x_bn254_ntt4_create", vp, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp]),
+    ("tachyon_mi355x_bn254_ntt4_destroy", None, [vp]),
+    ("tachyon_mi355x_bn254_ntt4_local_size", sz, [vp]),
+    ("tachyon_mi355x_bn254_ntt4_stage", None, [vp, i32, i32, vp, vp]),
+    ("tachyon_mi355x_bn254_ntt4_synchronize", None, [vp]),
     ("tachyon_bn254_g2_create_msm_gpu", vp, [u8]),
     ("tachyon_bn254_g2_destroy_msm_gpu", None, [vp]),
     ("tachyon_bn254_g2_affine_msm_gpu", vp, [vp, vp, vp, sz]),

@@ -524,6 +524,13 @@ void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(tachyon_
   else d->impl->forward_device(reinterpret_cast<Bn254Fr*>(d_data));
   GUARD_END
 }
+void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device(
+    tachyon_bn254_univariate_evaluation_domain* d, tachyon_bn254_fr* d_data, size_t batch, int inverse) {
+  GUARD_BEGIN
+  if (inverse) d->impl->inverse_device(reinterpret_cast<Bn254Fr*>(d_data), batch);
+  else d->impl->forward_device(reinterpret_cast<Bn254Fr*>(d_data), batch);
+  GUARD_END
+}
 void* tachyon_mi355x_bn254_univariate_evaluation_domain_stream(tachyon_bn254_univariate_evaluation_domain* d) {
   return d->impl->stream();
 }
@@ -538,6 +545,38 @@ int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(const tachyon
   int np = (int)t.passes.size();
   for (int i = 0; i < np && i < max_passes; ++i) pass_ms[i] = t.passes[i];
   return np;
+}
+
+struct tachyon_mi355x_bn254_ntt4 {
+  ntt::Ntt4Step<Bn254Fr>* impl;
+};
+tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create(uint32_t log_n, uint32_t log_world, uint32_t rank,
+                                                           void* stream) {
+  GUARD_BEGIN
+  return new tachyon_mi355x_bn254_ntt4{
+      new ntt::Ntt4Step<Bn254Fr>(log_n, log_world, rank, static_cast<hipStream_t>(stream))};
+  GUARD_END
+}
+void tachyon_mi355x_bn254_ntt4_destroy(tachyon_mi355x_bn254_ntt4* plan) {
+  if (!plan) return;
+  delete plan->impl;
+  delete plan;
+}
+size_t tachyon_mi355x_bn254_ntt4_local_size(const tachyon_mi355x_bn254_ntt4* plan) { return plan->impl->local_size(); }
+void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4* plan, int stage, int inverse,
+                                     const tachyon_bn254_fr* d_in, tachyon_bn254_fr* d_out) {
+  GUARD_BEGIN
+  const Bn254Fr* in = reinterpret_cast<const Bn254Fr*>(d_in);
+  Bn254Fr* out = reinterpret_cast<Bn254Fr*>(d_out);
+  if (stage != 1 && stage != 2) throw std::runtime_error("tachyon_mi355x: ntt4 stage is 1 or 2");
+  if (!inverse) (stage == 1) ? plan->impl->forward_stage1(in, out) : plan->impl->forward_stage2(in, out);
+  else (stage == 1) ? plan->impl->inverse_stage1(in, out) : plan->impl->inverse_stage2(in, out);
+  GUARD_END
+}
+void tachyon_mi355x_bn254_ntt4_synchronize(tachyon_mi355x_bn254_ntt4* plan) {
+  GUARD_BEGIN
+  TA_HIP(hipStreamSynchronize(plan->impl->stream()));
+  GUARD_END
 }
 
 }  // extern "C"

@@ -51,10 +51,11 @@ class NttDomain {
   void set_offset(const Fr& h);
   const Fr& offset() const { return offset_; }
 
-  // In-place transform of n device-resident elements (d_data), enqueued on
-  // stream(); scratch is owned by the domain.  Not synchronised.
-  void forward_device(Fr* d_data);
-  void inverse_device(Fr* d_data);
+  // In-place transform of `batch` consecutive arrays of n device-resident
+  // elements (d_data), enqueued on stream(); scratch is owned by the domain.
+  // Not synchronised.
+  void forward_device(Fr* d_data, size_t batch = 1);
+  void inverse_device(Fr* d_data, size_t batch = 1);
 
   // Host vector in/out: `len` <= n input elements, zero-padded to n; writes n
   // outputs to `out` (may alias `in`).  Synchronises.
@@ -71,7 +72,7 @@ class NttDomain {
   const std::vector<Pass>& plan() const { return plan_; }
 
  private:
-  void run(Fr* d_data, bool inverse);
+  void run(Fr* d_data, bool inverse, size_t batch);
   void build_twiddles();
   void build_powers(const Fr& base, const Fr& scale, Fr* d_lo, Fr* d_hi);
 
@@ -92,5 +93,52 @@ class NttDomain {
 
 extern template class NttDomain<Bn254Fr>;
 extern template class NttDomain<Bls381Fr>;
+
+}  // namespace tachyon_amd::ntt
+
+namespace tachyon_amd::ntt {
+
+// Distributed four-step NTT (Bailey) over G = 2^log_world ranks, one process
+// per GPU: n = R * C with R = 2^floor(L/2), C = n / R, both
+// >= G.  Rank g owns
+//   input   the columns c in [g C/G, (g+1) C/G) of the R x C row-major view
+//           of x, stored column by column: in[c_l * R + r] = x[C r + c]
+//   output  the rows k1 in [g R/G, (g+1) R/G) of X, stored row by row:
+//           out[k1_l * C + k2] = X[k1 + R k2]
+// forward = stage1 (R-point NTTs on the local columns, twiddles w_n^(c k1),
+// pack per destination rank), one all-to-all of n/G elements, stage2
+// (transpose, C-point NTTs on the local rows).  inverse mirrors it and maps
+// the output layout back to the input layout (n^-1 included).  The
+// all-to-all is the caller's (torch.distributed / RCCL): send and recv are
+// G equal chunks of n/G^2 elements, chunk h going to / coming from rank h.
+template <class Fr>
+class Ntt4Step {
+ public:
+  Ntt4Step(uint32_t log_n, uint32_t log_world, uint32_t rank, hipStream_t stream);
+  ~Ntt4Step();
+  Ntt4Step(const Ntt4Step&) = delete;
+  Ntt4Step& operator=(const Ntt4Step&) = delete;
+
+  size_t local_size() const { return n_ >> log_g_; }
+  uint32_t log_rows() const { return log_r_; }
+  hipStream_t stream() const { return stream_; }
+
+  void forward_stage1(const Fr* in, Fr* send);
+  void forward_stage2(const Fr* recv, Fr* out);
+  void inverse_stage1(const Fr* in, Fr* send);
+  void inverse_stage2(const Fr* recv, Fr* out);
+
+ private:
+  uint32_t log_n_, log_g_, rank_, log_r_, log_c_;
+  size_t n_;
+  hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
+  NttDomain<Fr>* dom_r_ = nullptr;
+  NttDomain<Fr>* dom_c_ = nullptr;
+  uint32_t pow_bits_ = 0;
+  DeviceBuffer work_, w_lo_, w_hi_, wi_lo_, wi_hi_;
+};
+
+extern template class Ntt4Step<Bn254Fr>;
 
 }  // namespace tachyon_amd::ntt

@@ -45,6 +45,8 @@ __global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__
   const uint32_t elems = M << k;
   const uint32_t n = 1u << L;
   const uint32_t b = blockIdx.x;
+  in += (size_t)blockIdx.y << L;  // batch of independent contiguous transforms
+  out += (size_t)blockIdx.y << L;
 
   // index(mid, m) of element m of the block's set, position mid in the set
   uint32_t hi_shift = L - a.s0;            // set stride in the hi dimension
@@ -165,6 +167,43 @@ std::vector<Fr> host_powers(const Fr& base, const Fr& scale, size_t count) {
   return out;
 }
 
+// out[c][r] = in[r][c] for a rows x cols row-major matrix, through 32 x 32 LDS tiles
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void transpose_kernel(const Fr* __restrict__ in, Fr* __restrict__ out,
+                                                           uint32_t rows, uint32_t cols) {
+  __shared__ Fr tile[32][33];
+  const uint32_t c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (uint32_t j = ty; j < 32; j += 8) {
+    const uint32_t r = r0 + j, c = c0 + tx;
+    if (r < rows && c < cols) tile[j][tx] = in[(size_t)r * cols + c];
+  }
+  __syncthreads();
+  for (uint32_t j = ty; j < 32; j += 8) {
+    const uint32_t c = c0 + j, r = r0 + tx;
+    if (r < rows && c < cols) out[(size_t)c * rows + r] = tile[tx][j];
+  }
+}
+
+// forward: send[(h * Cg + c_l) * Rg + k1_l] = work[c_l * R + k1] * w^((c0 + c_l) k1), k1 = h Rg + k1_l
+// inverse (unpack = true): out[c_l * R + k1] = recv[(h * Cg + c_l) * Rg + k1_l] * w^-((c0 + c_l) k1)
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void twiddle_exchange_kernel(const Fr* __restrict__ in, Fr* __restrict__ out,
+                                                                  uint32_t log_r, uint32_t log_rg, uint32_t log_cg,
+                                                                  uint32_t c0, uint32_t log_n, const Fr* __restrict__ lo,
+                                                                  const Fr* __restrict__ hi, uint32_t pow_bits,
+                                                                  uint32_t unpack) {
+  const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;  // position in the [c_l][k1] view
+  if (i >= ((size_t)1 << (log_cg + log_r))) return;
+  const uint32_t c_l = (uint32_t)(i >> log_r), k1 = (uint32_t)(i & ((1u << log_r) - 1));
+  const uint32_t h = k1 >> log_rg, k1_l = k1 & ((1u << log_rg) - 1);
+  const size_t j = (((size_t)h << log_cg) + c_l) * ((size_t)1 << log_rg) + k1_l;  // packed position
+  const uint64_t e = ((uint64_t)(c0 + c_l) * k1) & ((uint64_t(1) << log_n) - 1);
+  const Fr w = lo[e & ((1u << pow_bits) - 1)] * hi[e >> pow_bits];
+  if (!unpack) out[j] = in[i] * w;
+  else out[i] = in[j] * w;
+}
+
 }  // namespace
 
 template <class Fr>
@@ -278,13 +317,14 @@ void NttDomain<Fr>::set_offset(const Fr& h) {
 }
 
 template <class Fr>
-void NttDomain<Fr>::run(Fr* d_data, bool inverse) {
-  if (log_n_ == 0) {
+void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
+  if (log_n_ == 0 || batch == 0) {
     // size-1 domain: forward is the identity (h^0 = 1); inverse scales by n^-1 = 1
     return;
   }
+  if (batch > 65535) throw std::runtime_error("tachyon_mi355x: NTT batch exceeds the grid limit");
   const Fr* tw = inverse ? tw_inv_.as<Fr>() : tw_fwd_.as<Fr>();
-  Fr* scratch = plan_.size() > 1 ? static_cast<Fr*>(scratch_.ensure(n_ * sizeof(Fr))) : d_data;
+  Fr* scratch = plan_.size() > 1 ? static_cast<Fr*>(scratch_.ensure(batch * n_ * sizeof(Fr))) : d_data;
   if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
   for (size_t p = 0; p < plan_.size(); ++p) {
     const Pass& ps = plan_[p];
@@ -317,7 +357,8 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse) {
     uint32_t elems = (1u << ps.log_m) << ps.k;
     uint32_t blocks = (uint32_t)(n_ / elems);
     size_t lds = (size_t)elems * sizeof(Fr);
-    hipLaunchKernelGGL(dif_pass_kernel<Fr>, dim3(blocks), dim3(kBlock), lds, stream_, src, dst, tw, a);
+    hipLaunchKernelGGL(dif_pass_kernel<Fr>, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw,
+                       a);
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(ev_[p + 1], stream_));
   }
@@ -330,10 +371,10 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse) {
 }
 
 template <class Fr>
-void NttDomain<Fr>::forward_device(Fr* d_data) { run(d_data, false); }
+void NttDomain<Fr>::forward_device(Fr* d_data, size_t batch) { run(d_data, false, batch); }
 
 template <class Fr>
-void NttDomain<Fr>::inverse_device(Fr* d_data) { run(d_data, true); }
+void NttDomain<Fr>::inverse_device(Fr* d_data, size_t batch) { run(d_data, true, batch); }
 
 template <class Fr>
 void NttDomain<Fr>::forward_host(const Fr* in, size_t len, Fr* out) {
@@ -341,7 +382,7 @@ void NttDomain<Fr>::forward_host(const Fr* in, size_t len, Fr* out) {
   Fr* d = static_cast<Fr*>(io_.ensure(n_ * sizeof(Fr)));
   TA_HIP(hipMemcpyAsync(d, in, len * sizeof(Fr), hipMemcpyHostToDevice, stream_));
   if (len < n_) TA_HIP(hipMemsetAsync(d + len, 0, (n_ - len) * sizeof(Fr), stream_));
-  run(d, false);
+  run(d, false, 1);
   TA_HIP(hipMemcpyAsync(out, d, n_ * sizeof(Fr), hipMemcpyDeviceToHost, stream_));
   TA_HIP(hipStreamSynchronize(stream_));
 }
@@ -352,12 +393,100 @@ void NttDomain<Fr>::inverse_host(const Fr* in, size_t len, Fr* out) {
   Fr* d = static_cast<Fr*>(io_.ensure(n_ * sizeof(Fr)));
   TA_HIP(hipMemcpyAsync(d, in, len * sizeof(Fr), hipMemcpyHostToDevice, stream_));
   if (len < n_) TA_HIP(hipMemsetAsync(d + len, 0, (n_ - len) * sizeof(Fr), stream_));
-  run(d, true);
+  run(d, true, 1);
   TA_HIP(hipMemcpyAsync(out, d, n_ * sizeof(Fr), hipMemcpyDeviceToHost, stream_));
   TA_HIP(hipStreamSynchronize(stream_));
 }
 
+template <class Fr>
+Ntt4Step<Fr>::Ntt4Step(uint32_t log_n, uint32_t log_world, uint32_t rank, hipStream_t stream)
+    : log_n_(log_n), log_g_(log_world), rank_(rank), n_(size_t(1) << log_n), stream_(stream) {
+  require_gpu();
+  log_r_ = log_n / 2;
+  log_c_ = log_n - log_r_;
+  if (log_g_ > log_r_ || rank >= (1u << log_g_) || log_n > (uint32_t)Fr::Config::kTwoAdicity || log_n > 30)
+    throw std::runtime_error("tachyon_mi355x: four-step NTT needs R = 2^floor(L/2) >= world size");
+  if (!stream_) {
+    TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    own_stream_ = true;
+  }
+  dom_r_ = new NttDomain<Fr>(size_t(1) << log_r_, stream_);
+  dom_c_ = new NttDomain<Fr>(size_t(1) << log_c_, stream_);
+  // w_n and its two-level power tables (w_n^e = lo[e & mask] * hi[e >> bits])
+  Fr w = two_adic_root<Fr>();
+  for (uint32_t i = log_n; i < (uint32_t)Fr::Config::kTwoAdicity; ++i) w = w.sqr();
+  pow_bits_ = (log_n + 1) / 2;
+  const size_t lo_cnt = size_t(1) << pow_bits_, hi_cnt = size_t(1) << (log_n - pow_bits_);
+  const Fr wi = w.inverse();
+  DeviceBuffer* bufs[4] = {&w_lo_, &w_hi_, &wi_lo_, &wi_hi_};
+  const Fr bases[2] = {w, wi};
+  for (int d = 0; d < 2; ++d) {
+    Fr step = bases[d];
+    for (uint32_t i = 0; i < pow_bits_; ++i) step = step.sqr();
+    std::vector<Fr> lo_h = host_powers(bases[d], Fr::one(), lo_cnt);
+    std::vector<Fr> hi_h = host_powers(step, Fr::one(), hi_cnt);
+    TA_HIP(hipMemcpyAsync(bufs[2 * d]->ensure(lo_cnt * sizeof(Fr)), lo_h.data(), lo_cnt * sizeof(Fr),
+                          hipMemcpyHostToDevice, stream_));
+    TA_HIP(hipMemcpyAsync(bufs[2 * d + 1]->ensure(hi_cnt * sizeof(Fr)), hi_h.data(), hi_cnt * sizeof(Fr),
+                          hipMemcpyHostToDevice, stream_));
+    TA_HIP(hipStreamSynchronize(stream_));
+  }
+}
+
+template <class Fr>
+Ntt4Step<Fr>::~Ntt4Step() {
+  delete dom_r_;
+  delete dom_c_;
+  if (own_stream_) (void)hipStreamDestroy(stream_);
+}
+
+template <class Fr>
+void Ntt4Step<Fr>::forward_stage1(const Fr* in, Fr* send) {
+  const size_t m = local_size();
+  Fr* work = static_cast<Fr*>(work_.ensure(m * sizeof(Fr)));
+  TA_HIP(hipMemcpyAsync(work, in, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+  const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
+  dom_r_->forward_device(work, size_t(1) << log_cg);
+  hipLaunchKernelGGL(twiddle_exchange_kernel<Fr>, dim3(ceil_div(m, kBlock)), dim3(kBlock), 0, stream_, work, send,
+                     log_r_, log_rg, log_cg, rank_ << log_cg, log_n_, w_lo_.as<Fr>(), w_hi_.as<Fr>(), pow_bits_, 0u);
+  TA_HIP(hipGetLastError());
+}
+
+template <class Fr>
+void Ntt4Step<Fr>::forward_stage2(const Fr* recv, Fr* out) {
+  // recv = [c][k1_l] (C x Rg) -> out = [k1_l][c], then C-point NTTs on the rows
+  const uint32_t rows = 1u << log_c_, cols = 1u << (log_r_ - log_g_);
+  hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(cols, 32), ceil_div(rows, 32)), dim3(kBlock), 0, stream_,
+                     recv, out, rows, cols);
+  TA_HIP(hipGetLastError());
+  dom_c_->forward_device(out, cols);
+}
+
+template <class Fr>
+void Ntt4Step<Fr>::inverse_stage1(const Fr* in, Fr* send) {
+  // in = [k1_l][k2] (Rg x C): inverse C-point NTTs, then transpose to [c][k1_l] = G chunks [c_l][k1_l]
+  const size_t m = local_size();
+  Fr* work = static_cast<Fr*>(work_.ensure(m * sizeof(Fr)));
+  TA_HIP(hipMemcpyAsync(work, in, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+  const uint32_t rows = 1u << (log_r_ - log_g_), cols = 1u << log_c_;
+  dom_c_->inverse_device(work, rows);
+  hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(cols, 32), ceil_div(rows, 32)), dim3(kBlock), 0, stream_,
+                     work, send, rows, cols);
+  TA_HIP(hipGetLastError());
+}
+
+template <class Fr>
+void Ntt4Step<Fr>::inverse_stage2(const Fr* recv, Fr* out) {
+  const size_t m = local_size();
+  const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
+  hipLaunchKernelGGL(twiddle_exchange_kernel<Fr>, dim3(ceil_div(m, kBlock)), dim3(kBlock), 0, stream_, recv, out,
+                     log_r_, log_rg, log_cg, rank_ << log_cg, log_n_, wi_lo_.as<Fr>(), wi_hi_.as<Fr>(), pow_bits_, 1u);
+  TA_HIP(hipGetLastError());
+  dom_r_->inverse_device(out, size_t(1) << log_cg);
+}
+
 template class NttDomain<Bn254Fr>;
 template class NttDomain<Bls381Fr>;
+template class Ntt4Step<Bn254Fr>;
 
 }  // namespace tachyon_amd::ntt

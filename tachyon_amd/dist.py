@@ -6,6 +6,10 @@ results; the multi-GPU MSM is the same decomposition with one chunk per rank.
 The only exchange is one all-gather of the per-rank partial points (affine,
 64 B for BN254 G1) followed by a group sum on every rank -- elliptic-curve
 addition is not an RCCL reduction operator.
+
+The NTT shards as a four-step (Bailey) transform with ONE all-to-all
+(sharded_ntt): local R-point NTTs on column slabs, twiddles,
+all-to-all transpose, local C-point NTTs on row slabs.
 """
 from typing import Callable
 
@@ -49,3 +53,25 @@ def sharded_msm(curve: str, local_msm: Callable[[], bytes], group=None, device=N
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return part
     return combine_partials(curve, all_gather_partials(curve, part, group, device))
+
+
+def sharded_ntt(plan, local, inverse: bool = False, group=None):
+    """Distributed NTT of this rank's slab (tachyon_amd.ntt.FourStepNtt layouts).
+
+    `local` is a uint8 tensor of plan.local_size * 32 bytes (device tensor for
+    the GPU plan); returns the output slab.  The plan's kernels and the RCCL
+    all-to-all run on the same (current) stream, so no extra synchronisation
+    is needed between the stages.
+    """
+    import torch
+    import torch.distributed as dist
+    send = torch.empty_like(local)
+    out = torch.empty_like(local)
+    plan.run_stage(1, inverse, local, send)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        recv = torch.empty_like(local)
+        dist.all_to_all_single(recv, send, group=group)
+    else:
+        recv = send
+    plan.run_stage(2, inverse, recv, out)
+    return out

@@ -108,3 +108,69 @@ class Radix2EvaluationDomain:
         passes = (ctypes.c_float * 16)()
         k = lib().tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(self._d, ctypes.byref(total), passes, 16)
         return total.value, list(passes)[:k]
+
+    def transform_batch_device(self, d_ptr: int, batch: int, inverse: bool = False):
+        """In-place transform of `batch` consecutive arrays of `size` elements in HBM."""
+        lib().tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device(
+            self._d, d_ptr, batch, 1 if inverse else 0)
+
+
+class FourStepNtt:
+    """One rank's plan of the distributed four-step NTT (include/tachyon_mi355x.h,
+    tachyon_mi355x_bn254_ntt4_*).  n = 2^log_n = R*C, R = 2^floor(log_n/2).
+
+    Layouts (see input_indices / output_indices): rank r holds the columns
+    [r C/G, (r+1) C/G) of the R x C view of x, column-major, and produces the
+    rows [r R/G, (r+1) R/G) of X, row-major.  The inverse maps back.
+    """
+
+    def __init__(self, log_n: int, world: int, rank: int, stream: int = 0):
+        if world & (world - 1):
+            raise ValueError("world size must be a power of two")
+        self.log_n, self.world, self.rank = log_n, world, rank
+        self._p = lib().tachyon_mi355x_bn254_ntt4_create(log_n, world.bit_length() - 1, rank, stream or None)
+        if not self._p:
+            raise RuntimeError("four-step NTT plan creation failed")
+        self.local_size = lib().tachyon_mi355x_bn254_ntt4_local_size(self._p)
+
+    def close(self):
+        if self._p:
+            lib().tachyon_mi355x_bn254_ntt4_destroy(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stage(self, stage: int, inverse: bool, d_in: int, d_out: int):
+        """Enqueue stage 1 (in -> send) or 2 (recv -> out) on the plan's stream."""
+        lib().tachyon_mi355x_bn254_ntt4_stage(self._p, stage, 1 if inverse else 0, d_in, d_out)
+
+    def run_stage(self, stage: int, inverse: bool, src, dst):
+        """Tensor form of stage() for tachyon_amd.dist.sharded_ntt (device tensors)."""
+        self.stage(stage, inverse, src.data_ptr(), dst.data_ptr())
+
+    def synchronize(self):
+        lib().tachyon_mi355x_bn254_ntt4_synchronize(self._p)
+
+    @staticmethod
+    def input_indices(log_n: int, world: int, rank: int):
+        """Global index of each local input element: in[c_l*R + r] = x[C*r + c]."""
+        import numpy as np
+        R, C = 1 << (log_n // 2), 1 << (log_n - log_n // 2)
+        cg = C // world
+        c = rank * cg + np.arange(cg)[:, None]
+        r = np.arange(R)[None, :]
+        return (C * r + c).reshape(-1)
+
+    @staticmethod
+    def output_indices(log_n: int, world: int, rank: int):
+        """Global index of each local output element: out[k1_l*C + k2] = X[k1 + R*k2]."""
+        import numpy as np
+        R, C = 1 << (log_n // 2), 1 << (log_n - log_n // 2)
+        rg = R // world
+        k1 = rank * rg + np.arange(rg)[:, None]
+        k2 = np.arange(C)[None, :]
+        return (k1 + R * k2).reshape(-1)
