@@ -97,11 +97,18 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local_rank)
+    # one process per GPU; TACHYON_DIST_BACKEND=gloo rehearses the multi-rank
+    # path with several ranks on one GPU (host-staged collectives)
+    backend = os.environ.get("TACHYON_DIST_BACKEND", "nccl")
+    device_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
+        else:
+            dist.init_process_group(backend)
 
     from tachyon_amd import msm as M
     from tachyon_amd._lib import lib
@@ -137,7 +144,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     consistent = all(r == results[0] for r in results) and (args.warmup == 0 or results[0] == ref)
@@ -183,8 +190,38 @@ def main():
         "msm_phase_ms": phases,
     }
 
-    # ---- NTT 2^24 (rank 0, single GPU) ----
-    if not args.no_ntt and rank == 0:
+    # ---- NTT 2^24: one GPU, or the four-step sharded transform (one RCCL all-to-all) ----
+    if not args.no_ntt and world > 1:
+        from tachyon_amd.ntt import FourStepNtt
+        plan = FourStepNtt(args.ntt_log_n, world, rank, torch.cuda.current_stream().cuda_stream)
+        m = plan.local_size
+        x = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
+        M.gen_scalars("bn254_fr", SEED + 1, m, x.data_ptr(), start=rank * m)
+        torch.cuda.synchronize()
+        orig = x.clone()
+        for _ in range(2):
+            x = D.sharded_ntt(plan, D.sharded_ntt(plan, x), inverse=True)
+        reps = max(2, args.steps)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            x = D.sharded_ntt(plan, D.sharded_ntt(plan, x), inverse=True)
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                         device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item()) / (2 * reps)
+        ok = torch.tensor([1 if torch.equal(x, orig) else 0], dtype=torch.int32,
+                          device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        nn = 1 << args.ntt_log_n
+        out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
+                      "round_trip_ok": bool(ok.item()), "scaling": "strong",
+                      "mode": f"four-step sharded x{world}: local R/C-point NTTs + one RCCL all-to-all "
+                              f"({nn * 32 // world // world} B per rank pair)"}
+        plan.close()
+
+    if not args.no_ntt and world == 1:
         from tachyon_amd.ntt import Radix2EvaluationDomain
         nn = 1 << args.ntt_log_n
         dom = Radix2EvaluationDomain(nn)
@@ -213,7 +250,7 @@ def main():
         avg_pass = sum(passes) / len(passes)
         pass_gbs = nn * NTT_BYTES_PER_ELEM / (avg_pass * 1e-3) / 1e9
         out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
-                      "round_trip_ok": round_trip_ok, "pass_ms": passes,
+                      "round_trip_ok": round_trip_ok, "pass_ms": passes, "mode": "single GPU",
                       "roofline": {"bound": "hbm", "achieved": pass_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": pass_gbs / HBM_PEAK_GBS, "traffic": None,
                                    "kernel": "dif_pass_kernel", "kernel_ms": avg_pass}}

@@ -32,6 +32,14 @@ def combine_partials(curve: str, partials: bytes) -> bytes:
     return affine_sum(curve, partials)
 
 
+def _host_collectives(group=None) -> bool:
+    """gloo takes host tensors: it is the CPU rehearsal backend of the multi-rank
+    path (tests, or bench.py with TACHYON_DIST_BACKEND=gloo on a one-GPU box);
+    nccl (= RCCL on ROCm) moves device tensors over xGMI."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
+
+
 def all_gather_partials(curve: str, partial: bytes, group=None, device=None) -> bytes:
     """All-gather every rank's affine partial; returns the concatenation in rank order."""
     import torch
@@ -39,7 +47,7 @@ def all_gather_partials(curve: str, partial: bytes, group=None, device=None) -> 
     pb = CURVE_INFO[curve][0]
     world = dist.get_world_size(group)
     t = torch.frombuffer(bytearray(partial), dtype=torch.uint8)
-    if device is not None:
+    if device is not None and not _host_collectives(group):
         t = t.to(device)
     out = torch.empty(world * pb, dtype=torch.uint8, device=t.device)
     dist.all_gather_into_tensor(out, t, group=group)
@@ -69,8 +77,13 @@ def sharded_ntt(plan, local, inverse: bool = False, group=None):
     out = torch.empty_like(local)
     plan.run_stage(1, inverse, local, send)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        recv = torch.empty_like(local)
-        dist.all_to_all_single(recv, send, group=group)
+        if send.is_cuda and _host_collectives(group):
+            recv_h = torch.empty(send.shape, dtype=send.dtype)
+            dist.all_to_all_single(recv_h, send.cpu(), group=group)
+            recv = recv_h.to(send.device)
+        else:
+            recv = torch.empty_like(local)
+            dist.all_to_all_single(recv, send, group=group)
     else:
         recv = send
     plan.run_stage(2, inverse, recv, out)
