@@ -37,13 +37,22 @@ struct MsmPlan {
 };
 
 // Window size: more bits -> fewer windows (fewer madds, fewer sort passes)
-// but more buckets to reduce.  n*W madds dominate; bucket reduction costs
-// ~2*W*2^(c-1) adds.  Tuned on MI355X.
+// but more buckets to reduce.  n*W madds dominate at large n; below ~2^20 the
+// latency of the bucket/window reduction sets a ~1 ms floor, which favours
+// few windows.  Table = fastest c of the BN254 G1 sweeps on MI355X
+// (tools/tune_msm.py); only c with a distinct window count
+// (W = ceil(255/c)) are candidates.
+inline unsigned default_window_bits(unsigned lg) {
+  static constexpr unsigned kBest[] = {8, 10, 13, 15, 16, 16, 17, 17, 20, 20, 20};  // lg = 16 .. 26
+  if (lg < 16) return (unsigned)std::max<int>(4, (int)lg - 7);
+  return kBest[std::min<unsigned>(lg, 26) - 16];
+}
+
 inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
   MsmPlan p;
   unsigned lg = 1;
   while ((size_t(1) << lg) < n) ++lg;
-  unsigned c = force_c ? force_c : (unsigned)std::clamp<int>((int)lg - 6, 4, 20);
+  unsigned c = force_c ? force_c : default_window_bits(lg);
   p.c = c;
   p.windows = (scalar_bits + 1 + c - 1) / c;  // W*c >= bits+1
   p.buckets = 1u << (c - 1);
@@ -51,7 +60,7 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
   // aim for ~2^20 accumulation threads; K in [8, 512]
   size_t k = entries >> 20;
   p.K = (unsigned)std::clamp<size_t>(k, 8, 512);
-  p.K2 = 16;
+  p.K2 = 16;  // (binary levels measured slower here: more launches and level traffic)
   size_t maxchunks = (n + p.K - 1) / p.K;  // worst case: all entries of a window in one bucket
   p.levels = 0;
   while (maxchunks > 1) {

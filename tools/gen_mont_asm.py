@@ -15,7 +15,10 @@ and the Montgomery quotient digit m_k = acc.lo * (-p^-1) is folded in as the
 column ends (FIPS), so there is no separate reduction pass.
 
 Each column's products are one asm statement (hipcc pads one s_nop after every
-statement boundary, so per-product statements cost a nop each).
+statement boundary, so per-product statements cost a nop each).  The statements
+are not volatile: they are pure functions of their operands, and letting the
+scheduler interleave independent products (the several muls of one point
+addition) cut the latency-bound bucket/window reduction by ~20% on MI355X.
 """
 import os
 
@@ -79,7 +82,7 @@ def asm_stmt(pairs, fresh_c2=False):
     c2 = '[c2] "=&v"(c2)' if fresh_c2 else '[c2] "+&v"(c2)'
     nsg = min(NCARRY, len(pairs))
     sg = ", ".join(f'[s{i}] "=&s"(sc[{i}])' for i in range(nsg))
-    return (f'    asm volatile("{text}"\n'
+    return (f'    asm("{text}"\n'
             f'                 : [acc] "+&v"(acc), {c2}, {sg}\n'
             f'                 : {", ".join(ins)}\n'
             f'                 : "vcc");\n')
@@ -102,7 +105,7 @@ def gen(N):
         pairs.append((f"a{k}", "b0"))
         lines.append(f"  {{  // column {k}")
         if k == 0:  # a0*b0 + 0 cannot carry out
-            lines.append('    asm volatile("v_mad_u64_u32 %[acc], %[s0], %[a0], %[b0], %[acc]"\n'
+            lines.append('    asm("v_mad_u64_u32 %[acc], %[s0], %[a0], %[b0], %[acc]"\n'
                          '                 : [acc] "+&v"(acc), [s0] "=&s"(sc[0])\n'
                          '                 : [a0] "v"(a[0]), [b0] "v"(b[0]));')
             lines.append("    c2 = 0;")
