@@ -292,6 +292,40 @@ struct Fp2 {
   }
 };
 
+// The same field with every product inlined.  Wide fields (BLS12-381 Fq, and
+// Fq2 through Fp2<HotFp<Fq>>) multiply out of line by default to bound code
+// size and compile time; the one hot kernel of a curve (the MSM bucket
+// accumulation) views its data through this type instead, which has the same
+// layout.
+template <class F>
+struct HotFp : F {
+  HotFp() = default;
+  TA_HD HotFp(const F& f) : F(f) {}
+  TA_HD static HotFp zero() { return F::zero(); }
+  TA_HD static HotFp one() { return F::one(); }
+  TA_HD HotFp operator+(const HotFp& o) const { return F::operator+(o); }
+  TA_HD HotFp operator-(const HotFp& o) const { return F::operator-(o); }
+  TA_HD HotFp operator-() const { return F::operator-(); }
+  TA_HD HotFp operator*(const HotFp& o) const { return F::mul_inline(o); }
+  TA_HD HotFp dbl() const { return F::dbl(); }
+  TA_HD HotFp sqr() const { return F::mul_inline(*this); }
+  TA_HD HotFp inverse() const { return F::inverse(); }
+  TA_HD HotFp canonical() const { return F::canonical(); }
+};
+
+template <class F>
+struct HotOf {
+  using type = F;
+};
+template <class Cfg>
+struct HotOf<Fp<Cfg>> {
+  using type = HotFp<Fp<Cfg>>;
+};
+template <class F>
+struct HotOf<Fp2<F>> {
+  using type = Fp2<HotFp<F>>;
+};
+
 using Bn254Fq = Fp<consts::bn254_fq>;
 using Bn254Fr = Fp<consts::bn254_fr>;
 using Bls381Fq = Fp<consts::bls12_381_fq>;

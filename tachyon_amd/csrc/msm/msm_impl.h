@@ -89,7 +89,10 @@ __global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename C
                                                          XYZZ<typename Curve::F>* __restrict__ pieces,
                                                          uint32_t* __restrict__ tflags,
                                                          uint32_t* __restrict__ tlast) {
-  using F = typename Curve::F;
+  using F = typename HotOf<typename Curve::F>::type;  // inline products in this kernel (same layout)
+  const Affine<F>* __restrict__ hbases = reinterpret_cast<const Affine<F>*>(bases);
+  XYZZ<F>* __restrict__ hsum = reinterpret_cast<XYZZ<F>*>(bucket_sum);
+  XYZZ<F>* __restrict__ hpieces = reinterpret_cast<XYZZ<F>*>(pieces);
   const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t g0 = t * K;
   if (g0 >= total) return;
@@ -110,17 +113,17 @@ __global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename C
   uint32_t k0 = keys[g0], v0 = vals[g0];
   uint32_t k1 = 0, v1 = 0;
   if (g0 + 1 < g1) { k1 = keys[g0 + 1]; v1 = vals[g0 + 1]; }
-  Affine<F> P = bases[v0 & ~kSignBit];
+  Affine<F> P = hbases[v0 & ~kSignBit];
   for (uint64_t g = g0; g < g1; ++g) {
     uint32_t k2 = 0, v2 = 0;
     if (g + 2 < g1) { k2 = keys[g + 2]; v2 = vals[g + 2]; }
-    Affine<F> Pn = bases[v1 & ~kSignBit];
+    Affine<F> Pn = hbases[v1 & ~kSignBit];
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
       if (b != cur) {
         if (cur != kNoBucket) {  // close a run that is not the last one
-          if (runs == 1 && cur == prev_b) { pieces[2 * t] = acc; flags |= kHead; }
-          else bucket_sum[cur] = acc;
+          if (runs == 1 && cur == prev_b) { hpieces[2 * t] = acc; flags |= kHead; }
+          else hsum[cur] = acc;
         }
         cur = b;
         ++runs;
@@ -135,16 +138,16 @@ __global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename C
   if (cur != kNoBucket) {  // the last run
     const bool head = runs == 1 && cur == prev_b;
     const bool tail = cur == next_b;
-    if (head) { pieces[2 * t] = acc; flags |= kHead; }
+    if (head) { hpieces[2 * t] = acc; flags |= kHead; }
     if (tail) flags |= kTail;
-    if (tail && !head) pieces[2 * t + 1] = acc;
-    if (!head && !tail) bucket_sum[cur] = acc;
+    if (tail && !head) hpieces[2 * t + 1] = acc;
+    if (!head && !tail) hsum[cur] = acc;
   }
   if (runs <= 1) flags |= kSingle;
   // absent pieces are the identity so every chain sums a contiguous range
-  if (!(flags & kHead)) pieces[2 * t] = XYZZ<F>::zero();
+  if (!(flags & kHead)) hpieces[2 * t] = XYZZ<F>::zero();
   const bool through = (flags & kHead) && (flags & kTail) && (flags & kSingle);
-  if (!(flags & kTail) || through) pieces[2 * t + 1] = XYZZ<F>::zero();
+  if (!(flags & kTail) || through) hpieces[2 * t + 1] = XYZZ<F>::zero();
   tflags[t] = flags;
   tlast[t] = cur;
 }
@@ -234,17 +237,18 @@ __global__ __launch_bounds__(kBlock) void seg_reduce_kernel(const XYZZ<typename 
                                                             unsigned K2, XYZZ<typename Curve::F>* __restrict__ out,
                                                             const uint32_t* __restrict__ bucket,
                                                             XYZZ<typename Curve::F>* __restrict__ bucket_sum) {
-  using F = typename Curve::F;
+  using F = typename HotOf<typename Curve::F>::type;  // inline products (same layout)
+  const XYZZ<F>* hin = reinterpret_cast<const XYZZ<F>*>(in);
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= out_off[nseg]) return;
   uint32_t s = find_segment(out_off, nseg, t);
   uint32_t q = t - out_off[s];
   uint32_t e0 = beg[s] + q * K2;
   uint32_t e1 = min(end[s], e0 + K2);
-  XYZZ<F> acc = in[e0];
-  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc + in[e];
-  if (bucket) bucket_sum[bucket[s]] = acc;
-  else out[t] = acc;
+  XYZZ<F> acc = hin[e0];
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc + hin[e];
+  if (bucket) reinterpret_cast<XYZZ<F>*>(bucket_sum)[bucket[s]] = acc;
+  else reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
 }
 
 // m * P for a small non-negative integer m (double-and-add, high bit first)
@@ -270,19 +274,19 @@ template <class Curve>
 __global__ __launch_bounds__(kBlock) void window_segment_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                                 unsigned W, unsigned B, unsigned L,
                                                                 XYZZ<typename Curve::F>* __restrict__ out) {
-  using F = typename Curve::F;
+  using F = typename HotOf<typename Curve::F>::type;
   uint32_t S = B / L;
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= W * S) return;
   uint32_t w = t / S, j = t - w * S;
-  const XYZZ<F>* bs = bucket_sum + (size_t)w * B + (size_t)j * L;
+  const XYZZ<F>* bs = reinterpret_cast<const XYZZ<F>*>(bucket_sum) + (size_t)w * B + (size_t)j * L;
   XYZZ<F> R = XYZZ<F>::zero(), acc = XYZZ<F>::zero();
   for (int k = (int)L - 1; k >= 0; --k) {
     R = R + bs[k];
     acc = acc + R;
   }
   acc = acc + small_mul(R, j * L);
-  out[t] = acc;
+  reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
 }
 
 // Window reduction, stage 2: sum K2 consecutive segment sums per window.
@@ -290,16 +294,16 @@ template <class Curve>
 __global__ __launch_bounds__(kBlock) void reduce_uniform_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                                 unsigned W, unsigned S_in, unsigned K2,
                                                                 XYZZ<typename Curve::F>* __restrict__ out) {
-  using F = typename Curve::F;
+  using F = typename HotOf<typename Curve::F>::type;
   uint32_t S_out = (S_in + K2 - 1) / K2;
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= W * S_out) return;
   uint32_t w = t / S_out, q = t - w * S_out;
   uint32_t e0 = q * K2, e1 = min(S_in, e0 + K2);
-  const XYZZ<F>* src = in + (size_t)w * S_in;
+  const XYZZ<F>* src = reinterpret_cast<const XYZZ<F>*>(in) + (size_t)w * S_in;
   XYZZ<F> acc = src[e0];
   for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc + src[e];
-  out[t] = acc;
+  reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
 }
 
 inline unsigned grid_for(size_t threads) { return (unsigned)std::max<size_t>(1, (threads + kBlock - 1) / kBlock); }

@@ -21,21 +21,24 @@ def main():
     ap.add_argument("--non-uniform", action="store_true")
     ap.add_argument("--variants", type=int, nargs="+", default=[0])
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--curve", default="bn254_g1")
     args = ap.parse_args()
     import torch
     from tachyon_amd import msm as M
     for lg in args.log_n:
         n = 1 << lg
-        d_b = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+        from tachyon_amd._lib import CURVE_INFO
+        pb, sf = CURVE_INFO[args.curve]
+        d_b = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
         d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
-        M.gen_bases("bn254_g1", 1, n, 1024, d_b.data_ptr())
+        M.gen_bases(args.curve, 1, n, 1024, d_b.data_ptr())
         if args.non_uniform:
-            M.gen_scalars("bn254_fr", 1, 1, d_s.data_ptr())
+            M.gen_scalars(sf, 1, 1, d_s.data_ptr())
             d_s.view(n, 32)[:] = d_s[:32]
         else:
-            M.gen_scalars("bn254_fr", 1, n, d_s.data_ptr())
+            M.gen_scalars(sf, 1, n, d_s.data_ptr())
         torch.cuda.synchronize()
-        m = M.VariableBaseMSMGpu("bn254_g1")
+        m = M.VariableBaseMSMGpu(args.curve)
         ref = None
         for c, var in [(c, v) for _ in range(args.rounds) for c in args.c for v in args.variants]:
             m.set_window_bits(c)
@@ -51,7 +54,7 @@ def main():
                 times.append(m.last_timings())
                 assert r == ref
             best = min(range(args.reps), key=lambda i: walls[i])
-            print(json.dumps({"log_n": lg, "c": c or M.plan("bn254_g1", n)[0], "variant": var, "wall_ms": round(walls[best], 3),
+            print(json.dumps({"curve": args.curve, "log_n": lg, "c": c or M.plan(args.curve, n)[0], "variant": var, "wall_ms": round(walls[best], 3),
                               **{k: round(v, 3) for k, v in times[best].items()}}), flush=True)
         m.close()
 
