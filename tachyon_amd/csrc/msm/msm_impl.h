@@ -80,8 +80,26 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 //   * the first run, if the bucket started in an earlier thread ("head"), and
 //     the last run, if it continues into the next thread ("tail"), go to
 //     pieces[2t] / pieces[2t+1] and are joined by the chain kernels below.
+// Minimum waves per SIMD of the point-arithmetic kernels.  Left alone, the
+// scheduler interleaves the three Karatsuba products of an Fq2 multiply and
+// the G2 kernels land at 256+ VGPRs = one wave per SIMD; capping them at two
+// waves (a little scratch) made the BN254 G2 2^24 accumulation 89 -> 61 ms
+// and BLS12-381 G2 212 -> 174 ms.
 template <class Curve>
-__global__ __launch_bounds__(kBlock) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
+struct AccWaves {
+  static constexpr int value = 1;
+};
+template <>
+struct AccWaves<Bn254G2> {
+  static constexpr int value = 2;
+};
+template <>
+struct AccWaves<Bls381G2> {
+  static constexpr int value = 2;
+};
+
+template <class Curve>
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
                                                          const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, uint32_t c,
                                                          uint64_t total, uint32_t K,
@@ -230,7 +248,7 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ of
 // in[beg[s] + q*K2 .. min(end[s], +K2)).  On the last level every segment has
 // one output, which goes to bucket_sum[bucket[s]].
 template <class Curve>
-__global__ __launch_bounds__(kBlock) void seg_reduce_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_reduce_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                             const uint32_t* __restrict__ beg,
                                                             const uint32_t* __restrict__ end,
                                                             const uint32_t* __restrict__ out_off, uint32_t nseg,
@@ -271,7 +289,7 @@ __device__ XYZZ<F> small_mul(const XYZZ<F>& P, uint32_t m) {
 // sum_b (b+1) B_b is S + jL * R  (PippengerBase::AccumulateBuckets,
 // pippenger_base.h:36-57, split across threads).
 template <class Curve>
-__global__ __launch_bounds__(kBlock) void window_segment_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_segment_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                                 unsigned W, unsigned B, unsigned L,
                                                                 XYZZ<typename Curve::F>* __restrict__ out) {
   using F = typename HotOf<typename Curve::F>::type;
@@ -291,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void window_segment_kernel(const XYZZ<typen
 
 // Window reduction, stage 2: sum K2 consecutive segment sums per window.
 template <class Curve>
-__global__ __launch_bounds__(kBlock) void reduce_uniform_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void reduce_uniform_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                                 unsigned W, unsigned S_in, unsigned K2,
                                                                 XYZZ<typename Curve::F>* __restrict__ out) {
   using F = typename HotOf<typename Curve::F>::type;
