@@ -298,7 +298,7 @@ void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8
   GUARD_BEGIN CURVE_DISPATCH(curve, {
     const msm::MsmTimings& t = static_cast<const MsmCtx<C>*>(ctx)->impl.timings();
     out8[0] = t.h2d; out8[1] = t.recode; out8[2] = t.sort; out8[3] = t.prep; out8[4] = t.acc; out8[5] = t.reduce;
-    out8[6] = t.total; out8[7] = 0.f;
+    out8[6] = t.total; out8[7] = t.acc_launches;
   }) GUARD_END
 }
 void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows) {

@@ -33,6 +33,7 @@ struct MsmPlan {
   unsigned K2 = 16;      // fan-in of the partial-reduction levels
   unsigned levels = 0;   // number of K2 levels
   unsigned seg = 0;      // buckets per running-sum segment
+  unsigned group = 0;    // windows per sort/accumulate pipeline stage
   static inline MsmPlan make(size_t n, unsigned scalar_bits, unsigned force_c = 0);
 };
 
@@ -57,9 +58,17 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
   p.windows = (scalar_bits + 1 + c - 1) / c;  // W*c >= bits+1
   p.buckets = 1u << (c - 1);
   size_t entries = (size_t)n * p.windows;
-  // aim for ~2^20 accumulation threads; K in [8, 512]
+  // One sort + one accumulation launch over all windows.  (Pipelining one
+  // window at a time -- window w+1 sorting on a second stream while window w
+  // accumulates -- measured slower at 2^26: 108 vs 99 ms; the onesweep sort
+  // and the accumulation slow each other down by about the time they
+  // overlap.  set_variant bits 2-3 keep it for experiments.)
+  p.group = p.windows;
+  // entries per accumulation thread: ~2^20 threads, K in [8, 256]
+  // (2^26 sweep: K = 128/256/512/1024 -> 99.9/98.9/99.1/99.3 ms)
   size_t k = entries >> 20;
-  p.K = (unsigned)std::clamp<size_t>(k, 8, 512);
+  if (p.group == 1) k = n >> 18;  // ~1024 workgroups per window launch
+  p.K = (unsigned)std::clamp<size_t>(k, 8, 256);
   p.K2 = 16;  // (binary levels measured slower here: more launches and level traffic)
   size_t maxchunks = (n + p.K - 1) / p.K;  // worst case: all entries of a window in one bucket
   p.levels = 0;
@@ -80,6 +89,7 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
 // Per-phase device timings of the last run (ms), filled when profiling is on.
 struct MsmTimings {
   float h2d = 0, recode = 0, sort = 0, prep = 0, acc = 0, reduce = 0, total = 0;
+  float acc_launches = 0;  // acc = sum over this many accumulation launches
 };
 
 template <class Curve>
@@ -117,6 +127,9 @@ class MsmGpu {
 
  private:
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
+  void ensure_group_events(unsigned groups);
+  hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
+                        uint32_t* vout, size_t count, unsigned end_bit, hipStream_t s);
 
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;
@@ -127,6 +140,10 @@ class MsmGpu {
   DeviceBuffer bases_, scalars_, keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_;
   DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_, buckets_;
   hipEvent_t ev_[8] = {};
+  hipStream_t sort_stream_ = nullptr;  // group sorts run here, overlapping the accumulation on stream_
+  std::vector<hipEvent_t> gev_sorted_, gev_acc0_, gev_acc1_;
+  unsigned acc_launches_ = 0;
+  unsigned sort_bits_ = 0;
   DeviceBuffer maxlen_;
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;

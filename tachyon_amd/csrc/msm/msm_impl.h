@@ -102,7 +102,8 @@ template <class Curve>
 __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
                                                          const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, uint32_t c,
-                                                         uint64_t total, uint32_t K,
+                                                         uint64_t gbeg, uint64_t gend, uint64_t tbase,
+                                                         uint32_t K,
                                                          XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                          XYZZ<typename Curve::F>* __restrict__ pieces,
                                                          uint32_t* __restrict__ tflags,
@@ -111,18 +112,21 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
   const Affine<F>* __restrict__ hbases = reinterpret_cast<const Affine<F>*>(bases);
   XYZZ<F>* __restrict__ hsum = reinterpret_cast<XYZZ<F>*>(bucket_sum);
   XYZZ<F>* __restrict__ hpieces = reinterpret_cast<XYZZ<F>*>(pieces);
-  const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t g0 = t * K;
-  if (g0 >= total) return;
-  const uint64_t g1 = min(g0 + K, total);
+  const uint64_t tl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t g0 = gbeg + tl * K;
+  if (g0 >= gend) return;
+  const uint64_t g1 = min(g0 + K, gend);
+  const uint64_t t = tbase + tl;  // global thread slot (pieces/flags are in entry order)
   const uint32_t dmask = (1u << c) - 1;
   // bucket id (w * 2^(c-1) + |digit| - 1) of a combined key, or none for digit 0
   auto bucket_of_key = [&](uint32_t key) -> uint32_t {
     uint32_t d = key & dmask;
     return d ? ((key >> c) << (c - 1)) + (d - 1) : kNoBucket;
   };
-  const uint32_t prev_b = g0 ? bucket_of_key(keys[g0 - 1]) : kNoBucket;
-  const uint32_t next_b = (g1 < total) ? bucket_of_key(keys[g1]) : kNoBucket;
+  // neighbours outside this launch's entry range belong to other windows
+  // (possibly not sorted yet): they never share a bucket
+  const uint32_t prev_b = g0 > gbeg ? bucket_of_key(keys[g0 - 1]) : kNoBucket;
+  const uint32_t next_b = (g1 < gend) ? bucket_of_key(keys[g1]) : kNoBucket;
 
   uint32_t flags = 0, runs = 0, cur = kNoBucket;
   XYZZ<F> acc = XYZZ<F>::zero();
@@ -337,6 +341,7 @@ MsmGpu<Curve>::MsmGpu(hipStream_t stream) : stream_(stream) {
     TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     own_stream_ = true;
   }
+  TA_HIP(hipStreamCreateWithFlags(&sort_stream_, hipStreamNonBlocking));
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
   TA_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_max_), 2 * sizeof(uint32_t), hipHostMallocDefault));
 }
@@ -344,8 +349,48 @@ MsmGpu<Curve>::MsmGpu(hipStream_t stream) : stream_(stream) {
 template <class Curve>
 MsmGpu<Curve>::~MsmGpu() {
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+  for (auto* v : {&gev_sorted_, &gev_acc0_, &gev_acc1_})
+    for (auto& e : *v) (void)hipEventDestroy(e);
+  if (sort_stream_) (void)hipStreamDestroy(sort_stream_);
   if (h_max_) (void)hipHostFree(h_max_);
   if (own_stream_) (void)hipStreamDestroy(stream_);
+}
+
+template <class Curve>
+void MsmGpu<Curve>::ensure_group_events(unsigned groups) {
+  while (gev_sorted_.size() < groups) {
+    hipEvent_t a, b, c;
+    TA_HIP(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    TA_HIP(hipEventCreate(&b));
+    TA_HIP(hipEventCreate(&c));
+    gev_sorted_.push_back(a);
+    gev_acc0_.push_back(b);
+    gev_acc1_.push_back(c);
+  }
+}
+
+// rocPRIM pairs sort of [0, end_bit) key bits; sort_bits_ != 0 selects a
+// onesweep digit width (A/B tuning, set_variant bits 4-5)
+template <unsigned Bits>
+using OnesweepCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, Bits,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+template <class Curve>
+hipError_t MsmGpu<Curve>::sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout,
+                                     const uint32_t* vin, uint32_t* vout, size_t count, unsigned end_bit,
+                                     hipStream_t s) {
+  switch (sort_bits_) {
+    case 10:
+      return rocprim::radix_sort_pairs<OnesweepCfg<10>>(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+    case 11:
+      return rocprim::radix_sort_pairs<OnesweepCfg<11>>(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+    case 7:
+      return rocprim::radix_sort_pairs<OnesweepCfg<7>>(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+    default:
+      return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+  }
 }
 
 template <class Curve>
@@ -356,8 +401,19 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   const size_t nb = (size_t)W * B;
   if (n >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM size must be < 2^31 per device");
   const uint32_t K = plan.K;
-  const size_t T = (entries + K - 1) / K;  // accumulation threads
+  // window groups: group g covers windows [g*G, min(W, (g+1)*G)), i.e. the
+  // contiguous entry range [w0*n, w1*n); its sort (sort stream) overlaps the
+  // accumulation of the previous group (MSM stream) -- the sort is HBM-bound,
+  // the accumulation VALU-bound, so they share the CUs well
+  const unsigned G = std::max(1u, std::min(plan.group, W));
+  const unsigned ngroups = (W + G - 1) / G;
+  size_t T = 0;  // accumulation threads over all groups
+  for (unsigned g = 0; g < ngroups; ++g) {
+    const unsigned w0 = g * G, w1 = std::min(W, w0 + G);
+    T += ((size_t)(w1 - w0) * n + K - 1) / K;
+  }
   if (T >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM too large for the chunking");
+  ensure_group_events(ngroups);
 
   uint32_t* keys = static_cast<uint32_t*>(keys_.ensure(entries * 4));
   uint32_t* vals = static_cast<uint32_t*>(vals_.ensure(entries * 4));
@@ -383,26 +439,40 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
                      W, keys, vals);
   TA_HIP(hipGetLastError());
-  if (profile_) TA_HIP(hipEventRecord(ev_[2], stream_));
-
-  // ---- one radix sort of all (window, bucket, point) entries ----
-  unsigned wbits = 0;
-  while ((1u << wbits) < W) ++wbits;
-  const unsigned key_bits = c + wbits;
-  size_t sort_bytes = 0;
-  TA_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, entries, 0, key_bits, stream_));
-  void* sort_tmp = sort_tmp_.ensure(sort_bytes);
-  TA_HIP(rocprim::radix_sort_pairs(sort_tmp, sort_bytes, keys, keys2, vals, vals2, entries, 0, key_bits, stream_));
-  if (profile_) TA_HIP(hipEventRecord(ev_[3], stream_));
-
-  // ---- accumulation (every bucket without an entry stays the identity) ----
+  // every bucket without an entry stays the identity
   TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * sizeof(Point), stream_));
   TA_HIP(hipMemsetAsync(dscal, 0, 2 * sizeof(uint32_t), stream_));
-  if (profile_) TA_HIP(hipEventRecord(ev_[6], stream_));
-  hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(T)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2, c,
-                     (uint64_t)entries, K, bucket_sum, pieces, tflags, tlast);
-  TA_HIP(hipGetLastError());
-  if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));
+  TA_HIP(hipEventRecord(ev_[2], stream_));  // recode done (also the profile mark)
+  TA_HIP(hipStreamWaitEvent(sort_stream_, ev_[2], 0));
+
+  // ---- per group: radix sort of its (window, bucket, point) entries, then accumulation ----
+  unsigned wbits = 0;
+  while ((1u << wbits) < W) ++wbits;
+  const unsigned key_bits = (G == 1) ? c : c + wbits;  // the window bits only matter within a multi-window group
+  const size_t max_group_entries = (size_t)G * n;
+  size_t sort_bytes = 0;
+  TA_HIP(sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, max_group_entries, key_bits, sort_stream_));
+  void* sort_tmp = sort_tmp_.ensure(sort_bytes);
+  size_t tbase = 0;
+  acc_launches_ = ngroups;
+  for (unsigned g = 0; g < ngroups; ++g) {
+    const unsigned w0 = g * G, w1 = std::min(W, w0 + G);
+    const size_t e0 = (size_t)w0 * n, ecount = (size_t)(w1 - w0) * n;
+    size_t bytes = sort_bytes;
+    TA_HIP(sort_pairs(sort_tmp, bytes, keys + e0, keys2 + e0, vals + e0, vals2 + e0, ecount, key_bits,
+                      sort_stream_));
+    TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream_));
+    TA_HIP(hipStreamWaitEvent(stream_, gev_sorted_[g], 0));
+    if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
+    const size_t Tg = (ecount + K - 1) / K;
+    hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2, c,
+                       (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, bucket_sum, pieces, tflags, tlast);
+    TA_HIP(hipGetLastError());
+    if (profile_) TA_HIP(hipEventRecord(gev_acc1_[g], stream_));
+    tbase += Tg;
+  }
+  if (profile_) TA_HIP(hipEventRecord(ev_[3], sort_stream_));  // last sort done
+  if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));        // last accumulation done
 
   // ---- join buckets that cross thread boundaries ----
   hipLaunchKernelGGL(chain_mark_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, stream_, tflags, (uint32_t)T,
@@ -494,6 +564,14 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
     case 3: plan.K = std::max(4u, plan.K / 2); break;
     default: break;
   }
+  switch ((variant_ >> 2) & 3) {  // windows per sort/accumulate group
+    case 1: plan.group = 1; break;
+    case 2: plan.group = 2; break;
+    case 3: plan.group = plan.windows; break;
+    default: break;
+  }
+  static constexpr unsigned kSortBits[] = {0, 10, 11, 7};
+  sort_bits_ = kSortBits[(variant_ >> 4) & 3];
   if (plan_out) *plan_out = plan;
   out->assign(plan.windows, Point::zero());
   if (n == 0) return;
@@ -519,8 +597,16 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
     TA_HIP(hipEventElapsedTime(&timings_.h2d, ev_[0], ev_[1]));
     TA_HIP(hipEventElapsedTime(&timings_.recode, ev_[1], ev_[2]));
     TA_HIP(hipEventElapsedTime(&timings_.sort, ev_[2], ev_[3]));
-    TA_HIP(hipEventElapsedTime(&timings_.prep, ev_[3], ev_[6]));
-    TA_HIP(hipEventElapsedTime(&timings_.acc, ev_[6], ev_[4]));
+    // sort: recode end -> last sort end; prep: recode end -> last accumulation end
+    // (sort and accumulation overlap); acc: sum of the accumulation launches
+    TA_HIP(hipEventElapsedTime(&timings_.prep, ev_[2], ev_[4]));
+    timings_.acc = 0;
+    for (unsigned g = 0; g < acc_launches_; ++g) {
+      float ms = 0;
+      TA_HIP(hipEventElapsedTime(&ms, gev_acc0_[g], gev_acc1_[g]));
+      timings_.acc += ms;
+    }
+    timings_.acc_launches = (float)acc_launches_;
     TA_HIP(hipEventElapsedTime(&timings_.reduce, ev_[4], ev_[5]));
     TA_HIP(hipEventElapsedTime(&timings_.total, ev_[0], ev_[5]));
   }

@@ -105,7 +105,7 @@ class VariableBaseMSMGpu:
     def last_timings(self) -> dict:
         out = (ctypes.c_float * 8)()
         lib().tachyon_mi355x_msm_gpu_last_timings(self.curve_id, self._ctx, out)
-        return dict(zip(("h2d", "recode", "sort", "prep", "acc", "reduce", "total"), list(out)))
+        return dict(zip(("h2d", "recode", "sort", "prep", "acc", "reduce", "total", "acc_launches"), list(out)))
 
 
 def plan(curve: str, n: int):

@@ -9,19 +9,23 @@ import sys
 
 
 def short(name):
-    base = name.replace("(anonymous namespace)", "anon").split("(")[0]
-    for key in ("acc_kernel", "dif_pass_kernel", "reduce_level_kernel", "window_segment_kernel", "bounds_kernel",
-                "recode_kernel", "reduce_uniform_kernel", "gen_bases_kernel", "gen_scalars_kernel",
-                "chunk_count_kernel", "level_count_kernel", "twiddle_stage_kernel", "twiddle_base_kernel",
-                "segmented_acc_kernel", "fixup_kernel"):
-        if key in base:
-            return key
-    if "rocprim" in base:
+    """Kernel function name without namespaces, template arguments or parameters."""
+    if "rocprim" in name:
         for key in ("onesweep_histograms", "onesweep_iteration", "radix_sort", "lookback_scan", "scan"):
             if key in name:
                 return "rocprim::" + key
         return "rocprim::other"
-    return base.split("::")[-1][:60]
+    base = name.replace("(anonymous namespace)", "anon")
+    depth, out = 0, []
+    for ch in base:  # drop <...> template arguments
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth = max(0, depth - 1)
+        elif depth == 0:
+            out.append(ch)
+    base = "".join(out).split("(")[0].strip()
+    return base.split("::")[-1].split()[-1][:60] if base else name[:60]
 
 
 def main(d):
