@@ -267,6 +267,42 @@ TACHYON_C_EXPORT void tachyon_mi355x_field_op(int field, int op, const void* a, 
 /* point op: 0 add (affine + affine), 1 double, 2 add-mixed into xyzz of a. Affine in/out. */
 TACHYON_C_EXPORT void tachyon_mi355x_ec_op(int curve, int op, const void* a, const void* b, void* out, size_t count);
 
+/* Groth16 prover over a circom zkey (no reference C-ABI --
+ * the reference drives this path from C++: vendors/circom/prover_main.cc:82-160,
+ * QuadraticArithmeticProgram::WitnessMapFromMatrices
+ * (quadratic_arithmetic_program.h:24-113), CreateProofWithAssignment(NoZK)
+ * (tachyon/zk/r1cs/groth16/prove.h:52-186)).  The zkey bytes (v1, BN254 or
+ * BLS12-381) are parsed and the proving key uploaded once at create; a proof
+ * uploads only the witness.  Field elements are Montgomery form.
+ *   info: out4 = {curve (0 bn254, 1 bls12_381), num_vars, num_public, domain_size}
+ *   prove: full = num_vars assignments (full[0] = 1; host or device pointer),
+ *          r, s = blinding scalars or NULL for zero (the NoZK proof);
+ *          out_a: G1 affine, out_b: G2 affine, out_c: G1 affine (canonical).
+ *   witness_map: the h evaluations on the coset (domain_size Fr) to host memory.
+ *   last_timings (profiling on): upload, qap, msm_a, msm_b2, msm_b1, msm_l,
+ *          msm_h, total -- ms, 8 floats. */
+typedef struct tachyon_mi355x_groth16_prover tachyon_mi355x_groth16_prover;
+TACHYON_C_EXPORT tachyon_mi355x_groth16_prover* tachyon_mi355x_groth16_prover_create(const uint8_t* zkey,
+                                                                                     size_t len);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_prover_destroy(tachyon_mi355x_groth16_prover* prover);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_prover_info(const tachyon_mi355x_groth16_prover* prover,
+                                                         uint32_t* out4);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove(tachyon_mi355x_groth16_prover* prover, const void* full,
+                                                   size_t count, const void* r, const void* s, void* out_a,
+                                                   void* out_b, void* out_c);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full,
+                                                         size_t count, void* out_h);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_last_timings(const tachyon_mi355x_groth16_prover* prover,
+                                                          float* out8);
+/* zkey curve (0 bn254, 1 bls12_381) without building a prover. */
+TACHYON_C_EXPORT int tachyon_mi355x_zkey_curve(const uint8_t* zkey, size_t len);
+/* wtns v2 -> Montgomery field elements of the curve's scalar field
+ * (wtns.h:99-117).  Writes min(count, cap) elements to out (may be NULL);
+ * returns the witness count. */
+TACHYON_C_EXPORT size_t tachyon_mi355x_wtns_parse(int curve, const uint8_t* wtns, size_t len, void* out,
+                                                  size_t cap);
+
 /* delete a Jacobian returned by an *_msm / *_msm_gpu entry point (for callers
  * that cannot use C++ delete, e.g. ctypes). */
 TACHYON_C_EXPORT void tachyon_mi355x_jacobian_destroy(int curve, void* jacobian);

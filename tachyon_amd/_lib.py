@@ -106,6 +106,15 @@ SIGNATURES = [
     ("tachyon_mi355x_gen_bases", None, [i32, u64, sz, sz, vp, vp]),
     ("tachyon_mi355x_field_op", None, [i32, i32, vp, vp, vp, sz]),
     ("tachyon_mi355x_ec_op", None, [i32, i32, vp, vp, vp, sz]),
+    ("tachyon_mi355x_groth16_prover_create", vp, [vp, sz]),
+    ("tachyon_mi355x_groth16_prover_destroy", None, [vp]),
+    ("tachyon_mi355x_groth16_prover_info", None, [vp, ctypes.POINTER(ctypes.c_uint32)]),
+    ("tachyon_mi355x_groth16_prove", None, [vp, vp, sz, vp, vp, vp, vp, vp]),
+    ("tachyon_mi355x_groth16_witness_map", None, [vp, vp, sz, vp]),
+    ("tachyon_mi355x_groth16_set_profile", None, [vp, i32]),
+    ("tachyon_mi355x_groth16_last_timings", None, [vp, fp]),
+    ("tachyon_mi355x_zkey_curve", i32, [vp, sz]),
+    ("tachyon_mi355x_wtns_parse", sz, [i32, vp, sz, vp, sz]),
     ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
     ("tachyon_mi355x_version", ctypes.c_char_p, []),
     ("tachyon_mi355x_device_count", i32, []),

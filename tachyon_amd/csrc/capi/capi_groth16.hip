@@ -1,0 +1,145 @@
+// C-ABI of the Groth16 prover (include/tachyon_mi355x.h, "Groth16 prover").
+// Reference driver restated: vendors/circom/prover_main.cc:82-160 (parse zkey
+// and wtns, build the domain, WitnessMapFromMatrices, CreateProofWithAssignment
+// (NoZK)); errors abort like the reference's CHECKs.
+#include "../../../include/tachyon_mi355x.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <vector>
+
+#include "../groth16/groth16.h"
+
+using namespace tachyon_amd;
+
+namespace {
+
+[[noreturn]] void die(const char* fn, const char* what) {
+  fprintf(stderr, "[tachyon_mi355x] %s failed: %s\n", fn, what);
+  fflush(stderr);
+  abort();
+}
+
+#define GUARD_BEGIN try {
+#define GUARD_END                                                \
+  }                                                              \
+  catch (const std::exception& e) { die(__func__, e.what()); }   \
+  catch (...) { die(__func__, "unknown exception"); }
+
+using BnProver = groth16::Groth16Prover<Bn254G1, Bn254G2>;
+using BlsProver = groth16::Groth16Prover<Bls381G1, Bls381G2>;
+
+template <class P>
+void prove_into(P* p, const void* full, size_t count, const void* r, const void* s, void* a, void* b, void* c) {
+  using Fr = typename P::Fr;
+  auto proof = p->prove(static_cast<const Fr*>(full), count, static_cast<const Fr*>(r), static_cast<const Fr*>(s));
+  memcpy(a, &proof.a, sizeof(proof.a));
+  memcpy(b, &proof.b, sizeof(proof.b));
+  memcpy(c, &proof.c, sizeof(proof.c));
+}
+
+template <class P>
+void witness_map_into(P* p, const void* full, size_t count, void* out_h) {
+  using Fr = typename P::Fr;
+  const auto& k = p->key();
+  if (count != k.num_vars) throw std::runtime_error("assignment count != num_vars");
+  DeviceBuffer d_full, d_h;
+  Fr* df = static_cast<Fr*>(d_full.ensure(count * sizeof(Fr)));
+  Fr* dh = static_cast<Fr*>(d_h.ensure((size_t)k.domain_size * sizeof(Fr)));
+  TA_HIP(hipMemcpyAsync(df, full, count * sizeof(Fr), hipMemcpyDefault, p->stream()));
+  p->witness_map(df, dh);
+  TA_HIP(hipMemcpyAsync(out_h, dh, (size_t)k.domain_size * sizeof(Fr), hipMemcpyDeviceToHost, p->stream()));
+  TA_HIP(hipStreamSynchronize(p->stream()));
+}
+
+}  // namespace
+
+struct tachyon_mi355x_groth16_prover {
+  circom::CurveId curve;
+  std::unique_ptr<BnProver> bn;
+  std::unique_ptr<BlsProver> bls;
+};
+
+#define PROVER_DISPATCH(p, ...)                         \
+  do {                                                  \
+    if ((p)->curve == circom::CurveId::kBn254) {        \
+      auto* impl = (p)->bn.get();                       \
+      __VA_ARGS__;                                      \
+    } else {                                            \
+      auto* impl = (p)->bls.get();                      \
+      __VA_ARGS__;                                      \
+    }                                                   \
+  } while (0)
+
+extern "C" {
+
+int tachyon_mi355x_zkey_curve(const uint8_t* zkey, size_t len) {
+  GUARD_BEGIN return (int)circom::zkey_curve(zkey, len); GUARD_END
+}
+
+tachyon_mi355x_groth16_prover* tachyon_mi355x_groth16_prover_create(const uint8_t* zkey, size_t len) {
+  GUARD_BEGIN
+  auto* p = new tachyon_mi355x_groth16_prover();
+  p->curve = circom::zkey_curve(zkey, len);
+  if (p->curve == circom::CurveId::kBn254)
+    p->bn = std::make_unique<BnProver>(circom::parse_zkey<Bn254G1, Bn254G2>(zkey, len));
+  else
+    p->bls = std::make_unique<BlsProver>(circom::parse_zkey<Bls381G1, Bls381G2>(zkey, len));
+  return p;
+  GUARD_END
+}
+
+void tachyon_mi355x_groth16_prover_destroy(tachyon_mi355x_groth16_prover* prover) { delete prover; }
+
+void tachyon_mi355x_groth16_prover_info(const tachyon_mi355x_groth16_prover* prover, uint32_t* out4) {
+  GUARD_BEGIN
+  PROVER_DISPATCH(prover, {
+    const auto& k = impl->key();
+    out4[0] = (uint32_t)prover->curve;
+    out4[1] = k.num_vars;
+    out4[2] = k.num_public;
+    out4[3] = k.domain_size;
+  });
+  GUARD_END
+}
+
+void tachyon_mi355x_groth16_prove(tachyon_mi355x_groth16_prover* prover, const void* full, size_t count,
+                                  const void* r, const void* s, void* out_a, void* out_b, void* out_c) {
+  GUARD_BEGIN PROVER_DISPATCH(prover, prove_into(impl, full, count, r, s, out_a, out_b, out_c)); GUARD_END
+}
+
+void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full, size_t count,
+                                        void* out_h) {
+  GUARD_BEGIN PROVER_DISPATCH(prover, witness_map_into(impl, full, count, out_h)); GUARD_END
+}
+
+void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on) {
+  GUARD_BEGIN PROVER_DISPATCH(prover, impl->set_profile(on != 0)); GUARD_END
+}
+
+void tachyon_mi355x_groth16_last_timings(const tachyon_mi355x_groth16_prover* prover, float* out8) {
+  GUARD_BEGIN
+  PROVER_DISPATCH(prover, {
+    const auto& t = impl->timings();
+    const float v[8] = {t.upload, t.qap, t.msm_a, t.msm_b2, t.msm_b1, t.msm_l, t.msm_h, t.total};
+    memcpy(out8, v, sizeof(v));
+  });
+  GUARD_END
+}
+
+size_t tachyon_mi355x_wtns_parse(int curve, const uint8_t* wtns, size_t len, void* out, size_t cap) {
+  GUARD_BEGIN
+  auto emit = [&](const auto& v) {
+    if (out) memcpy(out, v.data(), std::min(cap, v.size()) * sizeof(v[0]));
+    return v.size();
+  };
+  if (curve == 0) return emit(circom::parse_wtns<Bn254Fr>(wtns, len));
+  if (curve == 1) return emit(circom::parse_wtns<Bls381Fr>(wtns, len));
+  throw std::runtime_error("curve must be 0 (bn254) or 1 (bls12_381)");
+  GUARD_END
+}
+
+}  // extern "C"

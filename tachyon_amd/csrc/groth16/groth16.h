@@ -1,0 +1,91 @@
+// Groth16 prover on MI355X: the circom witness map (QAP) and the five MSMs of
+// CreateProofWithAssignment on the GPU, behind one host object per proving key.
+//
+// Reference path restated:
+//   vendors/circom/prover_main.cc:82-160 (CreateProof: zkey -> proving key,
+//     wtns -> full assignments, WitnessMapFromMatrices, NoZK / ZK proof)
+//   vendors/circom/circomlib/circuit/quadratic_arithmetic_program.h:24-113
+//     (a, b from the A/B coefficients, c = a * b, IFFT x3, DistributePowers by
+//     the 2n-th root of unity, FFT x3, h = a * b - c on the coset)
+//   tachyon/zk/r1cs/groth16/prove.h:33-165 (CalculateCoeff and
+//     CreateProofWithAssignment: A, B in G2, B in G1 when r != 0, C)
+//   vendors/circom/circomlib/zkey/proving_key.h:42-52 (ToNativeProvingKey:
+//     l_g1_query = points C1, h_g1_query = points H1)
+//
+// Device residency: the proving key's points and the coefficient matrices
+// (CSR by constraint) are uploaded once in the constructor -- the analogue of
+// the device-resident bases the reference keeps for KZG (kzg.h:90-114); a
+// proof uploads only the m witness values.  The QAP is three kernels plus
+// six batched NTT launches; every MSM takes device pointers (no copies).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <vector>
+
+#include "../common/hip_util.h"
+#include "../msm/msm.h"
+#include "../ntt/ntt.h"
+#include "circom_io.h"
+
+namespace tachyon_amd::groth16 {
+
+template <class G1, class G2>
+struct Proof {
+  Affine<typename G1::F> a;
+  Affine<typename G2::F> b;
+  Affine<typename G1::F> c;
+};
+
+// Per-phase device timings of the last prove (ms), when profiling is on.
+struct ProveTimings {
+  float upload = 0, qap = 0, msm_a = 0, msm_b2 = 0, msm_b1 = 0, msm_l = 0, msm_h = 0, total = 0;
+};
+
+template <class G1, class G2>
+class Groth16Prover {
+ public:
+  using Fr = typename G1::Fr;
+  using F1 = typename G1::F;
+  using F2 = typename G2::F;
+  using Key = circom::ZKey<G1, G2>;
+
+  explicit Groth16Prover(const Key& key, hipStream_t stream = nullptr);
+  ~Groth16Prover();
+  Groth16Prover(const Groth16Prover&) = delete;
+  Groth16Prover& operator=(const Groth16Prover&) = delete;
+
+  // full: num_vars Montgomery-form assignments (full[0] = 1), host or device.
+  // r, s: the blinding scalars (Montgomery); null = zero (the NoZK proof,
+  // prove.h:178-186).  Returns canonical affine points.
+  Proof<G1, G2> prove(const Fr* full, size_t count, const Fr* r, const Fr* s);
+
+  // The witness map alone: h evaluations on the coset (domain_size values,
+  // canonical Montgomery) written to `d_h` (device) -- for parity tests.
+  void witness_map(const Fr* d_full, Fr* d_h);
+
+  const Key& key() const { return key_; }
+  void set_profile(bool on) { profile_ = on; }
+  const ProveTimings& timings() const { return timings_; }
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  Key key_;  // host copy: verifying-key points and the query heads used on the host
+  hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
+  bool profile_ = false;
+  size_t n_ = 0;  // domain size
+  std::unique_ptr<ntt::NttDomain<Fr>> dom_, coset_;
+  std::unique_ptr<msm::MsmGpu<G1>> msm1_;
+  std::unique_ptr<msm::MsmGpu<G2>> msm2_;
+  DeviceBuffer a1_, b1_, c1_, h1_, b2_;          // query points
+  DeviceBuffer row_a_, row_b_, col_, val_;       // CSR of the A and B matrices
+  DeviceBuffer full_, abc_;                      // witness, 3 x n work vectors
+  ProveTimings timings_;
+  hipEvent_t ev_[4] = {};
+};
+
+extern template class Groth16Prover<Bn254G1, Bn254G2>;
+extern template class Groth16Prover<Bls381G1, Bls381G2>;
+
+}  // namespace tachyon_amd::groth16

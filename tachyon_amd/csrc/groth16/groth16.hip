@@ -1,0 +1,378 @@
+// Groth16 prover on MI355X: circom zkey/wtns readers, the witness-map
+// kernels and the proof assembly.  See groth16.h for the reference mapping.
+#include "groth16.h"
+
+#include <algorithm>
+#include <chrono>
+
+namespace tachyon_amd {
+namespace circom {
+
+namespace {
+
+void check_magic(ByteReader& rd, const char* magic, uint32_t want_version, const char* what) {
+  const uint8_t* m = rd.ptr(4);
+  if (memcmp(m, magic, 4) != 0) throw std::runtime_error(std::string("circom: not a ") + what + " file (bad magic)");
+  uint32_t version = rd.read<uint32_t>();
+  if (version != want_version)
+    throw std::runtime_error(std::string("circom: unsupported ") + what + " version " + std::to_string(version));
+}
+
+const std::pair<size_t, size_t>& section(const std::map<uint32_t, std::pair<size_t, size_t>>& secs, uint32_t id) {
+  auto it = secs.find(id);
+  if (it == secs.end()) throw std::runtime_error("circom: missing section " + std::to_string(id));
+  return it->second;
+}
+
+template <class T>
+void read_array(ByteReader& rd, std::vector<T>* out, size_t count) {
+  out->resize(count);
+  if (count) rd.take(out->data(), count * sizeof(T));
+}
+
+template <class F>
+struct BaseCfgOf {
+  using type = typename F::Config;
+};
+template <class B>
+struct BaseCfgOf<Fp2<B>> {
+  using type = typename B::Config;
+};
+
+}  // namespace
+
+CurveId zkey_curve(const uint8_t* data, size_t len) {
+  ByteReader rd(data, len);
+  check_magic(rd, "zkey", 1, "zkey");
+  auto secs = read_sections(rd);
+  auto [off, size] = section(secs, 2);
+  ByteReader g(data + off, size);
+  uint32_t n8q = g.read<uint32_t>();
+  const uint8_t* q = g.ptr(n8q);
+  if (modulus_matches<consts::bn254_fq>(q, n8q)) return CurveId::kBn254;
+  if (modulus_matches<consts::bls12_381_fq>(q, n8q)) return CurveId::kBls12_381;
+  throw std::runtime_error("circom: zkey base field is neither BN254 nor BLS12-381");
+}
+
+template <class G1, class G2>
+ZKey<G1, G2> parse_zkey(const uint8_t* data, size_t len) {
+  using Z = ZKey<G1, G2>;
+  using Fr = typename Z::Fr;
+  Z z;
+  ByteReader rd(data, len);
+  check_magic(rd, "zkey", 1, "zkey");
+  auto secs = read_sections(rd);
+  {
+    auto [off, size] = section(secs, 1);  // header: prover type 1 = Groth16
+    ByteReader h(data + off, size);
+    if (h.read<uint32_t>() != 1) throw std::runtime_error("circom: zkey prover type is not Groth16");
+  }
+  {
+    auto [off, size] = section(secs, 2);
+    ByteReader g(data + off, size);
+    uint32_t n8q = g.read<uint32_t>();
+    if (!modulus_matches<typename BaseCfgOf<typename G1::F>::type>(g.ptr(n8q), n8q))
+      throw std::runtime_error("circom: zkey base field does not match the curve");
+    uint32_t n8r = g.read<uint32_t>();
+    if (!modulus_matches<typename Fr::Config>(g.ptr(n8r), n8r))
+      throw std::runtime_error("circom: zkey scalar field does not match the curve");
+    z.num_vars = g.read<uint32_t>();
+    z.num_public = g.read<uint32_t>();
+    z.domain_size = g.read<uint32_t>();
+    if (z.num_vars < z.num_public + 1) throw std::runtime_error("circom: zkey has fewer variables than inputs");
+    if (z.domain_size == 0 || (z.domain_size & (z.domain_size - 1)))
+      throw std::runtime_error("circom: zkey domain size is not a power of two");
+    z.alpha_g1 = g.read<typename Z::A1>();
+    z.beta_g1 = g.read<typename Z::A1>();
+    z.beta_g2 = g.read<typename Z::A2>();
+    z.gamma_g2 = g.read<typename Z::A2>();
+    z.delta_g1 = g.read<typename Z::A1>();
+    z.delta_g2 = g.read<typename Z::A2>();
+  }
+  auto points = [&](uint32_t id, auto* out, size_t count) {
+    auto [off, size] = section(secs, id);
+    ByteReader p(data + off, size);
+    read_array(p, out, count);
+  };
+  points(3, &z.ic, z.num_public + 1);
+  {
+    auto [off, size] = section(secs, 4);
+    ByteReader c(data + off, size);
+    uint32_t count = c.read<uint32_t>();
+    z.coefficients.resize(count);
+    for (uint32_t i = 0; i < count; ++i) {
+      auto& e = z.coefficients[i];
+      e.matrix = c.read<uint32_t>();
+      e.constraint = c.read<uint32_t>();
+      e.signal = c.read<uint32_t>();
+      Fr raw;
+      c.take(&raw, sizeof(Fr));
+      // zkey.h:219-220: value = F::FromMontgomery(value.ToBigInt()), i.e. the
+      // stored word times R^-1 becomes the Montgomery representation
+      e.value = raw.from_mont();
+    }
+  }
+  points(5, &z.a1, z.num_vars);
+  points(6, &z.b1, z.num_vars);
+  points(7, &z.b2, z.num_vars);
+  points(8, &z.c1, z.num_witness());
+  points(9, &z.h1, z.domain_size);
+  return z;
+}
+
+template <class Fr>
+std::vector<Fr> parse_wtns(const uint8_t* data, size_t len) {
+  ByteReader rd(data, len);
+  check_magic(rd, "wtns", 2, "wtns");
+  auto secs = read_sections(rd);
+  uint32_t count;
+  {
+    auto [off, size] = section(secs, 1);
+    ByteReader h(data + off, size);
+    uint32_t n8 = h.read<uint32_t>();
+    if (!modulus_matches<typename Fr::Config>(h.ptr(n8), n8))
+      throw std::runtime_error("circom: wtns field does not match the curve's scalar field");
+    count = h.read<uint32_t>();
+  }
+  auto [off, size] = section(secs, 2);
+  ByteReader d(data + off, size);
+  std::vector<Fr> out(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    Fr raw;
+    d.take(&raw, sizeof(Fr));
+    out[i] = raw.to_mont();  // wtns.h:116: F(witnesses[i].value()) -- canonical in, Montgomery out
+  }
+  return out;
+}
+
+template ZKey<Bn254G1, Bn254G2> parse_zkey<Bn254G1, Bn254G2>(const uint8_t*, size_t);
+template ZKey<Bls381G1, Bls381G2> parse_zkey<Bls381G1, Bls381G2>(const uint8_t*, size_t);
+template std::vector<Bn254Fr> parse_wtns<Bn254Fr>(const uint8_t*, size_t);
+template std::vector<Bls381Fr> parse_wtns<Bls381Fr>(const uint8_t*, size_t);
+
+}  // namespace circom
+
+namespace groth16 {
+
+namespace {
+
+constexpr unsigned kBlock = 256;
+
+// a_i = sum_A val * w[signal], b_i likewise, c_i = a_i * b_i
+// (quadratic_arithmetic_program.h:38-72; the OpenMP-locked scatter becomes a
+// gather over the constraint's CSR row -- field addition is exact, so the
+// order of the terms does not change the values)
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void qap_abc_kernel(const uint32_t* __restrict__ row_a,
+                                                         const uint32_t* __restrict__ row_b,
+                                                         const uint32_t* __restrict__ col,
+                                                         const Fr* __restrict__ val, const Fr* __restrict__ w,
+                                                         uint32_t n, Fr* __restrict__ abc) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Fr a = Fr::zero(), b = Fr::zero();
+  for (uint32_t k = row_a[i], e = row_a[i + 1]; k < e; ++k) a = a + val[k] * w[col[k]];
+  for (uint32_t k = row_b[i], e = row_b[i + 1]; k < e; ++k) b = b + val[k] * w[col[k]];
+  abc[i] = a.canonical();
+  abc[(size_t)n + i] = b.canonical();
+  abc[2 * (size_t)n + i] = (a * b).canonical();
+}
+
+// h_i = a_i * b_i - c_i on the coset (quadratic_arithmetic_program.h:102-108), in place over a
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void qap_h_kernel(Fr* __restrict__ abc, uint32_t n) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  abc[i] = (abc[i] * abc[(size_t)n + i] - abc[2 * (size_t)n + i]).canonical();
+}
+
+// k * P on the host, k a Montgomery-form scalar (double-and-add, high bit first)
+template <class F, class Fr>
+XYZZ<F> mul_scalar(const XYZZ<F>& P, const Fr& k) {
+  Fr c = k.from_mont().canonical();
+  XYZZ<F> r = XYZZ<F>::zero();
+  for (int i = Fr::N * 32 - 1; i >= 0; --i) {
+    r = r.dbl();
+    if ((c.v[i / 32] >> (i % 32)) & 1) r = r + P;
+  }
+  return r;
+}
+
+template <class T>
+T* upload(DeviceBuffer& buf, const std::vector<T>& v, size_t from = 0) {
+  size_t count = v.size() > from ? v.size() - from : 0;
+  T* d = static_cast<T*>(buf.ensure(std::max<size_t>(1, count) * sizeof(T)));
+  if (count) TA_HIP(hipMemcpy(d, v.data() + from, count * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+using Clock = std::chrono::steady_clock;
+inline float ms_since(Clock::time_point t0) {
+  return std::chrono::duration<float, std::milli>(Clock::now() - t0).count();
+}
+
+}  // namespace
+
+template <class G1, class G2>
+Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(key), stream_(stream) {
+  require_gpu();
+  if (!stream_) {
+    TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    own_stream_ = true;
+  }
+  n_ = key_.domain_size;
+  uint32_t log_n = 0;
+  while ((size_t(1) << log_n) < n_) ++log_n;
+  dom_ = std::make_unique<ntt::NttDomain<Fr>>(n_, stream_);
+  coset_ = std::make_unique<ntt::NttDomain<Fr>>(n_, stream_);
+  // DistributePowers(poly, w_2n) then FFT == the FFT on the coset w_2n * <w_n>
+  coset_->set_offset(ntt::root_of_unity<Fr>(log_n + 1));
+  msm1_ = std::make_unique<msm::MsmGpu<G1>>(stream_);
+  msm2_ = std::make_unique<msm::MsmGpu<G2>>(stream_);
+
+  upload(a1_, key_.a1);
+  upload(b1_, key_.b1);
+  upload(b2_, key_.b2);
+  upload(c1_, key_.c1);
+  upload(h1_, key_.h1);
+
+  // CSR by constraint: A rows first, then B rows, in one col/val array
+  const size_t n = n_;
+  std::vector<uint32_t> cnt(2 * n + 1, 0);
+  for (const auto& e : key_.coefficients) {
+    if (e.constraint >= n) throw std::runtime_error("circom: coefficient constraint index outside the domain");
+    if (e.signal >= key_.num_vars) throw std::runtime_error("circom: coefficient signal index out of range");
+    cnt[(e.matrix ? n : 0) + e.constraint + 1]++;
+  }
+  for (size_t i = 1; i <= 2 * n; ++i) cnt[i] += cnt[i - 1];
+  std::vector<uint32_t> col(key_.coefficients.size());
+  std::vector<Fr> val(key_.coefficients.size());
+  std::vector<uint32_t> fill(cnt.begin(), cnt.end() - 1);
+  for (const auto& e : key_.coefficients) {
+    uint32_t at = fill[(e.matrix ? n : 0) + e.constraint]++;
+    col[at] = e.signal;
+    val[at] = e.value;
+  }
+  std::vector<uint32_t> row_a(cnt.begin(), cnt.begin() + n + 1);
+  std::vector<uint32_t> row_b(cnt.begin() + n, cnt.end());
+  upload(row_a_, row_a);
+  upload(row_b_, row_b);
+  upload(col_, col);
+  upload(val_, val);
+  abc_.ensure(3 * n * sizeof(Fr));
+  full_.ensure(std::max<size_t>(1, key_.num_vars) * sizeof(Fr));
+  // the big host arrays are on the device now; keep the counts and the
+  // query heads that the proof assembly reads on the host
+  auto head = [](auto& v) { v.resize(std::min<size_t>(1, v.size())); v.shrink_to_fit(); };
+  head(key_.a1);
+  head(key_.b1);
+  head(key_.b2);
+  key_.c1.clear();
+  key_.c1.shrink_to_fit();
+  key_.h1.clear();
+  key_.h1.shrink_to_fit();
+  key_.coefficients.clear();
+  key_.coefficients.shrink_to_fit();
+}
+
+template <class G1, class G2>
+Groth16Prover<G1, G2>::~Groth16Prover() {
+  msm1_.reset();
+  msm2_.reset();
+  dom_.reset();
+  coset_.reset();
+  if (own_stream_) (void)hipStreamDestroy(stream_);
+}
+
+template <class G1, class G2>
+void Groth16Prover<G1, G2>::witness_map(const Fr* d_full, Fr* d_h) {
+  const uint32_t n = (uint32_t)n_;
+  Fr* abc = abc_.as<Fr>();
+  const unsigned grid = ceil_div(n, kBlock);
+  hipLaunchKernelGGL(qap_abc_kernel<Fr>, dim3(grid), dim3(kBlock), 0, stream_, row_a_.as<uint32_t>(),
+                     row_b_.as<uint32_t>(), col_.as<uint32_t>(), val_.as<Fr>(), d_full, n, abc);
+  TA_HIP(hipGetLastError());
+  dom_->inverse_device(abc, 3);    // a, b, c evaluations -> coefficients
+  coset_->forward_device(abc, 3);  // -> evaluations on the coset w_2n <w_n>
+  hipLaunchKernelGGL(qap_h_kernel<Fr>, dim3(grid), dim3(kBlock), 0, stream_, abc, n);
+  TA_HIP(hipGetLastError());
+  if (d_h != abc) TA_HIP(hipMemcpyAsync(d_h, abc, n_ * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+}
+
+template <class G1, class G2>
+Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const Fr* r_ptr, const Fr* s_ptr) {
+  using P1 = XYZZ<F1>;
+  using P2 = XYZZ<F2>;
+  const size_t m = key_.num_vars;
+  if (count != m)
+    throw std::runtime_error("tachyon_mi355x: Groth16 assignment count " + std::to_string(count) +
+                             " != num_vars " + std::to_string(m));
+  const Fr r = r_ptr ? *r_ptr : Fr::zero();
+  const Fr s = s_ptr ? *s_ptr : Fr::zero();
+  auto t0 = Clock::now();
+  const Fr* d_full = full;
+  if (!is_device_pointer(full)) {
+    d_full = full_.as<Fr>();
+    TA_HIP(hipMemcpyAsync(const_cast<Fr*>(d_full), full, m * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+  }
+  if (profile_) {
+    TA_HIP(hipStreamSynchronize(stream_));
+    timings_.upload = ms_since(t0);
+  }
+  auto t1 = Clock::now();
+  Fr* d_h = abc_.as<Fr>();
+  witness_map(d_full, d_h);
+  if (profile_) {
+    TA_HIP(hipStreamSynchronize(stream_));
+    timings_.qap = ms_since(t1);
+  }
+
+  // MSMs over device-resident bases and scalars (prove.h:95-146)
+  const Affine<F1>* a1 = a1_.as<Affine<F1>>();
+  const Affine<F1>* b1 = b1_.as<Affine<F1>>();
+  const Affine<F2>* b2 = b2_.as<Affine<F2>>();
+  auto t2 = Clock::now();
+  P1 acc_a = m > 1 ? msm1_->run(a1 + 1, d_full + 1, m - 1) : P1::zero();
+  timings_.msm_a = ms_since(t2);
+  t2 = Clock::now();
+  P2 acc_b2 = m > 1 ? msm2_->run(b2 + 1, d_full + 1, m - 1) : P2::zero();
+  timings_.msm_b2 = ms_since(t2);
+  t2 = Clock::now();
+  P1 acc_b1 = (!r.is_zero() && m > 1) ? msm1_->run(b1 + 1, d_full + 1, m - 1) : P1::zero();
+  timings_.msm_b1 = ms_since(t2);
+  t2 = Clock::now();
+  const size_t nw = key_.num_witness();
+  P1 acc_l = nw ? msm1_->run(c1_.as<Affine<F1>>(), d_full + key_.num_instance(), nw) : P1::zero();
+  timings_.msm_l = ms_since(t2);
+  t2 = Clock::now();
+  // h_coefficients.size() == h_g1_query.size() == domain size: the else branch of prove.h:103-112
+  P1 acc_h = msm1_->run(h1_.as<Affine<F1>>(), d_h, n_);
+  timings_.msm_h = ms_since(t2);
+
+  // assembly on the host (a handful of point operations)
+  auto aff1 = [](const Affine<F1>& a) { return P1::from_affine(a); };
+  auto aff2 = [](const Affine<F2>& a) { return P2::from_affine(a); };
+  const P1 delta1 = aff1(key_.delta_g1);
+  // [A]_1 = alpha + a_0 + sum x_i a_i + r delta   (CalculateCoeff, prove.h:33-49)
+  const P1 r_delta1 = mul_scalar(delta1, r);
+  const P1 A = r_delta1 + aff1(key_.a1[0]) + acc_a + aff1(key_.alpha_g1);
+  // [B]_2 = beta + b_0 + sum x_i b_i + s delta
+  const P2 B2 = mul_scalar(aff2(key_.delta_g2), s) + aff2(key_.b2[0]) + acc_b2 + aff2(key_.beta_g2);
+  // [C]_1 = s A + r B_1 - s r delta + sum_witness l_i + h
+  P1 C = mul_scalar(A, s);
+  if (!r.is_zero()) {
+    const P1 B1 = mul_scalar(delta1, s) + aff1(key_.b1[0]) + acc_b1 + aff1(key_.beta_g1);
+    C = C + mul_scalar(B1, r);
+    C = C + mul_scalar(r_delta1, s).neg();
+  }
+  C = C + acc_l;
+  C = C + acc_h;
+  timings_.total = ms_since(t0);
+  return Proof<G1, G2>{A.to_affine(), B2.to_affine(), C.to_affine()};
+}
+
+template class Groth16Prover<Bn254G1, Bn254G2>;
+template class Groth16Prover<Bls381G1, Bls381G2>;
+
+}  // namespace groth16
+}  // namespace tachyon_amd

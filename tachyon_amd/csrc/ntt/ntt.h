@@ -94,6 +94,14 @@ class NttDomain {
 extern template class NttDomain<Bn254Fr>;
 extern template class NttDomain<Bls381Fr>;
 
+// w_(2^log_n), Montgomery form: the two-adic root squared down
+// (PrimeFieldBase::GetRootOfUnity, prime_field_base.h:90-130).
+template <class Fr>
+Fr root_of_unity(uint32_t log_n);
+// n as a field element (Montgomery form)
+template <class Fr>
+Fr field_from_u64(uint64_t v);
+
 }  // namespace tachyon_amd::ntt
 
 namespace tachyon_amd::ntt {

@@ -485,8 +485,25 @@ void Ntt4Step<Fr>::inverse_stage2(const Fr* recv, Fr* out) {
   dom_r_->inverse_device(out, size_t(1) << log_cg);
 }
 
+template <class Fr>
+Fr root_of_unity(uint32_t log_n) {
+  if (log_n > (uint32_t)Fr::Config::kTwoAdicity)
+    throw std::runtime_error("tachyon_mi355x: no root of unity of that order in the field");
+  Fr w = two_adic_root<Fr>();
+  for (uint32_t i = log_n; i < (uint32_t)Fr::Config::kTwoAdicity; ++i) w = w.sqr();
+  return w;
+}
+template <class Fr>
+Fr field_from_u64(uint64_t v) {
+  return fr_from_u64<Fr>(v);
+}
+
 template class NttDomain<Bn254Fr>;
 template class NttDomain<Bls381Fr>;
+template Bn254Fr root_of_unity<Bn254Fr>(uint32_t);
+template Bls381Fr root_of_unity<Bls381Fr>(uint32_t);
+template Bn254Fr field_from_u64<Bn254Fr>(uint64_t);
+template Bls381Fr field_from_u64<Bls381Fr>(uint64_t);
 template class Ntt4Step<Bn254Fr>;
 
 }  // namespace tachyon_amd::ntt

@@ -1,0 +1,104 @@
+"""Host mirror of the circom Groth16 prover over the C-ABI.
+
+Reference interfaces mirrored (names and argument meaning):
+  vendors/circom/prover_main.cc:82-160  CreateProof(zkey, wtns): ParseZKey,
+      ParseWtns, then per run WitnessMapFromMatrices + CreateProofWithAssignment(NoZK|ZK)
+  vendors/circom/circomlib/circuit/quadratic_arithmetic_program.h:24-113
+      QuadraticArithmeticProgram::WitnessMapFromMatrices -> `witness_map`
+  tachyon/zk/r1cs/groth16/prove.h:52-186
+      CreateProofWithAssignment(pk, r, s, ...) / ...NoZK / ...ZK -> `prove`
+All compute runs in libtachyon_mi355x.so on the GPU (the proving key is
+uploaded once per Groth16Prover); there is no CPU fallback.
+
+Field elements cross the boundary as Montgomery-form little-endian bytes (the
+reference's in-memory layout); proofs come back as affine point bytes
+(G1: 2 x Fq, G2: 2 x Fq2; identity = all zero bytes).
+"""
+import ctypes
+
+from ._lib import lib
+from .msm import _ptr
+
+CURVE_NAMES = {0: "bn254", 1: "bls12_381"}
+POINT_BYTES = {"bn254": (64, 128), "bls12_381": (96, 192)}
+
+
+def wtns_parse(data: bytes, curve: str = "bn254") -> bytes:
+    """wtns v2 -> Montgomery Fr bytes (wtns.h:99-117: canonical in, Montgomery out)."""
+    cid = {v: k for k, v in CURVE_NAMES.items()}[curve]
+    p, n, keep = _ptr(data)
+    count = lib().tachyon_mi355x_wtns_parse(cid, p, n, None, 0)
+    out = ctypes.create_string_buffer(max(1, count * 32))
+    lib().tachyon_mi355x_wtns_parse(cid, p, n, out, count)
+    return out.raw[:count * 32]
+
+
+def zkey_curve(data: bytes) -> str:
+    p, n, keep = _ptr(data)
+    return CURVE_NAMES[lib().tachyon_mi355x_zkey_curve(p, n)]
+
+
+class Groth16Prover:
+    """ParseZKey + GetProvingKey().ToNativeProvingKey(), resident on the GPU."""
+
+    def __init__(self, zkey: bytes):
+        p, n, keep = _ptr(zkey)
+        self._h = lib().tachyon_mi355x_groth16_prover_create(p, n)
+        if not self._h:
+            raise RuntimeError("failed to create the Groth16 prover")
+        info = (ctypes.c_uint32 * 4)()
+        lib().tachyon_mi355x_groth16_prover_info(self._h, info)
+        self.curve = CURVE_NAMES[info[0]]
+        self.num_vars, self.num_public, self.domain_size = info[1], info[2], info[3]
+        self.g1_bytes, self.g2_bytes = POINT_BYTES[self.curve]
+
+    @property
+    def num_instance_variables(self):  # ZKey::GetNumInstanceVariables
+        return self.num_public + 1
+
+    def close(self):
+        if self._h:
+            lib().tachyon_mi355x_groth16_prover_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def witness_map(self, full) -> bytes:
+        """WitnessMapFromMatrices: h evaluations on the coset (domain_size x 32 B)."""
+        p, n, keep = _ptr(full)
+        out = ctypes.create_string_buffer(self.domain_size * 32)
+        lib().tachyon_mi355x_groth16_witness_map(self._h, p, n // 32, out)
+        return out.raw
+
+    def prove(self, full, r: bytes = None, s: bytes = None):
+        """CreateProofWithAssignment(pk, r, s, h, instance, witness, full[1:]);
+        r = s = None is CreateProofWithAssignmentNoZK.  `full` may be host
+        bytes/numpy or a CUDA tensor.  Returns (A, B, C) affine bytes."""
+        p, n, keep = _ptr(full)
+        a = ctypes.create_string_buffer(self.g1_bytes)
+        b = ctypes.create_string_buffer(self.g2_bytes)
+        c = ctypes.create_string_buffer(self.g1_bytes)
+        rb = ctypes.create_string_buffer(r, 32) if r is not None else None
+        sb = ctypes.create_string_buffer(s, 32) if s is not None else None
+        lib().tachyon_mi355x_groth16_prove(self._h, p, n // 32, rb, sb, a, b, c)
+        return a.raw, b.raw, c.raw
+
+    def set_profile(self, on: bool):
+        lib().tachyon_mi355x_groth16_set_profile(self._h, 1 if on else 0)
+
+    def last_timings(self) -> dict:
+        out = (ctypes.c_float * 8)()
+        lib().tachyon_mi355x_groth16_last_timings(self._h, out)
+        return dict(zip(("upload", "qap", "msm_a", "msm_b2", "msm_b1", "msm_l", "msm_h", "total"), list(out)))
+
+
+def create_proof_with_assignment_no_zk(prover: Groth16Prover, full):
+    return prover.prove(full)
+
+
+def create_proof_with_assignment(prover: Groth16Prover, r: bytes, s: bytes, full):
+    return prover.prove(full, r, s)
