@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <exception>
+#include <thread>
 
 namespace tachyon_amd {
 namespace circom {
@@ -228,7 +230,7 @@ Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(
   // DistributePowers(poly, w_2n) then FFT == the FFT on the coset w_2n * <w_n>
   coset_->set_offset(ntt::root_of_unity<Fr>(log_n + 1));
   msm1_ = std::make_unique<msm::MsmGpu<G1>>(stream_);
-  msm2_ = std::make_unique<msm::MsmGpu<G2>>(stream_);
+  msm2_ = std::make_unique<msm::MsmGpu<G2>>(nullptr);  // own stream: runs beside the G1 MSMs
 
   upload(a1_, key_.a1);
   upload(b1_, key_.b1);
@@ -331,12 +333,29 @@ Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const F
   const Affine<F1>* a1 = a1_.as<Affine<F1>>();
   const Affine<F1>* b1 = b1_.as<Affine<F1>>();
   const Affine<F2>* b2 = b2_.as<Affine<F2>>();
+  // The G2 MSM (about 3x the work of a G1 one) runs on its own stream from a
+  // second host thread while the G1 MSMs run here; each MSM is synchronous on
+  // its host thread (its read-back of the chain lengths).  The witness and h
+  // are ready once stream_ drains.
+  TA_HIP(hipStreamSynchronize(stream_));
+  P2 acc_b2 = P2::zero();
+  std::exception_ptr g2_error;
+  std::thread g2_thread([&] {
+    try {
+      auto tb = Clock::now();
+      if (m > 1) acc_b2 = msm2_->run(b2 + 1, d_full + 1, m - 1);
+      timings_.msm_b2 = ms_since(tb);
+    } catch (...) {
+      g2_error = std::current_exception();
+    }
+  });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() { if (t.joinable()) t.join(); }
+  } joiner{g2_thread};
   auto t2 = Clock::now();
   P1 acc_a = m > 1 ? msm1_->run(a1 + 1, d_full + 1, m - 1) : P1::zero();
   timings_.msm_a = ms_since(t2);
-  t2 = Clock::now();
-  P2 acc_b2 = m > 1 ? msm2_->run(b2 + 1, d_full + 1, m - 1) : P2::zero();
-  timings_.msm_b2 = ms_since(t2);
   t2 = Clock::now();
   P1 acc_b1 = (!r.is_zero() && m > 1) ? msm1_->run(b1 + 1, d_full + 1, m - 1) : P1::zero();
   timings_.msm_b1 = ms_since(t2);
@@ -348,6 +367,8 @@ Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const F
   // h_coefficients.size() == h_g1_query.size() == domain size: the else branch of prove.h:103-112
   P1 acc_h = msm1_->run(h1_.as<Affine<F1>>(), d_h, n_);
   timings_.msm_h = ms_since(t2);
+  g2_thread.join();
+  if (g2_error) std::rethrow_exception(g2_error);
 
   // assembly on the host (a handful of point operations)
   auto aff1 = [](const Affine<F1>& a) { return P1::from_affine(a); };

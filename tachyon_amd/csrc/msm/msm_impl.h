@@ -341,7 +341,6 @@ MsmGpu<Curve>::MsmGpu(hipStream_t stream) : stream_(stream) {
     TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     own_stream_ = true;
   }
-  TA_HIP(hipStreamCreateWithFlags(&sort_stream_, hipStreamNonBlocking));
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
   TA_HIP(hipHostMalloc(reinterpret_cast<void**>(&h_max_), 2 * sizeof(uint32_t), hipHostMallocDefault));
 }
@@ -414,6 +413,11 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   }
   if (T >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM too large for the chunking");
   ensure_group_events(ngroups);
+  // the sort runs on its own stream only when the windows are pipelined
+  // (created on first use: every extra stream may take one of the process's
+  // few hardware queues)
+  if (ngroups > 1 && !sort_stream_) TA_HIP(hipStreamCreateWithFlags(&sort_stream_, hipStreamNonBlocking));
+  hipStream_t sort_stream = ngroups > 1 ? sort_stream_ : stream_;
 
   uint32_t* keys = static_cast<uint32_t*>(keys_.ensure(entries * 4));
   uint32_t* vals = static_cast<uint32_t*>(vals_.ensure(entries * 4));
@@ -443,7 +447,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * sizeof(Point), stream_));
   TA_HIP(hipMemsetAsync(dscal, 0, 2 * sizeof(uint32_t), stream_));
   TA_HIP(hipEventRecord(ev_[2], stream_));  // recode done (also the profile mark)
-  TA_HIP(hipStreamWaitEvent(sort_stream_, ev_[2], 0));
+  if (sort_stream != stream_) TA_HIP(hipStreamWaitEvent(sort_stream, ev_[2], 0));
 
   // ---- per group: radix sort of its (window, bucket, point) entries, then accumulation ----
   unsigned wbits = 0;
@@ -451,7 +455,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   const unsigned key_bits = (G == 1) ? c : c + wbits;  // the window bits only matter within a multi-window group
   const size_t max_group_entries = (size_t)G * n;
   size_t sort_bytes = 0;
-  TA_HIP(sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, max_group_entries, key_bits, sort_stream_));
+  TA_HIP(sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, max_group_entries, key_bits, sort_stream));
   void* sort_tmp = sort_tmp_.ensure(sort_bytes);
   size_t tbase = 0;
   acc_launches_ = ngroups;
@@ -460,9 +464,11 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     const size_t e0 = (size_t)w0 * n, ecount = (size_t)(w1 - w0) * n;
     size_t bytes = sort_bytes;
     TA_HIP(sort_pairs(sort_tmp, bytes, keys + e0, keys2 + e0, vals + e0, vals2 + e0, ecount, key_bits,
-                      sort_stream_));
-    TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream_));
-    TA_HIP(hipStreamWaitEvent(stream_, gev_sorted_[g], 0));
+                      sort_stream));
+    if (sort_stream != stream_) {
+      TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream));
+      TA_HIP(hipStreamWaitEvent(stream_, gev_sorted_[g], 0));
+    }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
     hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2, c,
@@ -471,7 +477,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if (profile_) TA_HIP(hipEventRecord(gev_acc1_[g], stream_));
     tbase += Tg;
   }
-  if (profile_) TA_HIP(hipEventRecord(ev_[3], sort_stream_));  // last sort done
+  if (profile_) TA_HIP(hipEventRecord(ev_[3], sort_stream));  // last sort done
   if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));        // last accumulation done
 
   // ---- join buckets that cross thread boundaries ----

@@ -93,3 +93,32 @@ def test_device_resident_witness():
     d = torch.from_numpy(np.frombuffer(fb, dtype=np.uint8).copy()).cuda()
     assert list(prover.prove(d)) == list(OG.prove(zk, full))
     prover.close()
+
+
+def test_circom_prover_cli(tmp_path):
+    """bin/circom_prover (prover_main.cc on the C-ABI): snarkjs-style proof.json
+    and public.json; --no_zk reproduces the golden proof, the ZK proof verifies."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tachyon_amd", "bin",
+                       "circom_prover")
+    zk = CF.parse_zkey(open(os.path.join(GOLDEN, "multiplier_3.zkey"), "rb").read())
+    g = json.load(open(os.path.join(GOLDEN, "groth16_multiplier_3.json")))
+    G1, G2 = pyref.Curve("bn254_g1"), pyref.Curve("bn254_g2")
+    vk = {k: (G2 if k.endswith("g2") else G1).from_bytes(v) for k, v in zk["vk"].items()}
+    ic = [G1.from_bytes(b) for b in zk["ic"]]
+    for flags in (["--no_zk"], []):
+        proof_p, pub_p = tmp_path / "proof.json", tmp_path / "public.json"
+        cmd = [exe, "--zkey", os.path.join(GOLDEN, "multiplier_3.zkey"), "--wtns",
+               os.path.join(GOLDEN, "multiplier_3.wtns"), "--proof", str(proof_p), "--public", str(pub_p)] + flags
+        subprocess.run(cmd, check=True, timeout=120, capture_output=True)
+        proof = json.load(open(proof_p))
+        assert json.load(open(pub_p)) == ["60"]
+        assert proof["protocol"] == "groth16" and proof["curve"] == "bn128"
+        assert proof["pi_a"][2] == "1" and proof["pi_b"][2] == ["1", "0"]
+        A = tuple(int(x) for x in proof["pi_a"][:2])
+        B = tuple(tuple(int(x) for x in c) for c in proof["pi_b"][:2])
+        C = tuple(int(x) for x in proof["pi_c"][:2])
+        if flags:
+            want = g["cases"][0]["proof"]
+            assert G1.to_bytes(A).hex() == want[0] and G2.to_bytes(B).hex() == want[1] and G1.to_bytes(C).hex() == want[2]
+        assert BP.groth16_verify(vk, ic, [60], (A, B, C))
