@@ -281,7 +281,7 @@ def main():
     # ---- NTT 2^24: one GPU, or the four-step sharded transform (one RCCL all-to-all) ----
     if not args.no_ntt and world > 1:
         from tachyon_amd.ntt import FourStepNtt
-        plan = FourStepNtt(args.ntt_log_n, world, rank, torch.cuda.current_stream().cuda_stream)
+        plan = FourStepNtt(args.ntt_log_n, world, rank)  # its own stream; sharded_ntt orders on it
         m = plan.local_size
         x = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
         M.gen_scalars("bn254_fr", SEED + 1, m, x.data_ptr(), start=rank * m)

@@ -4,6 +4,7 @@
 #include "ntt.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace tachyon_amd::ntt {
@@ -35,7 +36,58 @@ __device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
 // same positions); the final pass (s0 + k == L) writes natural order through
 // the bit-reversal permutation, M bit-reversed-consecutive sets per workgroup
 // so every store row is M contiguous elements.
-template <class Fr>
+// R DIF stages (t .. t+R-1 of the pass) on groups of 2^R elements held in
+// registers.  Group g covers set m = g mod M and the positions
+// a0 + j q (j < 2^R, q = 2^(k-t-R)); stage t+u pairs j with j + 2^(R-1-u).
+// Twiddle of the butterfly whose low element has global index i at global
+// stage s: w_s^(i mod 2^(L-s-1)) (the reference's Radix2TwiddleCache row s).
+// kLast: the transform's last R stages (final pass, t + R == k).
+template <int R, bool kLast, class Fr, class IndexFn>
+__device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __restrict__ tw, const PassArgs<Fr>& a,
+                                           uint32_t t, IndexFn index) {
+  constexpr int E = 1 << R;
+  const uint32_t log_m = a.log_m, M = 1u << log_m;
+  const uint32_t n = 1u << a.L;
+  const uint32_t groups = (M << a.k) >> R;
+  const uint32_t qlog = a.k - t - R;
+  for (uint32_t g = threadIdx.x; g < groups; g += kBlock) {
+    const uint32_t m = g & (M - 1);
+    const uint32_t rr = g >> log_m;
+    const uint32_t off = rr & ((1u << qlog) - 1);
+    const uint32_t a0 = ((rr >> qlog) << (qlog + R)) + off;
+    Fr x[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) x[j] = lds[((a0 + ((uint32_t)j << qlog)) << log_m) + m];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint32_t st = a.s0 + t + u;
+      const uint32_t gap_mask = (1u << (a.L - st - 1)) - 1;
+      const Fr* tws = tw + (n - (n >> st));
+      const int half = E >> (u + 1);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        if (j & half) continue;
+        const Fr lo = x[j], hi = x[j + half];
+        // ButterflyFnInOut: lo = lo + hi; hi = (lo - hi) * w
+        x[j] = lo + hi;
+        if constexpr (kLast) {
+          // the transform's last R stages: the twiddle index is j mod 2^(R-1-u)
+          // (a0 and the set base are multiples of 2^R), known at compile time;
+          // index 0 is w = 1 -- the whole last stage and half the one before
+          const uint32_t idx = (uint32_t)j & ((1u << (R - 1 - u)) - 1);
+          x[j + half] = idx ? (lo - hi) * tws[idx] : (lo - hi);
+        } else {
+          const Fr w = tws[index(a0 + ((uint32_t)j << qlog), m) & gap_mask];
+          x[j + half] = (lo - hi) * w;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < E; ++j) lds[((a0 + ((uint32_t)j << qlog)) << log_m) + m] = x[j];
+  }
+}
+
+template <class Fr, int MaxR>
 __global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                           const Fr* __restrict__ tw, PassArgs<Fr> a) {
   extern __shared__ uint4 smem_raw[];
@@ -43,7 +95,6 @@ __global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__
   const uint32_t L = a.L, k = a.k, log_m = a.log_m;
   const uint32_t M = 1u << log_m;
   const uint32_t elems = M << k;
-  const uint32_t n = 1u << L;
   const uint32_t b = blockIdx.x;
   in += (size_t)blockIdx.y << L;  // batch of independent contiguous transforms
   out += (size_t)blockIdx.y << L;
@@ -75,27 +126,25 @@ __global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__
   }
   __syncthreads();
 
-  // ---- k butterfly stages ----
-  for (uint32_t t = 0; t < k; ++t) {
-    const uint32_t s = a.s0 + t;
-    const uint32_t half_log = k - 1 - t;
-    const uint32_t half = 1u << half_log;
-    const uint32_t gap = 1u << (L - s - 1);
-    const Fr* tws = tw + (n - (n >> s));
-    for (uint32_t u = threadIdx.x; u < (elems >> 1); u += kBlock) {
-      uint32_t m = u & (M - 1);
-      uint32_t r = u >> log_m;
-      uint32_t blk = r >> half_log, off = r & (half - 1);
-      uint32_t mid_lo = (blk << (half_log + 1)) + off;
-      uint32_t mid_hi = mid_lo + half;
-      uint32_t i_lo = index(mid_lo, m);
-      Fr w = tws[i_lo & (gap - 1)];
-      Fr x = lds[(mid_lo << log_m) + m];
-      Fr y = lds[(mid_hi << log_m) + m];
-      // ButterflyFnInOut: lo = lo + hi; hi = (lo - hi) * w
-      lds[(mid_lo << log_m) + m] = x + y;
-      lds[(mid_hi << log_m) + m] = (x - y) * w;
+  // ---- k butterfly stages, up to MaxR per LDS round trip ----
+  // A step of R stages loads 2^R elements of one set into registers, runs
+  // the R * 2^(R-1) butterflies there (2^(R-1) independent ones per stage,
+  // which the scheduler interleaves) and writes them back: one LDS round
+  // trip and one barrier per R stages instead of per stage.
+  for (uint32_t t = 0; t < k;) {
+    const uint32_t R = min((uint32_t)MaxR, k - t);
+    const bool last = a.final_pass && t + R == k;
+    if (MaxR >= 3 && R == 3) {
+      if (last) radix_step<3, true>(lds, tw, a, t, index);
+      else radix_step<3, false>(lds, tw, a, t, index);
+    } else if (MaxR >= 2 && R == 2) {
+      if (last) radix_step<2, true>(lds, tw, a, t, index);
+      else radix_step<2, false>(lds, tw, a, t, index);
+    } else {
+      if (last) radix_step<1, true>(lds, tw, a, t, index);
+      else radix_step<1, false>(lds, tw, a, t, index);
     }
+    t += R;
     __syncthreads();
   }
 
@@ -245,6 +294,9 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
     }
   }
   pow_bits_ = (log_n_ + 1) / 2;
+  // stages per register step (1 = radix-2 through LDS every stage); the
+  // TACHYON_NTT_RADIX_LOG override is for A/B measurements
+  if (const char* e = getenv("TACHYON_NTT_RADIX_LOG")) radix_ = std::clamp(atoi(e), 1, 3);
   ev_.resize(plan_.size() + 1);
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
   build_twiddles();
@@ -357,8 +409,8 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
     uint32_t elems = (1u << ps.log_m) << ps.k;
     uint32_t blocks = (uint32_t)(n_ / elems);
     size_t lds = (size_t)elems * sizeof(Fr);
-    hipLaunchKernelGGL(dif_pass_kernel<Fr>, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw,
-                       a);
+    auto kern = radix_ == 1 ? dif_pass_kernel<Fr, 1> : radix_ == 2 ? dif_pass_kernel<Fr, 2> : dif_pass_kernel<Fr, 3>;
+    hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw, a);
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(ev_[p + 1], stream_));
   }

@@ -68,9 +68,24 @@ def sharded_ntt(plan, local, inverse: bool = False, group=None):
 
     `local` is a uint8 tensor of plan.local_size * 32 bytes (device tensor for
     the GPU plan); returns the output slab.  The plan's kernels and the RCCL
-    all-to-all run on the same (current) stream, so no extra synchronisation
-    is needed between the stages.
+    all-to-all run on the plan's stream (plan.torch_stream), so no host
+    synchronisation is needed between the stages; the result is ready on that
+    stream (the caller's stream waits for it on the next sharded_ntt call or
+    should call plan.torch_stream.synchronize()).
     """
+    import torch
+    import torch.distributed as dist
+    stream = getattr(plan, "torch_stream", None)
+    if stream is None or not local.is_cuda:  # host plan (CPU rehearsal)
+        return _sharded_ntt_on_stream(plan, local, inverse, group)
+    # one stream orders the stages, the collective and the allocations
+    # (the caller's tensor must be ready on the plan's stream)
+    stream.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        return _sharded_ntt_on_stream(plan, local, inverse, group)
+
+
+def _sharded_ntt_on_stream(plan, local, inverse, group):
     import torch
     import torch.distributed as dist
     send = torch.empty_like(local)

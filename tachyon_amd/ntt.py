@@ -124,11 +124,23 @@ class FourStepNtt:
     rows [r R/G, (r+1) R/G) of X, row-major.  The inverse maps back.
     """
 
-    def __init__(self, log_n: int, world: int, rank: int, stream: int = 0):
+    def __init__(self, log_n: int, world: int, rank: int, stream=None):
+        """stream: a torch.cuda.Stream (or None for a new one).  The plan's
+        kernels run on it; callers run the exchange and any tensor work between
+        the stages under `with torch.cuda.stream(plan.torch_stream)` so that one
+        stream orders everything.  (PyTorch's default stream is the legacy null
+        stream, which does not order against the non-blocking streams HIP
+        libraries create -- a raw handle 0 is therefore not accepted.)"""
+        import torch
         if world & (world - 1):
             raise ValueError("world size must be a power of two")
+        if stream is None:
+            stream = torch.cuda.Stream()
+        if not isinstance(stream, torch.cuda.Stream) or stream.cuda_stream == 0:
+            raise ValueError("FourStepNtt needs a non-default torch.cuda.Stream")
+        self.torch_stream = stream
         self.log_n, self.world, self.rank = log_n, world, rank
-        self._p = lib().tachyon_mi355x_bn254_ntt4_create(log_n, world.bit_length() - 1, rank, stream or None)
+        self._p = lib().tachyon_mi355x_bn254_ntt4_create(log_n, world.bit_length() - 1, rank, stream.cuda_stream)
         if not self._p:
             raise RuntimeError("four-step NTT plan creation failed")
         self.local_size = lib().tachyon_mi355x_bn254_ntt4_local_size(self._p)

@@ -106,7 +106,8 @@ def test_four_step_simulated_ranks(log_n, world):
     X = x.copy().reshape(-1)
     O.fft_np(X)
     X = X.reshape(n, 4)
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = torch.cuda.Stream()  # the plans and every tensor op below share it
+    torch.cuda.set_stream(stream)
     plans = [FourStepNtt(log_n, world, r, stream) for r in range(world)]
     m = n // world
     chunk = (m // world) * 32
@@ -133,6 +134,7 @@ def test_four_step_simulated_ranks(log_n, world):
     back = run(outs, True)
     for r in range(world):
         assert torch.equal(back[r], ins[r]), r
+    torch.cuda.set_stream(torch.cuda.default_stream())
 
 
 def test_batched_transform_device():
