@@ -377,30 +377,32 @@ tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_d
 
 namespace {
 // UnivariateEvaluationDomain::FFT (univariate_evaluation_domain.h:141-182):
-// empty poly -> empty evals; otherwise n evaluations.
-std::vector<FrC> do_fft(const Domain* d, const std::vector<FrC>& coeffs) {
-  std::vector<FrC> out;
-  if (coeffs.empty()) return out;
-  out.resize(d->impl->size());
-  d->impl->forward_host(reinterpret_cast<const Bn254Fr*>(coeffs.data()), coeffs.size(),
-                        reinterpret_cast<Bn254Fr*>(out.data()));
-  return out;
+// empty poly -> empty evals; otherwise n evaluations.  The transform runs in
+// place on the vector it returns: the in-place entry points hand over the
+// caller's vector (no second host allocation -- first-touch page faults of a
+// fresh 512 MiB vector cost more than the transform), the copying ones copy
+// the input once.
+std::vector<FrC> do_fft(const Domain* d, std::vector<FrC>&& v) {
+  if (v.empty()) return std::move(v);
+  const size_t len = v.size(), n = d->impl->size();
+  if (len < n) v.resize(n);  // zero padding
+  d->impl->forward_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
+  return std::move(v);
 }
 // IFFT + RemoveHighDegreeZeros (radix2_evaluation_domain.h:218-223)
-std::vector<FrC> do_ifft(const Domain* d, const std::vector<FrC>& evals) {
-  std::vector<FrC> out;
-  if (evals.empty()) return out;
-  out.resize(d->impl->size());
-  d->impl->inverse_host(reinterpret_cast<const Bn254Fr*>(evals.data()), evals.size(),
-                        reinterpret_cast<Bn254Fr*>(out.data()));
-  size_t len = out.size();
-  while (len > 0) {
-    const FrC& x = out[len - 1];
+std::vector<FrC> do_ifft(const Domain* d, std::vector<FrC>&& v) {
+  if (v.empty()) return std::move(v);
+  const size_t len = v.size(), n = d->impl->size();
+  if (len < n) v.resize(n);
+  d->impl->inverse_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
+  size_t keep = v.size();
+  while (keep > 0) {
+    const FrC& x = v[keep - 1];
     if (x.limbs[0] | x.limbs[1] | x.limbs[2] | x.limbs[3]) break;
-    --len;
+    --keep;
   }
-  out.resize(len);
-  return out;
+  v.resize(keep);
+  return std::move(v);
 }
 }  // namespace
 
@@ -410,7 +412,7 @@ tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain
     const tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_univariate_dense_polynomial* poly) {
   GUARD_BEGIN
   auto* e = new tachyon_bn254_univariate_evaluations();
-  e->v = do_fft(domain, poly->v);
+  e->v = do_fft(domain, std::vector<FrC>(poly->v));
   return e;
   GUARD_END
 }
@@ -420,7 +422,7 @@ tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain
   auto* e = new tachyon_bn254_univariate_evaluations();
   std::vector<FrC> in = std::move(poly->v);  // moved-from, as FFT(DensePoly&&)
   poly->v.clear();
-  e->v = do_fft(domain, in);
+  e->v = do_fft(domain, std::move(in));
   return e;
   GUARD_END
 }
@@ -428,7 +430,7 @@ tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_d
     const tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_univariate_evaluations* evals) {
   GUARD_BEGIN
   auto* p = new tachyon_bn254_univariate_dense_polynomial();
-  p->v = do_ifft(domain, evals->v);
+  p->v = do_ifft(domain, std::vector<FrC>(evals->v));
   return p;
   GUARD_END
 }
@@ -438,7 +440,7 @@ tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_d
   auto* p = new tachyon_bn254_univariate_dense_polynomial();
   std::vector<FrC> in = std::move(evals->v);
   evals->v.clear();
-  p->v = do_ifft(domain, in);
+  p->v = do_ifft(domain, std::move(in));
   return p;
   GUARD_END
 }
