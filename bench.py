@@ -33,6 +33,26 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 
 MSM_BYTES_PER_POINT = 96  # 64 B affine base + 32 B scalar
 NTT_BYTES_PER_ELEM = 64   # 32 B in + 32 B out per transform
 SEED = 0x7AC40001
+# Measured BN254 Montgomery-multiply ceiling of the chip (tools/microbench/mulmod_rates.hip,
+# 8 waves/SIMD, profiles/r01/microbench_int_rates.txt): the VALU roofline of both kernels.
+MULMOD_PEAK_G = 129.0
+MADD_MULMODS = 10  # madd-2008-s: 8 multiplications + 2 squarings (point_xyzz_impl.h:129-176)
+
+
+def pmc_traffic(kernel):
+    """Per-dispatch HBM bytes of `kernel` from the newest committed rocprofv3 PMC
+    passes (profiles/<round>/pmc_traffic.json, written by tools/profile_round.sh
+    from separate FETCH_SIZE / WRITE_SIZE runs of this bench command); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    for f in reversed(files):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel in t:
+            return t[kernel]["traffic_bytes"] / 1e9, os.path.relpath(f, ROOT)
+    return None, None
 
 
 def parse():
@@ -249,6 +269,8 @@ def main():
     acc_ms = sorted(p["acc"] for p in prof)[1] / launches
     acc_gbs = n / launches * MSM_BYTES_PER_POINT / (acc_ms * 1e-3) / 1e9
     c, windows = M.plan("bn254_g1", n)
+    acc_traffic, acc_traffic_src = pmc_traffic("seg_acc_kernel")
+    acc_gmulmod = n * windows / launches * MADD_MULMODS / (acc_ms * 1e-3) / 1e9
 
     out = {
         "metric": METRIC,
@@ -270,12 +292,17 @@ def main():
                    "parallelism": f"msm point shards x{world} + RCCL all-gather of partial points"},
         "consistent_across_steps": consistent,
         "roofline": {"bound": "hbm", "achieved": acc_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": acc_gbs / HBM_PEAK_GBS, "traffic": None,
+                     "frac": acc_gbs / HBM_PEAK_GBS,
+                     "traffic": acc_traffic, "traffic_unit": "GB per launch", "traffic_source": acc_traffic_src,
                      "kernel": "seg_acc_kernel (bucket accumulation, madd-2008-s)", "kernel_ms": acc_ms,
                      "launches_per_msm": launches,
                      "note": "algorithmic bytes = 96 B/point x n/launches point-units per launch (one window "
                              "per launch); the kernel is VALU-bound (v_mad_u64_u32), see DESIGN.md"},
         "msm_phase_ms": phases,
+        "valu_roofline": {"bound": "valu", "kernel": "seg_acc_kernel", "achieved": acc_gmulmod,
+                          "peak": MULMOD_PEAK_G, "unit": "G mulmod/s", "frac": acc_gmulmod / MULMOD_PEAK_G,
+                          "note": "n x windows mixed additions x 10 Montgomery products per launch / launch time; "
+                                  "peak = measured BN254 mulmod ceiling (tools/microbench/mulmod_rates.hip)"},
     }
 
     # ---- NTT 2^24: one GPU, or the four-step sharded transform (one RCCL all-to-all) ----
@@ -337,11 +364,20 @@ def main():
         dom.set_profile(False)
         avg_pass = sum(passes) / len(passes)
         pass_gbs = nn * NTT_BYTES_PER_ELEM / (avg_pass * 1e-3) / 1e9
+        ntt_traffic, ntt_traffic_src = pmc_traffic("dif_pass_kernel")
+        # algorithmic butterflies (one Montgomery product each) per pass: n/2 x log n / passes
+        ntt_gmulmod = nn // 2 * args.ntt_log_n / len(passes) / (avg_pass * 1e-3) / 1e9
         out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
                       "round_trip_ok": round_trip_ok, "pass_ms": passes, "mode": "single GPU",
                       "roofline": {"bound": "hbm", "achieved": pass_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": pass_gbs / HBM_PEAK_GBS, "traffic": None,
-                                   "kernel": "dif_pass_kernel", "kernel_ms": avg_pass}}
+                                   "frac": pass_gbs / HBM_PEAK_GBS, "traffic": ntt_traffic,
+                                   "traffic_unit": "GB per launch", "traffic_source": ntt_traffic_src,
+                                   "kernel": "dif_pass_kernel", "kernel_ms": avg_pass},
+                      "valu_roofline": {"bound": "valu", "kernel": "dif_pass_kernel", "achieved": ntt_gmulmod,
+                                        "peak": MULMOD_PEAK_G, "unit": "G mulmod/s",
+                                        "frac": ntt_gmulmod / MULMOD_PEAK_G,
+                                        "note": "n/2 x log n butterflies per transform / passes, one product "
+                                                "each (the add/sub of a butterfly are not counted)"}}
         dom.close()
 
     if args.groth16_log_n and world == 1:

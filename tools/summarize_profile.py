@@ -4,6 +4,7 @@ kernel-trace stats (top kernels) and per-kernel PMC averages with the gfx950
 FETCH_SIZE correction (x2 for wide coalesced streams, MI355X_MICROARCH.md §HBM)."""
 import collections
 import csv
+import json
 import os
 import sys
 
@@ -68,6 +69,22 @@ def main(d):
             print(f"| {k} | {v} | {sc} | {l} | {fmt(fetch * 2 if fetch else None)} | {fmt(write)} | {fmt(insts)} | "
                   f"{valu} | - |")
         print("\nVALU busy % = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of wave-cycles issuing VALU).")
+        # per-dispatch HBM traffic for bench.py's roofline "traffic" field
+        # (FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a
+        # wide streaming read -- MI355X_MICROARCH.md, HBM/rocprofv3 -- so the x2
+        # value is the corrected one; other access widths are uncalibrated)
+        traffic = {}
+        for k in sorted({k for k, _ in agg}):
+            f = agg.get((k, "FETCH_SIZE"))
+            w = agg.get((k, "WRITE_SIZE"))
+            if not f or not w:
+                continue
+            fb = sum(f) / len(f) * 1024
+            wb = sum(w) / len(w) * 1024
+            traffic[k] = {"dispatches": len(f), "fetch_bytes_raw": fb, "fetch_bytes_x2": 2 * fb, "write_bytes": wb,
+                          "traffic_bytes": 2 * fb + wb}
+        with open(os.path.join(d, "pmc_traffic.json"), "w") as fh:
+            json.dump(traffic, fh, indent=1)
 
 
 if __name__ == "__main__":
