@@ -144,6 +144,7 @@ class MsmGpu {
   std::vector<hipEvent_t> gev_sorted_, gev_acc0_, gev_acc1_;
   unsigned acc_launches_ = 0;
   unsigned sort_bits_ = 0;
+  uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (experiments only)
   DeviceBuffer maxlen_;
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
                                                          const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ vals, uint32_t c,
                                                          uint64_t gbeg, uint64_t gend, uint64_t tbase,
-                                                         uint32_t K,
+                                                         uint32_t K, uint32_t idx_mask,
                                                          XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                          XYZZ<typename Curve::F>* __restrict__ pieces,
                                                          uint32_t* __restrict__ tflags,
@@ -135,11 +135,11 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
   uint32_t k0 = keys[g0], v0 = vals[g0];
   uint32_t k1 = 0, v1 = 0;
   if (g0 + 1 < g1) { k1 = keys[g0 + 1]; v1 = vals[g0 + 1]; }
-  Affine<F> P = hbases[v0 & ~kSignBit];
+  Affine<F> P = hbases[v0 & idx_mask];
   for (uint64_t g = g0; g < g1; ++g) {
     uint32_t k2 = 0, v2 = 0;
     if (g + 2 < g1) { k2 = keys[g + 2]; v2 = vals[g + 2]; }
-    Affine<F> Pn = hbases[v1 & ~kSignBit];
+    Affine<F> Pn = hbases[v1 & idx_mask];
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
       if (b != cur) {
@@ -465,6 +465,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     size_t bytes = sort_bytes;
     TA_HIP(sort_pairs(sort_tmp, bytes, keys + e0, keys2 + e0, vals + e0, vals2 + e0, ecount, key_bits,
                       sort_stream));
+    if (profile_ && g + 1 == ngroups) TA_HIP(hipEventRecord(ev_[3], sort_stream));  // last sort done
     if (sort_stream != stream_) {
       TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream));
       TA_HIP(hipStreamWaitEvent(stream_, gev_sorted_[g], 0));
@@ -472,12 +473,12 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
     hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2, c,
-                       (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, bucket_sum, pieces, tflags, tlast);
+                       (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
+                       tflags, tlast);
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(gev_acc1_[g], stream_));
     tbase += Tg;
   }
-  if (profile_) TA_HIP(hipEventRecord(ev_[3], sort_stream));  // last sort done
   if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));        // last accumulation done
 
   // ---- join buckets that cross thread boundaries ----
@@ -576,6 +577,9 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
     case 3: plan.group = plan.windows; break;
     default: break;
   }
+  // bit 6: gather-locality experiment -- every base index masked to 2^20
+  // points (a 64 MiB slice that stays in the Infinity Cache); results are wrong
+  idx_mask_ = (variant_ & 64) ? ((1u << 20) - 1) : ~kSignBit;
   static constexpr unsigned kSortBits[] = {0, 10, 11, 7};
   sort_bits_ = kSortBits[(variant_ >> 4) & 3];
   if (plan_out) *plan_out = plan;
