@@ -92,11 +92,24 @@ void dump_inputs(const std::string& dir, size_t idx, const void* bases, const vo
   fclose(f);
 }
 
-template <class F>
-void print_hex(const F& x) {
-  const uint64_t* l = reinterpret_cast<const uint64_t*>(&x);
-  printf("0x");
-  for (size_t i = sizeof(F) / 8; i-- > 0;) printf("%016lx", (unsigned long)l[i]);
+// canonical value in hex, "0x" + lowercase digits without leading zeros
+// (BigInt::ToHexString, big_int.cc:55-58; fields print their canonical value)
+template <class C>
+void print_hex(const Fp<C>& x) {
+  const Fp<C> c = x.from_mont();
+  const uint32_t* l = c.v;
+  int i = Fp<C>::N - 1;
+  while (i > 0 && l[i] == 0) --i;
+  printf("0x%x", l[i]);
+  while (--i >= 0) printf("%08x", l[i]);
+}
+template <class B>
+void print_hex(const Fp2<B>& x) {
+  printf("(");
+  print_hex(x.c0);
+  printf(", ");
+  print_hex(x.c1);
+  printf(")");
 }
 
 // DoMSMGpu: run, normalise, return a new Jacobian (z = 1, or the (1,1,0) zero).

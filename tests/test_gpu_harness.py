@@ -33,3 +33,43 @@ def test_fft_benchmark_gpu(flags):
     out, res = run(["fft_benchmark_gpu", "-k", "14", "-k", "10", "--check_results"] + flags)
     assert res["check_results"] == "pass"
     assert [r["k"] for r in res["results"]] == [10, 14]
+
+
+REPLAY_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+from tachyon_amd.msm import VariableBaseMSMGpu
+m = VariableBaseMSMGpu("bn254_g1")
+for i, n in enumerate((300, 77)):
+    m.run_jacobian(O.gen_bases("bn254_g1", 40 + i, n, 8).tobytes(), O.gen_scalars("bn254_fr", 40 + i, n).tobytes())
+"""
+
+
+def test_msm_dump_and_replay(tmp_path):
+    """TACHYON_MSM_GPU_INPUT_DIR dumps (msm_gpu.h:99-119) replayed by
+    bin/msm_gpu_replay (msm_gpu_replay.cc) give the oracle's MSM; the dump
+    holds canonical limbs after a u64 count; TACHYON_LOG_MSM prints the result."""
+    import sys
+    from oracle import oracle as O
+    from oracle import pyref
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, TACHYON_MSM_GPU_INPUT_DIR=str(tmp_path), TACHYON_LOG_MSM="1")
+    log = subprocess.run([sys.executable, "-c", REPLAY_CHILD, root], env=env, check=True, timeout=120,
+                         capture_output=True, text=True).stdout
+    G1 = pyref.Curve("bn254_g1")
+    expect = []
+    for i, n in enumerate((300, 77)):
+        bases = O.gen_bases("bn254_g1", 40 + i, n, 8).tobytes()
+        scalars = O.gen_scalars("bn254_fr", 40 + i, n).tobytes()
+        dump = open(tmp_path / f"scalars{i}.txt", "rb").read()
+        assert int.from_bytes(dump[:8], "little") == n
+        assert dump[8:40] == G1.Fr.from_bytes(scalars[:32]).to_bytes(32, "little")
+        pt = G1.from_bytes(O.msm("bn254_g1", bases, scalars)[0])
+        expect.append(f"({hex(pt[0])}, {hex(pt[1])})")
+        assert f"DoMSMGpu(){i}\n{expect[-1]}" in log
+    out = subprocess.run([os.path.join(BIN, "msm_gpu_replay"), "--input_dir", str(tmp_path), "--degree", "9",
+                          "--idx", "0", "--idx", "1"], check=True, timeout=120, capture_output=True, text=True,
+                         env={k: v for k, v in os.environ.items() if k != "TACHYON_MSM_GPU_INPUT_DIR"}).stdout
+    got = [l for l in out.splitlines() if l.startswith("(")]
+    assert got == expect
