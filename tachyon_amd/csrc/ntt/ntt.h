@@ -85,7 +85,7 @@ class NttDomain {
   bool profile_ = false;
   std::vector<Pass> plan_;
   uint32_t pow_bits_ = 0;  // split point of the two-level power tables
-  int radix_ = 3;          // DIF stages per register step of the pass kernel
+  int radix_ = 2;          // DIF stages per register step of the pass kernel (see kMaxLdsElems)
   DeviceBuffer tw_fwd_, tw_inv_, scratch_, io_;
   DeviceBuffer coset_lo_, coset_hi_, icoset_lo_, icoset_hi_;
   NttTimings timings_;

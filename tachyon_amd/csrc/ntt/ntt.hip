@@ -13,7 +13,12 @@ namespace {
 
 constexpr unsigned kBlock = 256;
 constexpr uint32_t kMaxPassStages = 8;
-constexpr uint32_t kMaxLdsElems = 2048;  // 64 KiB of 32-byte elements: 2 workgroups / CU
+// Elements per workgroup: 1024 (32 KiB of LDS) = 256 threads x 2^2, so every
+// thread owns one radix-4 group per register step and 5 workgroups fit a CU
+// (5 waves per SIMD at 88 VGPRs).  2^24 sweep (tools/tune_ntt.py,
+// TACHYON_NTT_LDS_ELEMS x TACHYON_NTT_RADIX_LOG): 2048/r3 2.43, 2048/r2 2.44,
+// 1024/r2 1.95, 1024/r3 2.82 (half the threads idle), 512/r2 2.54 ms.
+constexpr uint32_t kMaxLdsElems = 1024;
 
 enum : uint32_t { kLoadCoset = 1, kStoreScale = 2, kStoreCoset = 4 };
 
@@ -275,6 +280,9 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
   offset_ = Fr::one();
   offset_inv_ = Fr::one();
 
+  // elements per workgroup (LDS footprint); TACHYON_NTT_LDS_ELEMS overrides for A/B runs
+  uint32_t lds_elems = kMaxLdsElems;
+  if (const char* e = getenv("TACHYON_NTT_LDS_ELEMS")) lds_elems = std::clamp<uint32_t>(atoi(e), 256, 2048);
   // pass plan: ceil(L / 8) passes, stages split evenly
   if (log_n_ > 0) {
     uint32_t P = (log_n_ + kMaxPassStages - 1) / kMaxPassStages;
@@ -287,7 +295,7 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
       ps.final_pass = (s0 + k == log_n_);
       uint32_t avail = ps.final_pass ? (log_n_ - k) : (log_n_ - s0 - k);  // log2 of sets available
       uint32_t log_m = 0;
-      while (log_m < avail && ((2u << log_m) << k) <= kMaxLdsElems) ++log_m;
+      while (log_m < avail && ((2u << log_m) << k) <= lds_elems) ++log_m;
       ps.log_m = log_m;
       plan_.push_back(ps);
       s0 += k;
