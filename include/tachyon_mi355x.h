@@ -303,6 +303,25 @@ TACHYON_C_EXPORT int tachyon_mi355x_zkey_curve(const uint8_t* zkey, size_t len);
 TACHYON_C_EXPORT size_t tachyon_mi355x_wtns_parse(int curve, const uint8_t* wtns, size_t len, void* out,
                                                   size_t cap);
 
+/* KZG commitments with a device-resident SRS (the reference's
+ * tachyon/crypto/commitments/kzg/kzg.h is C++ only).  curve: 0 bn254_g1,
+ * 2 bls12_381_g1.  Field elements Montgomery form, points affine.
+ *   unsafe_setup: size a power of two; SRS = [tau^i] G and [L_i(tau)] G over
+ *     the size-n domain (UnsafeSetup :173-207), built and kept on the device;
+ *   downsize: returns 0 if n >= N (Downsize :210-215);
+ *   get_srs: the N points (lagrange = 0 powers of tau, 1 Lagrange) to host;
+ *   commit: MSM of the first min(N, len) SRS points with `scalars` (host or
+ *     device pointer) -- Commit (lagrange = 0) / CommitLagrange (1), :217-258. */
+typedef struct tachyon_mi355x_kzg tachyon_mi355x_kzg;
+TACHYON_C_EXPORT tachyon_mi355x_kzg* tachyon_mi355x_kzg_create(int curve);
+TACHYON_C_EXPORT void tachyon_mi355x_kzg_destroy(tachyon_mi355x_kzg* kzg);
+TACHYON_C_EXPORT void tachyon_mi355x_kzg_unsafe_setup(tachyon_mi355x_kzg* kzg, size_t size, const void* tau);
+TACHYON_C_EXPORT size_t tachyon_mi355x_kzg_n(const tachyon_mi355x_kzg* kzg);
+TACHYON_C_EXPORT int tachyon_mi355x_kzg_downsize(tachyon_mi355x_kzg* kzg, size_t n);
+TACHYON_C_EXPORT void tachyon_mi355x_kzg_get_srs(const tachyon_mi355x_kzg* kzg, int lagrange, void* out);
+TACHYON_C_EXPORT void tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* kzg, int lagrange, const void* scalars,
+                                                size_t len, void* out_affine);
+
 /* delete a Jacobian returned by an *_msm / *_msm_gpu entry point (for callers
  * that cannot use C++ delete, e.g. ctypes). */
 TACHYON_C_EXPORT void tachyon_mi355x_jacobian_destroy(int curve, void* jacobian);

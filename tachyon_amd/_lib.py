@@ -115,6 +115,13 @@ SIGNATURES = [
     ("tachyon_mi355x_groth16_last_timings", None, [vp, fp]),
     ("tachyon_mi355x_zkey_curve", i32, [vp, sz]),
     ("tachyon_mi355x_wtns_parse", sz, [i32, vp, sz, vp, sz]),
+    ("tachyon_mi355x_kzg_create", vp, [i32]),
+    ("tachyon_mi355x_kzg_destroy", None, [vp]),
+    ("tachyon_mi355x_kzg_unsafe_setup", None, [vp, sz, vp]),
+    ("tachyon_mi355x_kzg_n", sz, [vp]),
+    ("tachyon_mi355x_kzg_downsize", i32, [vp, sz]),
+    ("tachyon_mi355x_kzg_get_srs", None, [vp, i32, vp]),
+    ("tachyon_mi355x_kzg_commit", None, [vp, i32, vp, sz, vp]),
     ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
     ("tachyon_mi355x_version", ctypes.c_char_p, []),
     ("tachyon_mi355x_device_count", i32, []),

@@ -1,0 +1,59 @@
+// KZG commitments with a device-resident SRS on MI355X.
+//
+// Reference: tachyon/crypto/commitments/kzg/kzg.h
+//   :90-114   SetupForGpu -- the SRS lives in device memory next to the GPU MSM
+//   :173-207  UnsafeSetup(size, tau): g1_powers_of_tau = [tau^i] G and
+//             g1_powers_of_tau_lagrange = [L_i(tau)] G over the size-n domain
+//             (BatchMapScalarFieldToPoint, affine_point.h:184-206;
+//             EvaluateAllLagrangeCoefficients, univariate_evaluation_domain.h:279-360)
+//   :210-215  Downsize(n): false if n >= N
+//   :217-258  Commit / CommitLagrange = MSM over the first min(N, |v|) SRS points
+//   :267-313  DoMSM (batch commitments: one MSM per polynomial into a slot)
+// Both SRS vectors are built on the GPU: per-element tau^i and L_i(tau)
+// (Fermat inverse per element), then a fixed-base double-and-add per point.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <memory>
+
+#include "../common/hip_util.h"
+#include "../msm/msm.h"
+
+namespace tachyon_amd::kzg {
+
+template <class Curve>
+class Kzg {
+ public:
+  using F = typename Curve::F;
+  using Fr = typename Curve::Fr;
+  using Aff = Affine<F>;
+
+  explicit Kzg(hipStream_t stream = nullptr);
+  ~Kzg();
+  Kzg(const Kzg&) = delete;
+  Kzg& operator=(const Kzg&) = delete;
+
+  // size must be a power of two (the Lagrange basis is over the radix-2 domain)
+  void unsafe_setup(size_t size, const Fr& tau);
+  size_t n() const { return n_; }
+  bool downsize(size_t n);
+
+  // MSM of the first min(N, len) SRS points with `scalars` (host or device).
+  Aff commit(const Fr* scalars, size_t len, bool lagrange);
+
+  const Aff* d_srs(bool lagrange) const { return lagrange ? lagrange_.as<Aff>() : powers_.as<Aff>(); }
+  void copy_srs(bool lagrange, Aff* host_out) const;
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
+  size_t n_ = 0;
+  DeviceBuffer powers_, lagrange_, scratch_;
+  std::unique_ptr<msm::MsmGpu<Curve>> msm_;
+};
+
+extern template class Kzg<Bn254G1>;
+extern template class Kzg<Bls381G1>;
+
+}  // namespace tachyon_amd::kzg

@@ -1,0 +1,152 @@
+// KZG with a device-resident SRS (see kzg.h for the reference mapping).
+#include "kzg.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <vector>
+
+#include "../field/curve_constants.h"
+#include "../ntt/ntt.h"
+
+namespace tachyon_amd::kzg {
+
+namespace {
+
+constexpr unsigned kBlock = 256;
+
+template <class Curve>
+struct Generator;
+template <>
+struct Generator<Bn254G1> {
+  static constexpr const uint64_t* x = consts::bn254_g1::kXMont64;
+  static constexpr const uint64_t* y = consts::bn254_g1::kYMont64;
+};
+template <>
+struct Generator<Bls381G1> {
+  static constexpr const uint64_t* x = consts::bls12_381_g1::kXMont64;
+  static constexpr const uint64_t* y = consts::bls12_381_g1::kYMont64;
+};
+
+template <class F>
+F from_words(const uint64_t* w) {
+  F r;
+  for (int i = 0; i < F::N; ++i) r.v[i] = (uint32_t)(w[i / 2] >> (32 * (i & 1)));
+  return r;
+}
+
+// s_i = tau^i; l_i = L_i(tau) = (Z_H(tau) / n) * w^i / (tau - w^i)
+// (EvaluatePartialLagrangeCoefficients, univariate_evaluation_domain.h:308-360,
+// offset 1), one Fermat inverse per element
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void srs_scalars_kernel(Fr tau, Fr omega, Fr z_over_n, uint32_t n,
+                                                             Fr* __restrict__ s, Fr* __restrict__ l) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Fr ti = tau.pow(&i, 1);
+  s[i] = ti.canonical();
+  if (l) {
+    const Fr wi = omega.pow(&i, 1);
+    l[i] = (z_over_n * wi * (tau - wi).inverse()).canonical();
+  }
+}
+
+// out_i = k_i * G (BatchMapScalarFieldToPoint), double-and-add from the top bit
+template <class Curve>
+__global__ __launch_bounds__(kBlock) void fixed_base_kernel(Affine<typename Curve::F> g,
+                                                            const typename Curve::Fr* __restrict__ k, uint32_t n,
+                                                            Affine<typename Curve::F>* __restrict__ out) {
+  using F = typename Curve::F;
+  using Fr = typename Curve::Fr;
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Fr c = k[i].from_mont();
+  XYZZ<F> r = XYZZ<F>::zero();
+  for (int b = Fr::N * 32 - 1; b >= 0; --b) {
+    r = r.dbl();
+    if ((c.v[b / 32] >> (b % 32)) & 1) r = r.madd(g);
+  }
+  out[i] = r.to_affine();
+}
+
+}  // namespace
+
+template <class Curve>
+Kzg<Curve>::Kzg(hipStream_t stream) : stream_(stream) {
+  require_gpu();
+  if (!stream_) {
+    TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    own_stream_ = true;
+  }
+  msm_ = std::make_unique<msm::MsmGpu<Curve>>(stream_);
+}
+
+template <class Curve>
+Kzg<Curve>::~Kzg() {
+  msm_.reset();
+  if (own_stream_) (void)hipStreamDestroy(stream_);
+}
+
+template <class Curve>
+void Kzg<Curve>::unsafe_setup(size_t size, const Fr& tau) {
+  if (size == 0 || (size & (size - 1)) || size > (size_t(1) << 30))
+    throw std::runtime_error("tachyon_mi355x: KZG setup size must be a power of two <= 2^30");
+  uint32_t log_n = 0;
+  while ((size_t(1) << log_n) < size) ++log_n;
+  const Fr omega = ntt::root_of_unity<Fr>(log_n);
+  const uint32_t n = (uint32_t)size;
+  const uint32_t e = n;
+  const Fr z = tau.pow(&e, 1) - Fr::one();  // Z_H(tau) = tau^n - 1
+  Fr* d_s = static_cast<Fr*>(scratch_.ensure(2 * size * sizeof(Fr)));
+  Fr* d_l = d_s + size;
+  const unsigned grid = ceil_div(size, kBlock);
+  if (!z.is_zero()) {
+    const Fr z_over_n = z * ntt::field_from_u64<Fr>(size).inverse();
+    hipLaunchKernelGGL(srs_scalars_kernel<Fr>, dim3(grid), dim3(kBlock), 0, stream_, tau, omega, z_over_n, n, d_s,
+                       d_l);
+  } else {
+    // tau = w^j: L_j(tau) = 1, every other coefficient 0 (univariate_evaluation_domain.h:309-323)
+    hipLaunchKernelGGL(srs_scalars_kernel<Fr>, dim3(grid), dim3(kBlock), 0, stream_, tau, omega, Fr::zero(), n, d_s,
+                       static_cast<Fr*>(nullptr));
+    std::vector<Fr> l(size, Fr::zero());
+    Fr w = Fr::one();
+    for (size_t j = 0; j < size; ++j, w = w * omega)
+      if (w == tau) {
+        l[j] = Fr::one();
+        break;
+      }
+    TA_HIP(hipMemcpyAsync(d_l, l.data(), size * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+    TA_HIP(hipStreamSynchronize(stream_));
+  }
+  TA_HIP(hipGetLastError());
+  const Aff g{from_words<F>(Generator<Curve>::x), from_words<F>(Generator<Curve>::y)};
+  Aff* d_p = static_cast<Aff*>(powers_.ensure(size * sizeof(Aff)));
+  Aff* d_lg = static_cast<Aff*>(lagrange_.ensure(size * sizeof(Aff)));
+  hipLaunchKernelGGL(fixed_base_kernel<Curve>, dim3(grid), dim3(kBlock), 0, stream_, g, d_s, n, d_p);
+  hipLaunchKernelGGL(fixed_base_kernel<Curve>, dim3(grid), dim3(kBlock), 0, stream_, g, d_l, n, d_lg);
+  TA_HIP(hipGetLastError());
+  TA_HIP(hipStreamSynchronize(stream_));
+  n_ = size;
+}
+
+template <class Curve>
+bool Kzg<Curve>::downsize(size_t n) {
+  if (n >= n_) return false;
+  n_ = n;  // the device arrays keep their capacity; only the prefix is used
+  return true;
+}
+
+template <class Curve>
+typename Kzg<Curve>::Aff Kzg<Curve>::commit(const Fr* scalars, size_t len, bool lagrange) {
+  const size_t m = std::min(n_, len);
+  return msm_->run(d_srs(lagrange), scalars, m).to_affine();
+}
+
+template <class Curve>
+void Kzg<Curve>::copy_srs(bool lagrange, Aff* host_out) const {
+  TA_HIP(hipMemcpy(host_out, d_srs(lagrange), n_ * sizeof(Aff), hipMemcpyDeviceToHost));
+}
+
+template class Kzg<Bn254G1>;
+template class Kzg<Bls381G1>;
+
+}  // namespace tachyon_amd::kzg
