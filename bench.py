@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ntt", action="store_true")
     ap.add_argument("--cpu-sample-log-n", type=int, default=22)
+    ap.add_argument("--bls-log-n", type=int, default=24,
+                    help="BLS12-381 G1 + G2 MSM size (BASELINE configs[3]); 0 = skip")
     ap.add_argument("--groth16-log-n", type=int, default=20,
                     help="Groth16 prove on a synthetic 2^k-constraint circom key (BASELINE configs[4]); 0 = skip")
     return ap.parse_args()
@@ -162,6 +164,47 @@ def synth_groth16_zkey(log_n, seed=SEED):
     for t, body in secs:
         parts += [struct.pack("<IQ", t, len(body)), body]
     return b"".join(parts), full
+
+
+def bench_bls(args, rank, world, barrier, dist, backend):
+    """BLS12-381 G1 and G2 MSMs at 2^k (BASELINE configs[3]): point shards per
+    rank + the all-gather of partials, device-resident inputs, as the headline."""
+    import torch
+    from tachyon_amd import dist as D
+    from tachyon_amd import msm as M
+    out = {}
+    n_total = 1 << args.bls_log_n
+    start, n = D.shard_range(n_total, rank, world)
+    for curve, pb in (("bls12_381_g1", 96), ("bls12_381_g2", 192)):
+        d_b = torch.empty(max(1, n) * pb, dtype=torch.uint8, device="cuda")
+        d_s = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
+        M.gen_bases(curve, SEED + rank, n, 1 << 10, d_b.data_ptr())
+        M.gen_scalars("bls12_381_fr", SEED, n, d_s.data_ptr(), start=start)
+        torch.cuda.synchronize()
+        msm = M.VariableBaseMSMGpu(curve)
+
+        def step():
+            return D.sharded_msm(curve, lambda: msm.run(d_b, d_s, n), device="cuda")
+
+        ref = step()
+        reps = max(2, min(args.steps, 3))
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = step()
+        barrier()
+        dt = (time.perf_counter() - t0) / reps
+        if dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out[curve.split("_")[-1]] = {"ms_per_msm": dt * 1e3, "scalars_per_s": n_total / dt,
+                                     "consistent": res == ref, "points_per_gpu": n}
+        msm.close()
+        del d_b, d_s
+    out["workload"] = (f"BLS12-381 G1 and G2 VariableBaseMSM 2^{args.bls_log_n} (BASELINE configs[3]), "
+                       f"device-resident inputs, point shards x{world} + all-gather of partials")
+    return out
 
 
 def bench_groth16(args):
@@ -379,6 +422,9 @@ def main():
                                         "note": "n/2 x log n butterflies per transform / passes, one product "
                                                 "each (the add/sub of a butterfly are not counted)"}}
         dom.close()
+
+    if args.bls_log_n:
+        out["bls12_381"] = bench_bls(args, rank, world, barrier, dist, backend)
 
     if args.groth16_log_n and world == 1:
         out["groth16"] = bench_groth16(args)
