@@ -129,7 +129,7 @@ class MsmGpu {
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
   void ensure_group_events(unsigned groups);
   hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
-                        uint32_t* vout, size_t count, unsigned end_bit, hipStream_t s);
+                        uint32_t* vout, size_t count, unsigned begin_bit, unsigned end_bit, hipStream_t s);
 
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;
@@ -145,6 +145,8 @@ class MsmGpu {
   unsigned acc_launches_ = 0;
   unsigned sort_bits_ = 0;
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (experiments only)
+  bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
+  DeviceBuffer hist_, hscan_tmp_;
   DeviceBuffer maxlen_;
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;

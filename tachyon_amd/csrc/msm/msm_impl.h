@@ -30,15 +30,11 @@ enum : uint32_t { kHead = 1, kTail = 2, kSingle = 4 };
 // key = window << c | |digit| (digit 0 = no contribution), so one radix sort
 // over all windows orders the entries by (window, bucket) and every window
 // keeps its slice [w*n, (w+1)*n); val = point index | sign << 31.
-template <class Fr>
-__global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
-                                                        unsigned c, unsigned W,
-                                                        uint32_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ vals) {
-  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+// Signed c-bit digits of one scalar, window by window: emit(w, key, val).
+template <class Fr, class Emit>
+__device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsigned c, unsigned W, Emit emit) {
   constexpr int N = Fr::N;
-  Fr s = scalars[i].from_mont();
+  Fr s = scalar.from_mont();
   uint32_t limbs[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) limbs[k] = s.v[k];
@@ -61,9 +57,100 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
       key = coeff;  // top digit, carry folded in, non-negative
       sign = 0;
     }
+    emit(w, (w << c) | key, i | sign);
+  }
+}
+
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
+                                                        unsigned c, unsigned W,
+                                                        uint32_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ vals) {
+  uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  recode_scalar(scalars[i], i, c, W, [&](unsigned w, uint32_t key, uint32_t val) {
     size_t o = (size_t)w * n + i;
-    keys[o] = (w << c) | key;
-    vals[o] = i | sign;
+    keys[o] = key;
+    vals[o] = val;
+  });
+}
+
+// Recode fused with the first radix pass (key bits 0..7), in two launches:
+// recode_hist_kernel counts, per block of kRecodeScalars scalars, the entries
+// of each low-byte bin (LDS atomics) into hist[bin * nblocks + block]; after
+// an exclusive scan of hist, recode_scatter_kernel recomputes the digits and
+// writes every (key, val) to its bin's slot (the rank inside the block's run
+// from LDS atomics).  This pass need not be stable -- the later stable passes
+// over bits 8.. keep the bin grouping, and the order inside a bucket does not
+// change the bucket's sum -- so it replaces the recode's 8-byte write plus one
+// full onesweep pass (read + write + histogram read) with two reads of the
+// 32-byte scalars and one write.
+constexpr unsigned kRecodeScalars = 2 * kBlock;
+
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restrict__ scalars, uint32_t n, unsigned c,
+                                                             unsigned W, uint32_t nblocks,
+                                                             uint32_t* __restrict__ hist) {
+  __shared__ uint32_t cnt[256];
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t k = 0; k < kRecodeScalars / kBlock; ++k) {
+    const uint32_t i = blockIdx.x * kRecodeScalars + k * kBlock + threadIdx.x;
+    if (i < n)
+      recode_scalar(scalars[i], i, c, W, [&](unsigned, uint32_t key, uint32_t) { atomicAdd(&cnt[key & 255], 1u); });
+  }
+  __syncthreads();
+  hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+}
+
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __restrict__ scalars, uint32_t n,
+                                                                unsigned c, unsigned W, uint32_t nblocks,
+                                                                const uint32_t* __restrict__ hist,
+                                                                const uint32_t* __restrict__ off,
+                                                                uint32_t* __restrict__ keys,
+                                                                uint32_t* __restrict__ vals) {
+  // the block's entries are binned in LDS first, then written out bin run by
+  // bin run, so consecutive lanes store to consecutive addresses
+  extern __shared__ uint32_t lds_u32[];
+  uint32_t* lkeys = lds_u32;                           // kRecodeScalars * W
+  uint32_t* lvals = lds_u32 + kRecodeScalars * W;      // kRecodeScalars * W
+  __shared__ uint32_t base[256], loff[256], cur[256];
+  const uint32_t t = threadIdx.x;
+  base[t] = off[(size_t)t * nblocks + blockIdx.x];
+  const uint32_t mine = hist[(size_t)t * nblocks + blockIdx.x];
+  // exclusive scan of the block's 256 bin counts (4 waves x 64 lanes)
+  uint32_t v = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(v, d, 64);
+    if ((t & 63) >= (uint32_t)d) v += u;
+  }
+  __shared__ uint32_t wave_tot[kBlock / 64];
+  if ((t & 63) == 63) wave_tot[t >> 6] = v;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t w = 0; w < (t >> 6); ++w) add += wave_tot[w];
+  loff[t] = v - mine + add;
+  cur[t] = 0;
+  __syncthreads();
+  for (uint32_t k = 0; k < kRecodeScalars / kBlock; ++k) {
+    const uint32_t i = blockIdx.x * kRecodeScalars + k * kBlock + t;
+    if (i < n)
+      recode_scalar(scalars[i], i, c, W, [&](unsigned, uint32_t key, uint32_t val) {
+        const uint32_t bin = key & 255;
+        const uint32_t p = loff[bin] + atomicAdd(&cur[bin], 1u);
+        lkeys[p] = key;
+        lvals[p] = val;
+      });
+  }
+  __syncthreads();
+  const uint32_t total = loff[255] + cur[255];
+  for (uint32_t p = t; p < total; p += kBlock) {
+    const uint32_t key = lkeys[p];
+    const uint32_t bin = key & 255;
+    const uint32_t g = base[bin] + (p - loff[bin]);
+    keys[g] = key;
+    vals[g] = lvals[p];
   }
 }
 
@@ -378,17 +465,17 @@ using OnesweepCfg = rocprim::radix_sort_config<
 
 template <class Curve>
 hipError_t MsmGpu<Curve>::sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout,
-                                     const uint32_t* vin, uint32_t* vout, size_t count, unsigned end_bit,
-                                     hipStream_t s) {
+                                     const uint32_t* vin, uint32_t* vout, size_t count, unsigned begin_bit,
+                                     unsigned end_bit, hipStream_t s) {
   switch (sort_bits_) {
     case 10:
-      return rocprim::radix_sort_pairs<OnesweepCfg<10>>(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+      return rocprim::radix_sort_pairs<OnesweepCfg<10>>(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
     case 11:
-      return rocprim::radix_sort_pairs<OnesweepCfg<11>>(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+      return rocprim::radix_sort_pairs<OnesweepCfg<11>>(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
     case 7:
-      return rocprim::radix_sort_pairs<OnesweepCfg<7>>(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+      return rocprim::radix_sort_pairs<OnesweepCfg<7>>(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
     default:
-      return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, count, 0, end_bit, s);
+      return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
   }
 }
 
@@ -439,9 +526,38 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   uint32_t* loff = ctab + 4 * (T + 2);
   uint32_t* dscal = ctab + 5 * (T + 2);  // [0] nchains, [1] max chain length
 
+  unsigned wbits = 0;
+  while ((1u << wbits) < W) ++wbits;
+  const unsigned key_bits = (G == 1) ? c : c + wbits;  // the window bits only matter within a multi-window group
+  // recode fused with the first (low byte) radix pass; one sort group only
+  // (the scatter stages a block's 512 x W entries in LDS: W <= 16 keeps it
+  // within the default 64 KiB of dynamic LDS)
+  const bool fused = fuse_recode_ && G == W && W <= 16;
+  const unsigned sort_begin = fused ? std::min(8u, key_bits) : 0u;
+
   if (profile_) TA_HIP(hipEventRecord(ev_[1], stream_));
-  hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                     W, keys, vals);
+  if (fused) {
+    const uint32_t nblocks = (uint32_t)((n + kRecodeScalars - 1) / kRecodeScalars);
+    const size_t hn = (size_t)256 * nblocks;
+    uint32_t* hist = static_cast<uint32_t*>(hist_.ensure(2 * hn * 4));
+    uint32_t* hoff = hist + hn;
+    hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
+                       W, nblocks, hist);
+    TA_HIP(hipGetLastError());
+    size_t hscan_bytes = 0;
+    TA_HIP(rocprim::exclusive_scan(nullptr, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
+    void* hscan_tmp = hscan_tmp_.ensure(hscan_bytes);
+    TA_HIP(rocprim::exclusive_scan(hscan_tmp, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
+    // the scattered entries are fully sorted when the key has <= 8 bits
+    uint32_t* kdst = sort_begin < key_bits ? keys : keys2;
+    uint32_t* vdst = sort_begin < key_bits ? vals : vals2;
+    const size_t scatter_lds = (size_t)2 * kRecodeScalars * W * sizeof(uint32_t);
+    hipLaunchKernelGGL(recode_scatter_kernel<Fr>, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars,
+                       (uint32_t)n, c, W, nblocks, hist, hoff, kdst, vdst);
+  } else {
+    hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
+                       W, keys, vals);
+  }
   TA_HIP(hipGetLastError());
   // every bucket without an entry stays the identity
   TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * sizeof(Point), stream_));
@@ -450,12 +566,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   if (sort_stream != stream_) TA_HIP(hipStreamWaitEvent(sort_stream, ev_[2], 0));
 
   // ---- per group: radix sort of its (window, bucket, point) entries, then accumulation ----
-  unsigned wbits = 0;
-  while ((1u << wbits) < W) ++wbits;
-  const unsigned key_bits = (G == 1) ? c : c + wbits;  // the window bits only matter within a multi-window group
   const size_t max_group_entries = (size_t)G * n;
   size_t sort_bytes = 0;
-  TA_HIP(sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, max_group_entries, key_bits, sort_stream));
+  TA_HIP(sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, max_group_entries, sort_begin, key_bits,
+                    sort_stream));
   void* sort_tmp = sort_tmp_.ensure(sort_bytes);
   size_t tbase = 0;
   acc_launches_ = ngroups;
@@ -463,8 +577,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     const unsigned w0 = g * G, w1 = std::min(W, w0 + G);
     const size_t e0 = (size_t)w0 * n, ecount = (size_t)(w1 - w0) * n;
     size_t bytes = sort_bytes;
-    TA_HIP(sort_pairs(sort_tmp, bytes, keys + e0, keys2 + e0, vals + e0, vals2 + e0, ecount, key_bits,
-                      sort_stream));
+    if (sort_begin < key_bits)
+      TA_HIP(sort_pairs(sort_tmp, bytes, keys + e0, keys2 + e0, vals + e0, vals2 + e0, ecount, sort_begin, key_bits,
+                        sort_stream));
     if (profile_ && g + 1 == ngroups) TA_HIP(hipEventRecord(ev_[3], sort_stream));  // last sort done
     if (sort_stream != stream_) {
       TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream));
@@ -580,6 +695,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   // bit 6: gather-locality experiment -- every base index masked to 2^20
   // points (a 64 MiB slice that stays in the Infinity Cache); results are wrong
   idx_mask_ = (variant_ & 64) ? ((1u << 20) - 1) : ~kSignBit;
+  fuse_recode_ = !(variant_ & 128);  // bit 7: the separate recode + full sort (A/B)
   static constexpr unsigned kSortBits[] = {0, 10, 11, 7};
   sort_bits_ = kSortBits[(variant_ >> 4) & 3];
   if (plan_out) *plan_out = plan;
