@@ -146,6 +146,8 @@ class MsmGpu {
   unsigned sort_bits_ = 0;
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (experiments only)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
+  uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode
+  bool scatter_lds_set_ = false;
   DeviceBuffer hist_, hscan_tmp_;
   DeviceBuffer maxlen_;
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 }
 
 // Recode fused with the first radix pass (key bits 0..7), in two launches:
-// recode_hist_kernel counts, per block of kRecodeScalars scalars, the entries
+// recode_hist_kernel counts, per block of spt x 256 scalars, the entries
 // of each low-byte bin (LDS atomics) into hist[bin * nblocks + block]; after
 // an exclusive scan of hist, recode_scatter_kernel recomputes the digits and
 // writes every (key, val) to its bin's slot (the rank inside the block's run
@@ -85,17 +85,17 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 // change the bucket's sum -- so it replaces the recode's 8-byte write plus one
 // full onesweep pass (read + write + histogram read) with two reads of the
 // 32-byte scalars and one write.
-constexpr unsigned kRecodeScalars = 2 * kBlock;
+constexpr unsigned kRecodeSpt = 2;  // default scalars per thread of the fused recode
 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restrict__ scalars, uint32_t n, unsigned c,
-                                                             unsigned W, uint32_t nblocks,
+                                                             unsigned W, uint32_t nblocks, uint32_t spt,
                                                              uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[256];
   cnt[threadIdx.x] = 0;
   __syncthreads();
-  for (uint32_t k = 0; k < kRecodeScalars / kBlock; ++k) {
-    const uint32_t i = blockIdx.x * kRecodeScalars + k * kBlock + threadIdx.x;
+  for (uint32_t k = 0; k < spt; ++k) {
+    const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + threadIdx.x;
     if (i < n)
       recode_scalar(scalars[i], i, c, W, [&](unsigned, uint32_t key, uint32_t) { atomicAdd(&cnt[key & 255], 1u); });
   }
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __restrict__ scalars, uint32_t n,
-                                                                unsigned c, unsigned W, uint32_t nblocks,
+                                                                unsigned c, unsigned W, uint32_t nblocks, uint32_t spt,
                                                                 const uint32_t* __restrict__ hist,
                                                                 const uint32_t* __restrict__ off,
                                                                 uint32_t* __restrict__ keys,
@@ -113,8 +113,8 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
   // the block's entries are binned in LDS first, then written out bin run by
   // bin run, so consecutive lanes store to consecutive addresses
   extern __shared__ uint32_t lds_u32[];
-  uint32_t* lkeys = lds_u32;                           // kRecodeScalars * W
-  uint32_t* lvals = lds_u32 + kRecodeScalars * W;      // kRecodeScalars * W
+  uint32_t* lkeys = lds_u32;                      // spt * kBlock * W
+  uint32_t* lvals = lds_u32 + spt * kBlock * W;   // spt * kBlock * W
   __shared__ uint32_t base[256], loff[256], cur[256];
   const uint32_t t = threadIdx.x;
   base[t] = off[(size_t)t * nblocks + blockIdx.x];
@@ -133,8 +133,8 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
   loff[t] = v - mine + add;
   cur[t] = 0;
   __syncthreads();
-  for (uint32_t k = 0; k < kRecodeScalars / kBlock; ++k) {
-    const uint32_t i = blockIdx.x * kRecodeScalars + k * kBlock + t;
+  for (uint32_t k = 0; k < spt; ++k) {
+    const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + t;
     if (i < n)
       recode_scalar(scalars[i], i, c, W, [&](unsigned, uint32_t key, uint32_t val) {
         const uint32_t bin = key & 255;
@@ -530,19 +530,20 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   while ((1u << wbits) < W) ++wbits;
   const unsigned key_bits = (G == 1) ? c : c + wbits;  // the window bits only matter within a multi-window group
   // recode fused with the first (low byte) radix pass; one sort group only
-  // (the scatter stages a block's 512 x W entries in LDS: W <= 16 keeps it
-  // within the default 64 KiB of dynamic LDS)
-  const bool fused = fuse_recode_ && G == W && W <= 16;
+  // (the scatter stages a block's spt x 256 x W entries in LDS, <= 128 KiB)
+  const uint32_t spt = recode_spt_;
+  const size_t scatter_lds = (size_t)2 * spt * kBlock * W * sizeof(uint32_t);
+  const bool fused = fuse_recode_ && G == W && scatter_lds <= 128 * 1024;
   const unsigned sort_begin = fused ? std::min(8u, key_bits) : 0u;
 
   if (profile_) TA_HIP(hipEventRecord(ev_[1], stream_));
   if (fused) {
-    const uint32_t nblocks = (uint32_t)((n + kRecodeScalars - 1) / kRecodeScalars);
+    const uint32_t nblocks = (uint32_t)((n + spt * kBlock - 1) / (spt * kBlock));
     const size_t hn = (size_t)256 * nblocks;
     uint32_t* hist = static_cast<uint32_t*>(hist_.ensure(2 * hn * 4));
     uint32_t* hoff = hist + hn;
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       W, nblocks, hist);
+                       W, nblocks, spt, hist);
     TA_HIP(hipGetLastError());
     size_t hscan_bytes = 0;
     TA_HIP(rocprim::exclusive_scan(nullptr, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
@@ -551,9 +552,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     // the scattered entries are fully sorted when the key has <= 8 bits
     uint32_t* kdst = sort_begin < key_bits ? keys : keys2;
     uint32_t* vdst = sort_begin < key_bits ? vals : vals2;
-    const size_t scatter_lds = (size_t)2 * kRecodeScalars * W * sizeof(uint32_t);
+    if (scatter_lds > 64 * 1024 && !scatter_lds_set_) {
+      TA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&recode_scatter_kernel<Fr>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+      scatter_lds_set_ = true;
+    }
     hipLaunchKernelGGL(recode_scatter_kernel<Fr>, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars,
-                       (uint32_t)n, c, W, nblocks, hist, hoff, kdst, vdst);
+                       (uint32_t)n, c, W, nblocks, spt, hist, hoff, kdst, vdst);
   } else {
     hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
                        W, keys, vals);
@@ -696,6 +701,8 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   // points (a 64 MiB slice that stays in the Infinity Cache); results are wrong
   idx_mask_ = (variant_ & 64) ? ((1u << 20) - 1) : ~kSignBit;
   fuse_recode_ = !(variant_ & 128);  // bit 7: the separate recode + full sort (A/B)
+  static constexpr uint32_t kSpt[] = {kRecodeSpt, 1, 4, 3};
+  recode_spt_ = kSpt[(variant_ >> 8) & 3];  // bits 8-9: scalars per thread of the fused recode
   static constexpr unsigned kSortBits[] = {0, 10, 11, 7};
   sort_bits_ = kSortBits[(variant_ >> 4) & 3];
   if (plan_out) *plan_out = plan;
