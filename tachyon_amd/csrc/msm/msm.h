@@ -148,6 +148,9 @@ class MsmGpu {
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode
   bool scatter_lds_set_ = false;
+  const void* pending_host_bases_ = nullptr;  // host bases still to upload (see enqueue)
+  hipStream_t copy_stream_ = nullptr;
+  hipEvent_t copy_done_ = nullptr;
   DeviceBuffer hist_, hscan_tmp_;
   DeviceBuffer maxlen_;
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket

@@ -438,6 +438,8 @@ MsmGpu<Curve>::~MsmGpu() {
   for (auto* v : {&gev_sorted_, &gev_acc0_, &gev_acc1_})
     for (auto& e : *v) (void)hipEventDestroy(e);
   if (sort_stream_) (void)hipStreamDestroy(sort_stream_);
+  if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
+  if (copy_done_) (void)hipEventDestroy(copy_done_);
   if (h_max_) (void)hipHostFree(h_max_);
   if (own_stream_) (void)hipStreamDestroy(stream_);
 }
@@ -590,6 +592,18 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream));
       TA_HIP(hipStreamWaitEvent(stream_, gev_sorted_[g], 0));
     }
+    if (g == 0 && pending_host_bases_) {
+      // host-resident bases: their upload (the larger of the two) runs on its
+      // own stream while the recode and the sort run; the host call returns
+      // once the pageable copy is staged, i.e. with the GPU busy meanwhile
+      if (!copy_stream_) TA_HIP(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+      if (!copy_done_) TA_HIP(hipEventCreateWithFlags(&copy_done_, hipEventDisableTiming));
+      TA_HIP(hipMemcpyAsync(const_cast<Aff*>(d_bases), pending_host_bases_, n * sizeof(Aff), hipMemcpyHostToDevice,
+                            copy_stream_));
+      TA_HIP(hipEventRecord(copy_done_, copy_stream_));
+      TA_HIP(hipStreamWaitEvent(stream_, copy_done_, 0));
+      pending_host_bases_ = nullptr;
+    }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
     hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2, c,
@@ -711,10 +725,10 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
   const Aff* d_bases = static_cast<const Aff*>(bases);
   const Fr* d_scalars = static_cast<const Fr*>(scalars);
-  if (!is_device_pointer(bases)) {
-    void* p = bases_.ensure(n * sizeof(Aff));
-    TA_HIP(hipMemcpyAsync(p, bases, n * sizeof(Aff), hipMemcpyHostToDevice, stream_));
-    d_bases = static_cast<const Aff*>(p);
+  pending_host_bases_ = nullptr;
+  if (!is_device_pointer(bases)) {  // uploaded inside enqueue(), overlapping the recode and the sort
+    d_bases = static_cast<const Aff*>(bases_.ensure(n * sizeof(Aff)));
+    pending_host_bases_ = bases;
   }
   if (!is_device_pointer(scalars)) {
     void* p = scalars_.ensure(n * sizeof(Fr));
