@@ -280,7 +280,17 @@ TACHYON_C_EXPORT void tachyon_mi355x_ec_op(int curve, int op, const void* a, con
  *          out_a: G1 affine, out_b: G2 affine, out_c: G1 affine (canonical).
  *   witness_map: the h evaluations on the coset (domain_size Fr) to host memory.
  *   last_timings (profiling on): upload, qap, msm_a, msm_b2, msm_b1, msm_l,
- *          msm_h, total -- ms, 8 floats. */
+ *          msm_h, total -- ms, 8 floats.
+ * Multi-GPU split of prove (one process per GPU):
+ *   prove_partials: this rank's shard (contiguous ceil(count / world) chunk
+ *          `rank` of every MSM's points, the kParallelTerm split of
+ *          pippenger_adapter.h:82-113) of the five MSMs, after the full
+ *          witness map; writes partials_size() bytes (an opaque blob of
+ *          XYZZ sums, identical layout on every rank of one build).
+ *          with_b1 != 0 runs the B-in-G1 MSM (required when r != 0).
+ *   assemble: `world` blobs (one per rank, any order, concatenated -- the
+ *          result of one all-gather) -> the proof, as prove() would return.
+ *   prove(full, r, s) == assemble(prove_partials(full, r != 0, 0, 1), 1, r, s). */
 typedef struct tachyon_mi355x_groth16_prover tachyon_mi355x_groth16_prover;
 TACHYON_C_EXPORT tachyon_mi355x_groth16_prover* tachyon_mi355x_groth16_prover_create(const uint8_t* zkey,
                                                                                      size_t len);
@@ -290,6 +300,13 @@ TACHYON_C_EXPORT void tachyon_mi355x_groth16_prover_info(const tachyon_mi355x_gr
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                    size_t count, const void* r, const void* s, void* out_a,
                                                    void* out_b, void* out_c);
+TACHYON_C_EXPORT size_t tachyon_mi355x_groth16_partials_size(const tachyon_mi355x_groth16_prover* prover);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_partials(tachyon_mi355x_groth16_prover* prover, const void* full,
+                                                            size_t count, int with_b1, uint32_t rank,
+                                                            uint32_t world, void* out);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_assemble(tachyon_mi355x_groth16_prover* prover, const void* parts,
+                                                      size_t world, const void* r, const void* s, void* out_a,
+                                                      void* out_b, void* out_c);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                          size_t count, void* out_h);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on);

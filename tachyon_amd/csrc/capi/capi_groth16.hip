@@ -9,6 +9,7 @@
 #include <cstring>
 #include <exception>
 #include <memory>
+#include <type_traits>
 #include <vector>
 
 #include "../groth16/groth16.h"
@@ -36,6 +37,29 @@ template <class P>
 void prove_into(P* p, const void* full, size_t count, const void* r, const void* s, void* a, void* b, void* c) {
   using Fr = typename P::Fr;
   auto proof = p->prove(static_cast<const Fr*>(full), count, static_cast<const Fr*>(r), static_cast<const Fr*>(s));
+  memcpy(a, &proof.a, sizeof(proof.a));
+  memcpy(b, &proof.b, sizeof(proof.b));
+  memcpy(c, &proof.c, sizeof(proof.c));
+}
+
+template <class P>
+using PartialsOf = groth16::ProofPartials<typename std::remove_pointer_t<P>::G1Type,
+                                          typename std::remove_pointer_t<P>::G2Type>;
+
+template <class P>
+void partials_into(P* p, const void* full, size_t count, int with_b1, uint32_t rank, uint32_t world, void* out) {
+  using Fr = typename P::Fr;
+  static_assert(std::is_trivially_copyable_v<PartialsOf<P>>);
+  auto part = p->partials(static_cast<const Fr*>(full), count, with_b1 != 0, rank, world);
+  memcpy(out, &part, sizeof(part));
+}
+
+template <class P>
+void assemble_into(P* p, const void* parts, size_t world, const void* r, const void* s, void* a, void* b, void* c) {
+  using Fr = typename P::Fr;
+  std::vector<PartialsOf<P>> v(world);
+  if (world) memcpy(v.data(), parts, world * sizeof(PartialsOf<P>));
+  auto proof = p->assemble(v.data(), world, static_cast<const Fr*>(r), static_cast<const Fr*>(s));
   memcpy(a, &proof.a, sizeof(proof.a));
   memcpy(b, &proof.b, sizeof(proof.b));
   memcpy(c, &proof.c, sizeof(proof.c));
@@ -109,6 +133,22 @@ void tachyon_mi355x_groth16_prover_info(const tachyon_mi355x_groth16_prover* pro
 void tachyon_mi355x_groth16_prove(tachyon_mi355x_groth16_prover* prover, const void* full, size_t count,
                                   const void* r, const void* s, void* out_a, void* out_b, void* out_c) {
   GUARD_BEGIN PROVER_DISPATCH(prover, prove_into(impl, full, count, r, s, out_a, out_b, out_c)); GUARD_END
+}
+
+size_t tachyon_mi355x_groth16_partials_size(const tachyon_mi355x_groth16_prover* prover) {
+  GUARD_BEGIN
+  PROVER_DISPATCH(prover, return sizeof(PartialsOf<decltype(impl)>));
+  GUARD_END
+}
+
+void tachyon_mi355x_groth16_prove_partials(tachyon_mi355x_groth16_prover* prover, const void* full, size_t count,
+                                           int with_b1, uint32_t rank, uint32_t world, void* out) {
+  GUARD_BEGIN PROVER_DISPATCH(prover, partials_into(impl, full, count, with_b1, rank, world, out)); GUARD_END
+}
+
+void tachyon_mi355x_groth16_assemble(tachyon_mi355x_groth16_prover* prover, const void* parts, size_t world,
+                                     const void* r, const void* s, void* out_a, void* out_b, void* out_c) {
+  GUARD_BEGIN PROVER_DISPATCH(prover, assemble_into(impl, parts, world, r, s, out_a, out_b, out_c)); GUARD_END
 }
 
 void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full, size_t count,

@@ -37,6 +37,20 @@ struct Proof {
   Affine<typename G1::F> c;
 };
 
+// One rank's share of the five MSMs of CreateProofWithAssignment
+// (prove.h:95-146) as XYZZ sums: rank k of `world` takes the contiguous
+// ceil(count / world) chunk k of every MSM's point range (the kParallelTerm
+// split, pippenger_adapter.h:82-113).  The partials of all ranks added
+// together are the single-GPU MSM results, whatever the split.
+template <class G1, class G2>
+struct ProofPartials {
+  uint32_t magic = 0x31363247;  // "G261": layout tag of the C-ABI blob
+  uint32_t with_b1 = 0;         // the B-in-G1 MSM was run (needed when r != 0)
+  uint32_t rank = 0, world = 1;
+  XYZZ<typename G1::F> a, b1, l, h;
+  XYZZ<typename G2::F> b2;
+};
+
 // Per-phase device timings of the last prove (ms), when profiling is on.
 struct ProveTimings {
   float upload = 0, qap = 0, msm_a = 0, msm_b2 = 0, msm_b1 = 0, msm_l = 0, msm_h = 0, total = 0;
@@ -45,6 +59,8 @@ struct ProveTimings {
 template <class G1, class G2>
 class Groth16Prover {
  public:
+  using G1Type = G1;
+  using G2Type = G2;
   using Fr = typename G1::Fr;
   using F1 = typename G1::F;
   using F2 = typename G2::F;
@@ -59,6 +75,14 @@ class Groth16Prover {
   // r, s: the blinding scalars (Montgomery); null = zero (the NoZK proof,
   // prove.h:178-186).  Returns canonical affine points.
   Proof<G1, G2> prove(const Fr* full, size_t count, const Fr* r, const Fr* s);
+
+  // The multi-GPU split of prove(): every rank runs the witness map (it is a
+  // few percent of the proof) and its shard of the five MSMs; the partials of
+  // all ranks are exchanged (one all-gather) and assemble() adds them and
+  // applies r, s and the key's alpha/beta/delta terms on the host.
+  // prove(full, r, s) == assemble({partials(full, r != 0, 0, 1)}, r, s).
+  ProofPartials<G1, G2> partials(const Fr* full, size_t count, bool with_b1, uint32_t rank, uint32_t world);
+  Proof<G1, G2> assemble(const ProofPartials<G1, G2>* parts, size_t world, const Fr* r, const Fr* s) const;
 
   // The witness map alone: h evaluations on the coset (domain_size values,
   // canonical Montgomery) written to `d_h` (device) -- for parity tests.

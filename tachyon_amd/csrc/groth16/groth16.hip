@@ -302,15 +302,15 @@ void Groth16Prover<G1, G2>::witness_map(const Fr* d_full, Fr* d_h) {
 }
 
 template <class G1, class G2>
-Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const Fr* r_ptr, const Fr* s_ptr) {
+ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t count, bool with_b1, uint32_t rank,
+                                                      uint32_t world) {
   using P1 = XYZZ<F1>;
   using P2 = XYZZ<F2>;
   const size_t m = key_.num_vars;
   if (count != m)
     throw std::runtime_error("tachyon_mi355x: Groth16 assignment count " + std::to_string(count) +
                              " != num_vars " + std::to_string(m));
-  const Fr r = r_ptr ? *r_ptr : Fr::zero();
-  const Fr s = s_ptr ? *s_ptr : Fr::zero();
+  if (world == 0 || rank >= world) throw std::runtime_error("tachyon_mi355x: Groth16 shard rank >= world");
   auto t0 = Clock::now();
   const Fr* d_full = full;
   if (!is_device_pointer(full)) {
@@ -329,10 +329,23 @@ Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const F
     timings_.qap = ms_since(t1);
   }
 
+  // this rank's chunk [lo, lo + len) of an MSM over `total` points
+  auto shard = [&](size_t total, size_t* lo) {
+    const size_t chunk = (total + world - 1) / world;
+    *lo = std::min<size_t>((size_t)rank * chunk, total);
+    return std::min(chunk, total - *lo);
+  };
+  ProofPartials<G1, G2> out;
+  out.with_b1 = with_b1 ? 1u : 0u;
+  out.rank = rank;
+  out.world = world;
+
   // MSMs over device-resident bases and scalars (prove.h:95-146)
   const Affine<F1>* a1 = a1_.as<Affine<F1>>();
   const Affine<F1>* b1 = b1_.as<Affine<F1>>();
   const Affine<F2>* b2 = b2_.as<Affine<F2>>();
+  size_t q_lo = 0;  // queries 1 .. m-1 (index 0 is added on the host)
+  const size_t q_len = m > 1 ? shard(m - 1, &q_lo) : 0;
   // The G2 MSM (about 3x the work of a G1 one) runs on its own stream from a
   // second host thread while the G1 MSMs run here; each MSM is synchronous on
   // its host thread (its read-back of the chain lengths).  The witness and h
@@ -343,7 +356,7 @@ Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const F
   std::thread g2_thread([&] {
     try {
       auto tb = Clock::now();
-      if (m > 1) acc_b2 = msm2_->run(b2 + 1, d_full + 1, m - 1);
+      if (q_len) acc_b2 = msm2_->run(b2 + 1 + q_lo, d_full + 1 + q_lo, q_len);
       timings_.msm_b2 = ms_since(tb);
     } catch (...) {
       g2_error = std::current_exception();
@@ -354,21 +367,53 @@ Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const F
     ~Joiner() { if (t.joinable()) t.join(); }
   } joiner{g2_thread};
   auto t2 = Clock::now();
-  P1 acc_a = m > 1 ? msm1_->run(a1 + 1, d_full + 1, m - 1) : P1::zero();
+  out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
   timings_.msm_a = ms_since(t2);
   t2 = Clock::now();
-  P1 acc_b1 = (!r.is_zero() && m > 1) ? msm1_->run(b1 + 1, d_full + 1, m - 1) : P1::zero();
+  out.b1 = (with_b1 && q_len) ? msm1_->run(b1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
   timings_.msm_b1 = ms_since(t2);
   t2 = Clock::now();
-  const size_t nw = key_.num_witness();
-  P1 acc_l = nw ? msm1_->run(c1_.as<Affine<F1>>(), d_full + key_.num_instance(), nw) : P1::zero();
+  size_t l_lo = 0;
+  const size_t l_len = shard(key_.num_witness(), &l_lo);
+  out.l = l_len ? msm1_->run(c1_.as<Affine<F1>>() + l_lo, d_full + key_.num_instance() + l_lo, l_len) : P1::zero();
   timings_.msm_l = ms_since(t2);
   t2 = Clock::now();
   // h_coefficients.size() == h_g1_query.size() == domain size: the else branch of prove.h:103-112
-  P1 acc_h = msm1_->run(h1_.as<Affine<F1>>(), d_h, n_);
+  size_t h_lo = 0;
+  const size_t h_len = shard(n_, &h_lo);
+  out.h = h_len ? msm1_->run(h1_.as<Affine<F1>>() + h_lo, d_h + h_lo, h_len) : P1::zero();
   timings_.msm_h = ms_since(t2);
   g2_thread.join();
   if (g2_error) std::rethrow_exception(g2_error);
+  out.b2 = acc_b2;
+  timings_.total = ms_since(t0);
+  return out;
+}
+
+template <class G1, class G2>
+Proof<G1, G2> Groth16Prover<G1, G2>::assemble(const ProofPartials<G1, G2>* parts, size_t world, const Fr* r_ptr,
+                                              const Fr* s_ptr) const {
+  using P1 = XYZZ<F1>;
+  using P2 = XYZZ<F2>;
+  const Fr r = r_ptr ? *r_ptr : Fr::zero();
+  const Fr s = s_ptr ? *s_ptr : Fr::zero();
+  if (world == 0) throw std::runtime_error("tachyon_mi355x: Groth16 assemble needs at least one partial");
+  P1 acc_a = P1::zero(), acc_b1 = P1::zero(), acc_l = P1::zero(), acc_h = P1::zero();
+  P2 acc_b2 = P2::zero();
+  std::vector<bool> seen(world, false);
+  for (size_t k = 0; k < world; ++k) {
+    const auto& p = parts[k];
+    if (p.magic != ProofPartials<G1, G2>().magic || p.world != world || p.rank >= world || seen[p.rank])
+      throw std::runtime_error("tachyon_mi355x: Groth16 partials are not one rank each of the same world");
+    if (!r.is_zero() && !p.with_b1)
+      throw std::runtime_error("tachyon_mi355x: Groth16 partials lack the B1 MSM that r != 0 needs");
+    seen[p.rank] = true;
+    acc_a = acc_a + p.a;
+    acc_b1 = acc_b1 + p.b1;
+    acc_l = acc_l + p.l;
+    acc_h = acc_h + p.h;
+    acc_b2 = acc_b2 + p.b2;
+  }
 
   // assembly on the host (a handful of point operations)
   auto aff1 = [](const Affine<F1>& a) { return P1::from_affine(a); };
@@ -388,8 +433,17 @@ Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const F
   }
   C = C + acc_l;
   C = C + acc_h;
-  timings_.total = ms_since(t0);
   return Proof<G1, G2>{A.to_affine(), B2.to_affine(), C.to_affine()};
+}
+
+template <class G1, class G2>
+Proof<G1, G2> Groth16Prover<G1, G2>::prove(const Fr* full, size_t count, const Fr* r, const Fr* s) {
+  auto t0 = Clock::now();
+  const bool with_b1 = r && !r->is_zero();
+  const ProofPartials<G1, G2> part = partials(full, count, with_b1, 0, 1);
+  Proof<G1, G2> proof = assemble(&part, 1, r, s);
+  timings_.total = ms_since(t0);
+  return proof;
 }
 
 template class Groth16Prover<Bn254G1, Bn254G2>;

@@ -40,18 +40,26 @@ def _host_collectives(group=None) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
-def all_gather_partials(curve: str, partial: bytes, group=None, device=None) -> bytes:
-    """All-gather every rank's affine partial; returns the concatenation in rank order."""
+def all_gather_bytes(blob: bytes, group=None, device=None) -> bytes:
+    """All-gather one equal-length byte blob per rank; returns the concatenation
+    in rank order (device tensors over RCCL when `device` is given, host
+    tensors under gloo)."""
     import torch
     import torch.distributed as dist
-    pb = CURVE_INFO[curve][0]
     world = dist.get_world_size(group)
-    t = torch.frombuffer(bytearray(partial), dtype=torch.uint8)
+    t = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
     if device is not None and not _host_collectives(group):
         t = t.to(device)
-    out = torch.empty(world * pb, dtype=torch.uint8, device=t.device)
+    out = torch.empty(world * len(blob), dtype=torch.uint8, device=t.device)
     dist.all_gather_into_tensor(out, t, group=group)
     return out.cpu().numpy().tobytes()
+
+
+def all_gather_partials(curve: str, partial: bytes, group=None, device=None) -> bytes:
+    """All-gather every rank's affine partial; returns the concatenation in rank order."""
+    if len(partial) != CURVE_INFO[curve][0]:
+        raise ValueError(f"{curve} partial must be one affine point")
+    return all_gather_bytes(partial, group, device)
 
 
 def sharded_msm(curve: str, local_msm: Callable[[], bytes], group=None, device=None) -> bytes:

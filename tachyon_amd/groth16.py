@@ -87,6 +87,47 @@ class Groth16Prover:
         lib().tachyon_mi355x_groth16_prove(self._h, p, n // 32, rb, sb, a, b, c)
         return a.raw, b.raw, c.raw
 
+    # ---- multi-GPU split (one process per GPU) ----
+    def partials_size(self) -> int:
+        return lib().tachyon_mi355x_groth16_partials_size(self._h)
+
+    def prove_partials(self, full, rank: int, world: int, with_b1: bool = False) -> bytes:
+        """This rank's shard of the five MSMs (after the full witness map) as an
+        opaque blob of partials_size() bytes; with_b1 is required when the
+        proof will be assembled with r != 0."""
+        p, n, keep = _ptr(full)
+        out = ctypes.create_string_buffer(self.partials_size())
+        lib().tachyon_mi355x_groth16_prove_partials(self._h, p, n // 32, 1 if with_b1 else 0, rank, world, out)
+        return out.raw
+
+    def assemble(self, parts: bytes, r: bytes = None, s: bytes = None):
+        """Sum the per-rank partials (concatenated blobs, one per rank) and
+        apply r, s and the key's alpha/beta/delta terms -> (A, B, C)."""
+        size = self.partials_size()
+        if len(parts) % size:
+            raise ValueError("partials blob length is not a multiple of partials_size()")
+        p, n, keep = _ptr(parts)
+        a = ctypes.create_string_buffer(self.g1_bytes)
+        b = ctypes.create_string_buffer(self.g2_bytes)
+        c = ctypes.create_string_buffer(self.g1_bytes)
+        rb = ctypes.create_string_buffer(r, 32) if r is not None else None
+        sb = ctypes.create_string_buffer(s, 32) if s is not None else None
+        lib().tachyon_mi355x_groth16_assemble(self._h, p, len(parts) // size, rb, sb, a, b, c)
+        return a.raw, b.raw, c.raw
+
+    def prove_sharded(self, full, r: bytes = None, s: bytes = None, group=None, device=None):
+        """prove() across the ranks of `group`: every rank runs the witness map
+        and its MSM shard, one all-gather exchanges the partials, every rank
+        assembles the same proof.  World size 1 (or no process group) is prove()."""
+        import torch.distributed as dist
+        from .dist import all_gather_bytes
+        if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+            return self.prove(full, r, s)
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        with_b1 = r is not None and any(r)
+        part = self.prove_partials(full, rank, world, with_b1)
+        return self.assemble(all_gather_bytes(part, group, device), r, s)
+
     def set_profile(self, on: bool):
         lib().tachyon_mi355x_groth16_set_profile(self._h, 1 if on else 0)
 

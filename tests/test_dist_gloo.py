@@ -123,3 +123,32 @@ def test_four_step_layouts_partition():
             for f in (FourStepNtt.input_indices, FourStepNtt.output_indices):
                 idx = np.concatenate([f(log_n, world, r) for r in range(world)])
                 assert sorted(idx.tolist()) == list(range(1 << log_n))
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tachyon_amd import dist as D
+        blob = bytes((rank * 37 + i) & 0xFF for i in range(1000))
+        got = D.all_gather_bytes(blob)
+        if rank == 0:
+            q.put(got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_all_gather_bytes_world3():
+    """The exchange of the multi-GPU Groth16 split (Groth16Prover.prove_sharded):
+    one equal-length opaque blob per rank, concatenated in rank order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == b"".join(bytes((r * 37 + i) & 0xFF for i in range(1000)) for r in range(3))
