@@ -353,8 +353,11 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   TA_HIP(hipStreamSynchronize(stream_));
   P2 acc_b2 = P2::zero();
   std::exception_ptr g2_error;
+  int device = 0;
+  TA_HIP(hipGetDevice(&device));  // a new host thread starts on device 0, not this rank's GPU
   std::thread g2_thread([&] {
     try {
+      TA_HIP(hipSetDevice(device));
       auto tb = Clock::now();
       if (q_len) acc_b2 = msm2_->run(b2 + 1 + q_lo, d_full + 1 + q_lo, q_len);
       timings_.msm_b2 = ms_since(tb);

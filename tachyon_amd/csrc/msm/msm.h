@@ -127,6 +127,7 @@ class MsmGpu {
 
  private:
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
+  Point run_host_pipelined(const void* bases, const void* scalars, size_t n, size_t chunks);
   void ensure_group_events(unsigned groups);
   hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
                         uint32_t* vout, size_t count, unsigned begin_bit, unsigned end_bit, hipStream_t s);
@@ -151,6 +152,7 @@ class MsmGpu {
   const void* pending_host_bases_ = nullptr;  // host bases still to upload (see enqueue)
   hipStream_t copy_stream_ = nullptr;
   hipEvent_t copy_done_ = nullptr;
+  std::vector<hipEvent_t> chunk_ev_;  // host-resident pipeline: chunk k uploaded
   DeviceBuffer hist_, hscan_tmp_;
   DeviceBuffer maxlen_;
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket

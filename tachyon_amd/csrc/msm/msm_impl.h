@@ -12,6 +12,11 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <cstdlib>
+#include <exception>
+#include <mutex>
+#include <thread>
 
 namespace tachyon_amd::msm {
 
@@ -440,6 +445,7 @@ MsmGpu<Curve>::~MsmGpu() {
   if (sort_stream_) (void)hipStreamDestroy(sort_stream_);
   if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   if (copy_done_) (void)hipEventDestroy(copy_done_);
+  for (auto e : chunk_ev_) (void)hipEventDestroy(e);
   if (h_max_) (void)hipHostFree(h_max_);
   if (own_stream_) (void)hipStreamDestroy(stream_);
 }
@@ -772,8 +778,100 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::combine_windows(const std::vector<P
   return total;
 }
 
+// Host-resident inputs of >= 2^24 points: the upload, not the GPU, is the
+// bound (≈6.4 GB at ≈54 GB/s for 2^26 BN254 G1 against ≈95 ms of kernels),
+// and the accumulation of a window needs every base, so a single MSM cannot
+// start before the last byte arrives.  Split the points into chunks of
+// ≥ 2^22 (the kParallelTerm decomposition, pippenger_adapter.h:82-113): a
+// copy thread queues every chunk's H2D on copy_stream_ (recording one event
+// per chunk) while this thread runs the MSM of chunk k as soon as its event
+// is recorded, so the kernels of chunk k overlap the upload of k+1..; the
+// chunk results are added on the host.  TACHYON_MSM_HOST_CHUNKS overrides
+// the chunk count (1 = one MSM after one upload).  msm_benchmark_gpu sweep
+// (host-resident, s): 2^26 chunks 1/4/6/8/12/16 -> 0.193/0.142/0.143/0.136/
+// 0.140/0.140; 2^24 1/2/3/4/8 -> 0.053/0.046/0.043/0.042/0.043; 2^22 stays
+// whole (1/3/4 -> 0.015/0.021/0.018: the per-chunk reduction dominates).
+inline size_t host_chunk_count(size_t n) {
+  if (const char* e = getenv("TACHYON_MSM_HOST_CHUNKS")) return std::clamp<size_t>(atoi(e), 1, 64);
+  if (n < (size_t(1) << 24)) return 1;
+  return std::min<size_t>(8, n >> 22);
+}
+
+template <class Curve>
+typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_host_pipelined(const void* bases, const void* scalars, size_t n,
+                                                                size_t chunks) {
+  const bool host_b = !is_device_pointer(bases), host_s = !is_device_pointer(scalars);
+  Aff* d_b = host_b ? static_cast<Aff*>(bases_.ensure(n * sizeof(Aff))) : const_cast<Aff*>(static_cast<const Aff*>(bases));
+  Fr* d_s = host_s ? static_cast<Fr*>(scalars_.ensure(n * sizeof(Fr))) : const_cast<Fr*>(static_cast<const Fr*>(scalars));
+  if (!copy_stream_) TA_HIP(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+  while (chunk_ev_.size() < chunks) {
+    hipEvent_t e;
+    TA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    chunk_ev_.push_back(e);
+  }
+  const size_t step = (n + chunks - 1) / chunks;
+  int device = 0;
+  TA_HIP(hipGetDevice(&device));
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t ready = 0;  // chunks whose copies and event are queued
+  bool failed = false;
+  std::exception_ptr copy_error;
+  std::thread copier([&] {
+    try {
+      TA_HIP(hipSetDevice(device));
+      for (size_t k = 0; k < chunks; ++k) {
+        const size_t lo = std::min(n, k * step), len = std::min(step, n - lo);
+        if (host_b && len)
+          TA_HIP(hipMemcpyAsync(d_b + lo, static_cast<const Aff*>(bases) + lo, len * sizeof(Aff),
+                                hipMemcpyHostToDevice, copy_stream_));
+        if (host_s && len)
+          TA_HIP(hipMemcpyAsync(d_s + lo, static_cast<const Fr*>(scalars) + lo, len * sizeof(Fr),
+                                hipMemcpyHostToDevice, copy_stream_));
+        TA_HIP(hipEventRecord(chunk_ev_[k], copy_stream_));
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          ready = k + 1;
+        }
+        cv.notify_all();
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      copy_error = std::current_exception();
+      failed = true;
+      cv.notify_all();
+    }
+  });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() { if (t.joinable()) t.join(); }
+  } joiner{copier};
+  Point total = Point::zero();
+  std::vector<Point> ws;
+  MsmPlan plan;
+  for (size_t k = 0; k < chunks; ++k) {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return ready > k || failed; });
+      if (failed) break;
+    }
+    const size_t lo = std::min(n, k * step), len = std::min(step, n - lo);
+    if (!len) continue;
+    TA_HIP(hipStreamWaitEvent(stream_, chunk_ev_[k], 0));
+    run_windows(d_b + lo, d_s + lo, len, &ws, &plan);
+    total = total + combine_windows(ws, plan.c);
+  }
+  copier.join();
+  if (copy_error) std::rethrow_exception(copy_error);
+  return total;
+}
+
 template <class Curve>
 typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* scalars, size_t n) {
+  if (n && (!is_device_pointer(bases) || !is_device_pointer(scalars))) {
+    const size_t chunks = host_chunk_count(n);
+    if (chunks > 1) return run_host_pipelined(bases, scalars, n, chunks);
+  }
   std::vector<Point> ws;
   MsmPlan plan;
   run_windows(bases, scalars, n, &ws, &plan);

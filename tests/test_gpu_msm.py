@@ -151,3 +151,28 @@ def test_device_resident_inputs_and_shard_sum():
     assert M.affine_sum("bn254_g1", a + b) == whole
     hb, hs = d_b.cpu().numpy(), d_s.cpu().numpy()
     assert O.msm_np("bn254_g1", hb, hs) == whole
+
+
+@pytest.mark.parametrize("chunks,mixed", [(3, None), (8, "bases"), (5, "scalars")])
+def test_host_pipelined_upload(chunks, mixed, monkeypatch):
+    """Host-resident inputs run as chunked MSMs overlapping the per-chunk
+    uploads (MsmGpu::run_host_pipelined); the sum must equal the one-shot
+    device-resident MSM -- also with only one operand on the host and an
+    uneven split (TACHYON_MSM_HOST_CHUNKS forces the chunking at 2^18)."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    n = (1 << 18) + 77
+    d_b = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    M.gen_bases("bn254_g1", 8, n, 512, d_b.data_ptr())
+    M.gen_scalars("bn254_fr", 8, n, d_s.data_ptr())
+    torch.cuda.synchronize()
+    m = ctx("bn254_g1")
+    whole = m.run(d_b, d_s)
+    hb, hs = d_b.cpu().numpy(), d_s.cpu().numpy()
+    monkeypatch.setenv("TACHYON_MSM_HOST_CHUNKS", str(chunks))
+    b = d_b if mixed == "scalars" else hb
+    s = d_s if mixed == "bases" else hs
+    assert m.run(b, s) == whole
+    monkeypatch.setenv("TACHYON_MSM_HOST_CHUNKS", "1")
+    assert m.run(hb, hs) == whole
