@@ -239,8 +239,14 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, i
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule) */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
- * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total, 0 (8 floats) */
+ * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total,
+ * accumulation launches (8 floats; of the last point chunk when the run was divided) */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8);
+/* Point chunks the last run was split into: > 1 when the working set did not
+ * fit the free device memory (DetermineMsmDivisionsForMemory,
+ * icicle_msm_utils.cc:10-68; TACHYON_MSM_MEM_LIMIT caps the free bytes) or when
+ * host-resident inputs were uploaded chunk by chunk under the kernels. */
+TACHYON_C_EXPORT size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx);
 /* window bits / windows the planner picks for `size` points */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows);
 /* Host-side group arithmetic on affine points (multi-GPU partial sums):

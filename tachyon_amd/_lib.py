@@ -98,6 +98,7 @@ SIGNATURES = [
     ("tachyon_mi355x_msm_gpu_set_window_bits", None, [i32, vp, ctypes.c_uint]),
     ("tachyon_mi355x_msm_gpu_set_profile", None, [i32, vp, i32]),
     ("tachyon_mi355x_msm_gpu_set_variant", None, [i32, vp, i32]),
+    ("tachyon_mi355x_msm_gpu_last_divisions", sz, [i32, vp]),
     ("tachyon_mi355x_msm_gpu_last_timings", None, [i32, vp, fp]),
     ("tachyon_mi355x_msm_plan", None, [i32, sz, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]),
     ("tachyon_mi355x_affine_sum", None, [i32, vp, sz, vp]),

@@ -314,6 +314,10 @@ void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8
     out8[6] = t.total; out8[7] = t.acc_launches;
   }) GUARD_END
 }
+size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.last_divisions()) GUARD_END
+  return 0;
+}
 void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows) {
   GUARD_BEGIN CURVE_DISPATCH(curve, {
     msm::MsmPlan p = msm::MsmPlan::make(size, C::Fr::Config::kModulusBits);

@@ -124,10 +124,16 @@ class MsmGpu {
   const MsmTimings& timings() const { return timings_; }
   hipStream_t stream() const { return stream_; }
   unsigned last_levels() const { return last_levels_; }
+  // number of point chunks the last run() was split into for device memory
+  // (DetermineMsmDivisionsForMemory) or for the host-upload pipeline
+  size_t last_divisions() const { return last_divisions_; }
 
  private:
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
   Point run_host_pipelined(const void* bases, const void* scalars, size_t n, size_t chunks);
+  size_t work_bytes(size_t n) const;
+  size_t held_bytes() const;
+  size_t memory_divisions(size_t n, size_t resident_bytes) const;
   void ensure_group_events(unsigned groups);
   hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
                         uint32_t* vout, size_t count, unsigned begin_bit, unsigned end_bit, hipStream_t s);
@@ -157,6 +163,7 @@ class MsmGpu {
   DeviceBuffer maxlen_;
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;
+  size_t last_divisions_ = 1;
 };
 
 extern template class MsmGpu<Bn254G1>;

@@ -866,17 +866,92 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_host_pipelined(const void* base
   return total;
 }
 
+// Device bytes of the working buffers enqueue() grows for an n-point MSM
+// (keys/values and their sort double buffers, sort scratch, accumulation
+// pieces and chain tables, bucket and segment sums), plus 10 %.
+template <class Curve>
+size_t MsmGpu<Curve>::work_bytes(size_t n) const {
+  const MsmPlan p = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_);
+  const size_t entries = n * p.windows;
+  const size_t T = (entries + p.K - 1) / p.K;
+  size_t bytes = entries * 16 + entries / 2;                 // keys, vals (x2) + onesweep scratch
+  bytes += (2 * T + 2 * T / p.K2 + T + 2) * sizeof(Point);   // pieces + first join level
+  bytes += (T + 2) * 4 * 9;                                  // flags, last bucket, chain tables
+  bytes += (size_t)p.windows * p.buckets * sizeof(Point);    // bucket sums
+  bytes += 2 * (size_t)p.windows * (p.buckets / p.seg) * sizeof(Point);
+  return bytes + bytes / 10;
+}
+
+template <class Curve>
+size_t MsmGpu<Curve>::held_bytes() const {
+  const DeviceBuffer* bufs[] = {&keys_,  &vals_,  &keys2_, &vals2_, &sort_tmp_, &scan_tmp_, &start_, &end_,
+                                &cnt_,   &off_a_, &off_b_, &part_a_, &part_b_,  &seg_a_,    &seg_b_, &buckets_,
+                                &hist_, &hscan_tmp_};
+  size_t s = 0;
+  for (const DeviceBuffer* b : bufs) s += b->capacity();
+  return s;
+}
+
+// Point chunks an n-point MSM runs in so that its working set fits the
+// device: the analogue of DetermineMsmDivisionsForMemory
+// (icicle_msm_utils.cc:10-68; halve the chunk until the estimate is below the
+// free memory) for this backend's buffers.  `resident_bytes`: what the call
+// itself must keep on the device for all chunks (uploaded host inputs).
+// Free memory = hipMemGetInfo + the buffers this context already holds
+// (they are reused); TACHYON_MSM_MEM_LIMIT (bytes) caps it for tests.
+template <class Curve>
+size_t MsmGpu<Curve>::memory_divisions(size_t n, size_t resident_bytes) const {
+  size_t free_b = 0, total_b = 0;
+  TA_HIP(hipMemGetInfo(&free_b, &total_b));
+  size_t avail = free_b + held_bytes();
+  if (const char* e = getenv("TACHYON_MSM_MEM_LIMIT")) avail = std::min<size_t>(avail, strtoull(e, nullptr, 10));
+  avail = avail / 10 * 9;
+  size_t d = 1;
+  while (resident_bytes + work_bytes((n + d - 1) / d) > avail) {
+    if ((n + d - 1) / d <= (size_t(1) << 16))
+      throw std::runtime_error("tachyon_mi355x: not enough device memory for the MSM (need " +
+                               std::to_string(resident_bytes + work_bytes((n + d - 1) / d)) + " B, have " +
+                               std::to_string(avail) + " B)");
+    d *= 2;
+  }
+  return d;
+}
+
 template <class Curve>
 typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* scalars, size_t n) {
-  if (n && (!is_device_pointer(bases) || !is_device_pointer(scalars))) {
-    const size_t chunks = host_chunk_count(n);
-    if (chunks > 1) return run_host_pipelined(bases, scalars, n, chunks);
+  last_divisions_ = 1;
+  if (n == 0) {
+    std::vector<Point> ws;
+    run_windows(bases, scalars, n, &ws, nullptr);
+    return Point::zero();
+  }
+  const bool host_b = !is_device_pointer(bases), host_s = !is_device_pointer(scalars);
+  const size_t resident = (host_b ? n * sizeof(Aff) : 0) + (host_s ? n * sizeof(Fr) : 0);
+  const size_t divisions = memory_divisions(n, resident);
+  if (host_b || host_s) {
+    const size_t chunks = std::max(host_chunk_count(n), divisions);
+    if (chunks > 1) {
+      last_divisions_ = chunks;
+      return run_host_pipelined(bases, scalars, n, chunks);
+    }
   }
   std::vector<Point> ws;
   MsmPlan plan;
-  run_windows(bases, scalars, n, &ws, &plan);
-  if (n == 0) return Point::zero();
-  return combine_windows(ws, plan.c);
+  if (divisions == 1) {
+    run_windows(bases, scalars, n, &ws, &plan);
+    return combine_windows(ws, plan.c);
+  }
+  // device-resident inputs larger than the working memory: consecutive point
+  // chunks, results added (the kParallelTerm sum, pippenger_adapter.h:82-113)
+  last_divisions_ = divisions;
+  const size_t step = (n + divisions - 1) / divisions;
+  Point total = Point::zero();
+  for (size_t lo = 0; lo < n; lo += step) {
+    const size_t len = std::min(step, n - lo);
+    run_windows(static_cast<const Aff*>(bases) + lo, static_cast<const Fr*>(scalars) + lo, len, &ws, &plan);
+    total = total + combine_windows(ws, plan.c);
+  }
+  return total;
 }
 
 }  // namespace tachyon_amd::msm

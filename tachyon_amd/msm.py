@@ -102,6 +102,10 @@ class VariableBaseMSMGpu:
     def set_variant(self, variant: int):
         lib().tachyon_mi355x_msm_gpu_set_variant(self.curve_id, self._ctx, variant)
 
+    def last_divisions(self) -> int:
+        """Point chunks the last run was split into (device memory or host-upload pipeline)."""
+        return lib().tachyon_mi355x_msm_gpu_last_divisions(self.curve_id, self._ctx)
+
     def last_timings(self) -> dict:
         out = (ctypes.c_float * 8)()
         lib().tachyon_mi355x_msm_gpu_last_timings(self.curve_id, self._ctx, out)

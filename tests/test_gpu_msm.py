@@ -176,3 +176,30 @@ def test_host_pipelined_upload(chunks, mixed, monkeypatch):
     assert m.run(b, s) == whole
     monkeypatch.setenv("TACHYON_MSM_HOST_CHUNKS", "1")
     assert m.run(hb, hs) == whole
+
+
+def test_memory_divisions(monkeypatch):
+    """DetermineMsmDivisionsForMemory (icicle_msm_utils.cc:10-68): with the free
+    device memory capped below the working set of one MSM, the run is split
+    into point chunks whose sum equals the undivided result (device- and
+    host-resident inputs)."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    n = 1 << 19
+    d_b = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    M.gen_bases("bn254_g1", 12, n, 512, d_b.data_ptr())
+    M.gen_scalars("bn254_fr", 12, n, d_s.data_ptr())
+    torch.cuda.synchronize()
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    m = VariableBaseMSMGpu("bn254_g1")  # fresh context: no buffers held yet
+    whole = ctx("bn254_g1").run(d_b, d_s)
+    # the 2^19 working set is ~0.7 GB (MsmGpu::work_bytes); 400 MB -> 2^17-point chunks
+    monkeypatch.setenv("TACHYON_MSM_MEM_LIMIT", str(400 << 20))
+    assert m.run(d_b, d_s) == whole
+    assert m.last_divisions() >= 2
+    monkeypatch.setenv("TACHYON_MSM_HOST_CHUNKS", "1")
+    monkeypatch.setenv("TACHYON_MSM_MEM_LIMIT", str(560 << 20))
+    assert m.run(d_b.cpu().numpy(), d_s.cpu().numpy()) == whole
+    assert m.last_divisions() >= 2
+    m.close()
