@@ -58,3 +58,22 @@ def test_ntt_sweep_vs_oracle(logn):
     assert np.array_equal(evals, expect)
     O.fft_np(expect, inverse=True)
     assert np.array_equal(back, expect) and np.array_equal(back, coeffs)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("curve,pb", [("bls12_381_g1", 96), ("bls12_381_g2", 192)])
+def test_bls_shard_vs_oracle(curve, pb):
+    """BASELINE configs[3] (BLS12-381 G1 + G2 MSM 2^24 over 8 GPUs): one
+    rank's 2^21-point shard of the bench's input equals the oracle."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    n = 1 << 21
+    d_b = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
+    d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    M.gen_bases(curve, SEED, n, 1 << 10, d_b.data_ptr())
+    M.gen_scalars("bls12_381_fr", SEED, n, d_s.data_ptr())
+    torch.cuda.synchronize()
+    m = M.VariableBaseMSMGpu(curve)
+    got = m.run(d_b, d_s)
+    m.close()
+    assert O.msm_np(curve, d_b.cpu().numpy(), d_s.cpu().numpy()) == got
