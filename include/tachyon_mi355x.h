@@ -184,6 +184,13 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_offs
  * consecutive arrays of size() elements. */
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(
     tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_fr* d_data, int inverse);
+/* Host-resident in-place transform (IcicleNTT<bn254::Fr>::Run on a host
+ * pointer, icicle_ntt.h:53-142 / icicle_ntt_bn254.cc:31-116: natural order in
+ * and out, the domain's coset offset): inout holds exactly size() Montgomery
+ * elements; synchronous.  The C++ hook over it is
+ * include/tachyon_mi355x_ntt_holder.h (IcicleNTTHolder's shape). */
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_host(
+    tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_fr* inout, size_t len, int inverse);
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device(
     tachyon_bn254_univariate_evaluation_domain* domain, tachyon_bn254_fr* d_data, size_t batch, int inverse);
 TACHYON_C_EXPORT void* tachyon_mi355x_bn254_univariate_evaluation_domain_stream(

@@ -79,6 +79,7 @@ SIGNATURES = [
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_group_gen", None, [vp, vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset", None, [vp, vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device", None, [vp, vp, i32]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_transform_host", None, [vp, vp, sz, i32]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device", None, [vp, vp, sz, i32]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_stream", vp, [vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile", None, [vp, i32]),

@@ -543,6 +543,18 @@ void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(tachyon_
   else d->impl->forward_device(reinterpret_cast<Bn254Fr*>(d_data));
   GUARD_END
 }
+void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_host(tachyon_bn254_univariate_evaluation_domain* d,
+                                                                      tachyon_bn254_fr* inout, size_t len,
+                                                                      int inverse) {
+  GUARD_BEGIN
+  if (len != d->impl->size())
+    throw std::runtime_error("transform_host: the vector must hold exactly size() elements (" + std::to_string(len) +
+                             " != " + std::to_string(d->impl->size()) + ")");
+  auto* v = reinterpret_cast<Bn254Fr*>(inout);
+  if (inverse) d->impl->inverse_host(v, len, v);
+  else d->impl->forward_host(v, len, v);
+  GUARD_END
+}
 void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device(
     tachyon_bn254_univariate_evaluation_domain* d, tachyon_bn254_fr* d_data, size_t batch, int inverse) {
   GUARD_BEGIN

@@ -96,6 +96,18 @@ class Radix2EvaluationDomain:
         runs on self.stream)."""
         lib().tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(self._d, d_ptr, 1 if inverse else 0)
 
+    def transform_host(self, buf, inverse: bool = False):
+        """IcicleNTT::Run semantics (icicle_ntt.h:53-142): in place on a writable
+        host buffer (ctypes buffer / numpy array) of exactly `size` Montgomery
+        elements, natural order, on the domain's coset; synchronous."""
+        import numpy as np
+        if isinstance(buf, np.ndarray):
+            ptr, nbytes = buf.ctypes.data, buf.nbytes
+        else:
+            ptr, nbytes = ctypes.addressof(buf), ctypes.sizeof(buf)
+        lib().tachyon_mi355x_bn254_univariate_evaluation_domain_transform_host(self._d, ptr, nbytes // 32,
+                                                                              1 if inverse else 0)
+
     @property
     def stream(self) -> int:
         return lib().tachyon_mi355x_bn254_univariate_evaluation_domain_stream(self._d)

@@ -65,3 +65,18 @@ def test_no_oracle_in_product():
                 assert not bad.search(text), f
     out = subprocess.run(["nm", "-D", LIB], capture_output=True, text=True).stdout if os.path.exists(LIB) else ""
     assert "oracle_" not in out
+
+
+def test_ntt_holder_header_compiles(tmp_path):
+    """include/tachyon_mi355x_ntt_holder.h (the IcicleNTTHolder-shaped C++ hook)
+    is self-contained C++17 over the C-ABI header, usable with any 32-byte
+    Montgomery element type (bn254::Fr in a Tachyon build)."""
+    src = tmp_path / "use_holder.cc"
+    src.write_text('#include "tachyon_mi355x_ntt_holder.h"\n'
+                   "struct Fr { unsigned long long limbs[4]; };\n"
+                   "bool f(std::vector<Fr>& v, const Fr* h) {\n"
+                   "  auto holder = tachyon_mi355x::NTTHolder::Create(v.size());\n"
+                   "  return holder->FFT(v, h) && holder->IFFT(v);\n}\n")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

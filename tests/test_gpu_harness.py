@@ -73,3 +73,20 @@ def test_msm_dump_and_replay(tmp_path):
                          env={k: v for k, v in os.environ.items() if k != "TACHYON_MSM_GPU_INPUT_DIR"}).stdout
     got = [l for l in out.splitlines() if l.startswith("(")]
     assert got == expect
+
+
+@pytest.mark.parametrize("log_n", [1, 10, 16])
+def test_ntt_holder_cpp_hook(tmp_path, log_n):
+    """include/tachyon_mi355x_ntt_holder.h (the IcicleNTTHolder-shaped C++
+    hook): in-place host FFT/IFFT, plain and on the coset 5<w>, from a C++
+    client; its outputs equal the CPU oracle's transforms."""
+    from oracle import oracle as O
+    dump = tmp_path / "ntt.bin"
+    _, res = run(["ntt_holder_check", str(log_n), "--dump", str(dump)])
+    assert all(res[k] for k in ("fft_matches_capi", "round_trip", "coset_differs", "coset_round_trip")), res
+    n = 1 << log_n
+    raw = dump.read_bytes()
+    inp, fft, coset = raw[:n * 32], raw[n * 32:2 * n * 32], raw[2 * n * 32:]
+    five = O.field_op("bn254_fr", "to_mont", (5).to_bytes(32, "little"))
+    assert fft == O.fft(inp, n)
+    assert coset == O.fft(inp, n, five)

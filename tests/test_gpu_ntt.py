@@ -152,3 +152,23 @@ def test_batched_transform_device():
         e = v[b].copy()
         O.fft_np(e)
         assert got[b].tobytes() == e.tobytes(), b
+
+
+def test_transform_host_in_place():
+    """tachyon_mi355x_..._transform_host: IcicleNTT::Run semantics (in place on
+    a host vector of size() elements, natural order, the domain's coset)."""
+    import ctypes
+    n = 1 << 11
+    coeffs = O.gen_scalars("bn254_fr", 77, n).tobytes()
+    d = domain(n)
+    buf = ctypes.create_string_buffer(coeffs, n * 32)
+    d.transform_host(buf)
+    assert buf.raw == O.fft(coeffs, n)
+    d.transform_host(buf, inverse=True)
+    assert buf.raw == coeffs
+    five = O.field_op("bn254_fr", "to_mont", (5).to_bytes(32, "little"))
+    d.set_offset(five)
+    arr = np.frombuffer(coeffs, dtype=np.uint64).copy()
+    d.transform_host(arr)
+    assert arr.tobytes() == O.fft(coeffs, n, five)
+    d.close()
