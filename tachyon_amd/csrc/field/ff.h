@@ -145,6 +145,28 @@ struct Fp {
   }
   TA_HD Fp dbl() const { return *this + *this; }
 
+  // a - b + 2p without the borrow test: in [0, 4p) for lazy a, b.  Only as
+  // the left factor of a product whose other factor is canonical (< p): the
+  // lazy product is then (x y + m p) / R < 4p^2/R + p < 2p since 4p < R.
+  TA_HD Fp sub_unreduced(const Fp& o) const {
+    if constexpr (!kLazy) {
+      return *this - o;
+    } else {
+      Fp r;
+#if defined(__HIP_DEVICE_COMPILE__) && TA_FIELD_ASM
+      if constexpr (N == 8) { detail::sub_unreduced_8<Cfg, true>(r.v, v, o.v); return r; }
+      else if constexpr (N == 12) { detail::sub_unreduced_12<Cfg, true>(r.v, v, o.v); return r; }
+#endif
+      uint32_t br = 0;
+#pragma unroll
+      for (int i = 0; i < N; ++i) r.v[i] = subb(v[i], o.v[i], br, &br);
+      uint32_t c = 0;  // the borrow of a - b cancels against the carry of + 2p
+#pragma unroll
+      for (int i = 0; i < N; ++i) r.v[i] = addc(r.v[i], Cfg::kP232[i], c, &c);
+      return r;
+    }
+  }
+
   // prime_field_fallback.h:234-251 (Sub: add p back on borrow); lazy: add 2p
   TA_HD Fp operator-(const Fp& o) const {
     Fp r;
@@ -306,6 +328,7 @@ struct HotFp : F {
   TA_HD HotFp operator+(const HotFp& o) const { return F::operator+(o); }
   TA_HD HotFp operator-(const HotFp& o) const { return F::operator-(o); }
   TA_HD HotFp operator-() const { return F::operator-(); }
+  TA_HD HotFp sub_unreduced(const HotFp& o) const { return F::sub_unreduced(o); }
   TA_HD HotFp operator*(const HotFp& o) const { return F::mul_inline(o); }
   TA_HD HotFp dbl() const { return F::dbl(); }
   TA_HD HotFp sqr() const { return F::mul_inline(*this); }

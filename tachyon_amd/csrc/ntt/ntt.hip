@@ -80,10 +80,11 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __res
           // (a0 and the set base are multiples of 2^R), known at compile time;
           // index 0 is w = 1 -- the whole last stage and half the one before
           const uint32_t idx = (uint32_t)j & ((1u << (R - 1 - u)) - 1);
-          x[j + half] = idx ? (lo - hi) * tws[idx] : (lo - hi);
+          x[j + half] = idx ? lo.sub_unreduced(hi) * tws[idx] : (lo - hi);
         } else {
+          // twiddles are canonical, so lo - hi + 2p needs no borrow test
           const Fr w = tws[index(a0 + ((uint32_t)j << qlog), m) & gap_mask];
-          x[j + half] = (lo - hi) * w;
+          x[j + half] = lo.sub_unreduced(hi) * w;
         }
       }
     }
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void twiddle_base_kernel(Fr* __restrict__ t
                                                               uint32_t bits) {
   uint32_t j = blockIdx.x * kBlock + threadIdx.x;
   if (j >= count) return;
-  t0[j] = lo[j & ((1u << bits) - 1)] * hi[j >> bits];
+  t0[j] = (lo[j & ((1u << bits) - 1)] * hi[j >> bits]).canonical();  // canonical: see radix_step
 }
 
 // T_s[j] = T_0[j << s]  (the strided sub-sampling of radix2_twiddle_cache.h:105-117)

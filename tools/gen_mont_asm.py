@@ -228,6 +228,22 @@ def gen_addsub(N):
                + asm_block(L, r_out + t_out + sb_out, a_in + b_in + m_in) + "#else\n  (void)sb;\n"
                + asm_block(L1, r_out + t_out, a_in + b_in + m_in) + "#endif\n}\n")
 
+    # ---- sub_unreduced: r = a - b + M (mod 2^32N), no borrow test: the a - b
+    # chain on VCC, + M one step behind on %[sb]; the final borrow and carry
+    # cancel.  ff.h's Fp::sub_unreduced (M = 2p, lazy a, b < 2p, so r < 4p)
+    # feeds the result straight into a product with a canonical factor
+    def unr_b(i):
+        return ("v_add_co_u32_e64 %[r0], %[sb], %[r0], %[t0]" if i == 0
+                else f"v_addc_co_u32_e64 %[r{i}], %[sb], %[r{i}], %[t{i}], %[sb]")
+    L = interleave_select(N, sub_a, unr_b, [])
+    assert L[-1] == "s_nop 1"
+    L = L[:-1]  # nothing reads the last carry
+    out.append(f"// r = a - b + M (mod 2^{32 * N}) without the borrow test\n"
+               f"template <class Cfg, bool k2p>\n"
+               f"__device__ __forceinline__ void sub_unreduced_{N}(uint32_t* r, const uint32_t* a, const uint32_t* b) {{\n"
+               f"  uint32_t t[{N}];\n  uint64_t sb;\n"
+               + asm_block(L, r_out + t_out + sb_out, a_in + b_in + m_in) + "}\n")
+
     # ---- cond_sub: r = r >= M ? r - M : r  (in place; off the hot path)
     rio = [f'[r{i}] "+v"(r[{i}])' for i in range(N)]
     L = [f"v_mov_b32 %[t{i}], %[m{i}]" for i in range(1, N)]
