@@ -64,9 +64,17 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
   // and the accumulation slow each other down by about the time they
   // overlap.  set_variant bits 2-3 keep it for experiments.)
   p.group = p.windows;
-  // entries per accumulation thread: ~2^20 threads, K in [8, 256]
-  // (2^26 sweep: K = 128/256/512/1024 -> 99.9/98.9/99.1/99.3 ms)
-  size_t k = entries >> 20;
+  // entries per accumulation thread: ~2^18 threads with K in [16, 64] below
+  // 2^26 entries, then 128, and 256 from 2^29 entries.  Longer runs per
+  // thread leave fewer bucket pieces for the chain join, which dominates the
+  // small sizes (tools/tune_msm.py; old rule K = entries/2^20 at 1x/2x/4x, ms:
+  // 2^18 1.63/1.59/1.66, 2^19 2.14/2.08/2.10, 2^20 2.94/2.89/2.77,
+  // 2^21 4.72/4.71/4.66, 2^22 8.14/8.10/8.24; one box, K = 128 vs 64: 2^20
+  // 2.88 (K 64) vs 2.94 (K 32), 2^22 8.87 vs 8.57, 2^23 15.56 vs 15.77;
+  // 2^26: K = 128/256/512/1024 -> 99.9/98.9/99.1/99.3)
+  size_t k = entries >= (size_t(1) << 29)   ? 256
+             : entries >= (size_t(1) << 26) ? 128
+                                            : std::clamp<size_t>(entries >> 18, 16, 64);
   if (p.group == 1) k = n >> 18;  // ~1024 workgroups per window launch
   p.K = (unsigned)std::clamp<size_t>(k, 8, 256);
   p.K2 = 16;  // (binary levels measured slower here: more launches and level traffic)
