@@ -60,15 +60,33 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __res
     const uint32_t rr = g >> log_m;
     const uint32_t off = rr & ((1u << qlog) - 1);
     const uint32_t a0 = ((rr >> qlog) << (qlog + R)) + off;
+    // the step's twiddles first: their global loads overlap the LDS reads
+    // and the first butterflies instead of stalling each product
+    Fr wv[R][E / 2];
+    if constexpr (!kLast) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const uint32_t st = a.s0 + t + u;
+        const uint32_t gap_mask = (1u << (a.L - st - 1)) - 1;
+        const Fr* tws = tw + (n - (n >> st));
+        const int half = E >> (u + 1);
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          if (j & half) continue;
+          wv[u][c++] = tws[index(a0 + ((uint32_t)j << qlog), m) & gap_mask];
+        }
+      }
+    }
     Fr x[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) x[j] = lds[((a0 + ((uint32_t)j << qlog)) << log_m) + m];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const uint32_t st = a.s0 + t + u;
-      const uint32_t gap_mask = (1u << (a.L - st - 1)) - 1;
       const Fr* tws = tw + (n - (n >> st));
       const int half = E >> (u + 1);
+      int c = 0;
 #pragma unroll
       for (int j = 0; j < E; ++j) {
         if (j & half) continue;
@@ -83,8 +101,7 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __res
           x[j + half] = idx ? lo.sub_unreduced(hi) * tws[idx] : (lo - hi);
         } else {
           // twiddles are canonical, so lo - hi + 2p needs no borrow test
-          const Fr w = tws[index(a0 + ((uint32_t)j << qlog), m) & gap_mask];
-          x[j + half] = lo.sub_unreduced(hi) * w;
+          x[j + half] = lo.sub_unreduced(hi) * wv[u][c++];
         }
       }
     }
