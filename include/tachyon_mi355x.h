@@ -293,11 +293,12 @@ TACHYON_C_EXPORT void tachyon_mi355x_ec_op(int curve, int op, const void* a, con
  *          out_a: G1 affine, out_b: G2 affine, out_c: G1 affine (canonical).
  *   witness_map: the h evaluations on the coset (domain_size Fr) to host memory.
  *   last_timings (profiling on): upload, qap, msm_a, msm_b2, msm_b1, msm_l,
- *          msm_h, total -- ms, 8 floats.
+ *          msm_h, total -- ms, 8 floats (msm_l: the witness and h MSMs, run as
+ *          one MSM over C1 | H1 since the proof only uses their sum; msm_h 0).
  * Multi-GPU split of prove (one process per GPU):
  *   prove_partials: this rank's shard (contiguous ceil(count / world) chunk
  *          `rank` of every MSM's points, the kParallelTerm split of
- *          pippenger_adapter.h:82-113) of the five MSMs, after the full
+ *          pippenger_adapter.h:82-113) of the proof's MSMs, after the full
  *          witness map; writes partials_size() bytes (an opaque blob of
  *          XYZZ sums, identical layout on every rank of one build).
  *          with_b1 != 0 runs the B-in-G1 MSM (required when r != 0).

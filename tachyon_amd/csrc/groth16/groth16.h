@@ -37,7 +37,7 @@ struct Proof {
   Affine<typename G1::F> c;
 };
 
-// One rank's share of the five MSMs of CreateProofWithAssignment
+// One rank's share of the MSMs of CreateProofWithAssignment
 // (prove.h:95-146) as XYZZ sums: rank k of `world` takes the contiguous
 // ceil(count / world) chunk k of every MSM's point range (the kParallelTerm
 // split, pippenger_adapter.h:82-113).  The partials of all ranks added
@@ -47,7 +47,7 @@ struct ProofPartials {
   uint32_t magic = 0x31363247;  // "G261": layout tag of the C-ABI blob
   uint32_t with_b1 = 0;         // the B-in-G1 MSM was run (needed when r != 0)
   uint32_t rank = 0, world = 1;
-  XYZZ<typename G1::F> a, b1, l, h;
+  XYZZ<typename G1::F> a, b1, lh;  // lh: the witness (C1) and h (H1) MSMs, merged
   XYZZ<typename G2::F> b2;
 };
 
@@ -77,7 +77,7 @@ class Groth16Prover {
   Proof<G1, G2> prove(const Fr* full, size_t count, const Fr* r, const Fr* s);
 
   // The multi-GPU split of prove(): every rank runs the witness map (it is a
-  // few percent of the proof) and its shard of the five MSMs; the partials of
+  // few percent of the proof) and its shard of the MSMs; the partials of
   // all ranks are exchanged (one all-gather) and assemble() adds them and
   // applies r, s and the key's alpha/beta/delta terms on the host.
   // prove(full, r, s) == assemble({partials(full, r != 0, 0, 1)}, r, s).
@@ -102,7 +102,8 @@ class Groth16Prover {
   std::unique_ptr<ntt::NttDomain<Fr>> dom_, coset_;
   std::unique_ptr<msm::MsmGpu<G1>> msm1_;
   std::unique_ptr<msm::MsmGpu<G2>> msm2_;
-  DeviceBuffer a1_, b1_, c1_, h1_, b2_;          // query points
+  DeviceBuffer a1_, b1_, lh1_, b2_;              // query points (lh1 = C1 | H1)
+  DeviceBuffer lh_;                              // scalars of the merged MSM: witness | h
   DeviceBuffer row_a_, row_b_, col_, val_;       // CSR of the A and B matrices
   DeviceBuffer full_, abc_;                      // witness, 3 x n work vectors
   ProveTimings timings_;

@@ -235,8 +235,16 @@ Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(
   upload(a1_, key_.a1);
   upload(b1_, key_.b1);
   upload(b2_, key_.b2);
-  upload(c1_, key_.c1);
-  upload(h1_, key_.h1);
+  // C1 (witness query) and H1 back to back: their MSMs are only ever added
+  // (C = ... + sum l_i C1_i + sum h_k H1_k, prove.h:146-160), so one MSM over
+  // the concatenation (scalars: witness values | h) replaces two
+  {
+    const size_t nw = key_.c1.size(), nh = key_.h1.size();
+    auto* d = static_cast<Affine<F1>*>(lh1_.ensure(std::max<size_t>(1, nw + nh) * sizeof(Affine<F1>)));
+    if (nw) TA_HIP(hipMemcpy(d, key_.c1.data(), nw * sizeof(Affine<F1>), hipMemcpyHostToDevice));
+    if (nh) TA_HIP(hipMemcpy(d + nw, key_.h1.data(), nh * sizeof(Affine<F1>), hipMemcpyHostToDevice));
+    lh_.ensure(std::max<size_t>(1, nw + nh) * sizeof(Fr));
+  }
 
   // CSR by constraint: A rows first, then B rows, in one col/val array
   const size_t n = n_;
@@ -322,8 +330,12 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     timings_.upload = ms_since(t0);
   }
   auto t1 = Clock::now();
-  Fr* d_h = abc_.as<Fr>();
-  witness_map(d_full, d_h);
+  // scalars of the merged witness + h MSM: [witness values | h]
+  const size_t nw = key_.num_witness();
+  Fr* d_lh = lh_.as<Fr>();
+  if (nw)
+    TA_HIP(hipMemcpyAsync(d_lh, d_full + key_.num_instance(), nw * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+  witness_map(d_full, d_lh + nw);
   if (profile_) {
     TA_HIP(hipStreamSynchronize(stream_));
     timings_.qap = ms_since(t1);
@@ -376,16 +388,13 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   out.b1 = (with_b1 && q_len) ? msm1_->run(b1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
   timings_.msm_b1 = ms_since(t2);
   t2 = Clock::now();
-  size_t l_lo = 0;
-  const size_t l_len = shard(key_.num_witness(), &l_lo);
-  out.l = l_len ? msm1_->run(c1_.as<Affine<F1>>() + l_lo, d_full + key_.num_instance() + l_lo, l_len) : P1::zero();
+  // witness (l) and h MSMs merged; h_coefficients.size() == h_g1_query.size()
+  // == domain size: the else branch of prove.h:103-112
+  size_t lh_lo = 0;
+  const size_t lh_len = shard(nw + n_, &lh_lo);
+  out.lh = lh_len ? msm1_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
   timings_.msm_l = ms_since(t2);
-  t2 = Clock::now();
-  // h_coefficients.size() == h_g1_query.size() == domain size: the else branch of prove.h:103-112
-  size_t h_lo = 0;
-  const size_t h_len = shard(n_, &h_lo);
-  out.h = h_len ? msm1_->run(h1_.as<Affine<F1>>() + h_lo, d_h + h_lo, h_len) : P1::zero();
-  timings_.msm_h = ms_since(t2);
+  timings_.msm_h = 0;
   g2_thread.join();
   if (g2_error) std::rethrow_exception(g2_error);
   out.b2 = acc_b2;
@@ -401,7 +410,7 @@ Proof<G1, G2> Groth16Prover<G1, G2>::assemble(const ProofPartials<G1, G2>* parts
   const Fr r = r_ptr ? *r_ptr : Fr::zero();
   const Fr s = s_ptr ? *s_ptr : Fr::zero();
   if (world == 0) throw std::runtime_error("tachyon_mi355x: Groth16 assemble needs at least one partial");
-  P1 acc_a = P1::zero(), acc_b1 = P1::zero(), acc_l = P1::zero(), acc_h = P1::zero();
+  P1 acc_a = P1::zero(), acc_b1 = P1::zero(), acc_lh = P1::zero();
   P2 acc_b2 = P2::zero();
   std::vector<bool> seen(world, false);
   for (size_t k = 0; k < world; ++k) {
@@ -413,8 +422,7 @@ Proof<G1, G2> Groth16Prover<G1, G2>::assemble(const ProofPartials<G1, G2>* parts
     seen[p.rank] = true;
     acc_a = acc_a + p.a;
     acc_b1 = acc_b1 + p.b1;
-    acc_l = acc_l + p.l;
-    acc_h = acc_h + p.h;
+    acc_lh = acc_lh + p.lh;
     acc_b2 = acc_b2 + p.b2;
   }
 
@@ -434,8 +442,7 @@ Proof<G1, G2> Groth16Prover<G1, G2>::assemble(const ProofPartials<G1, G2>* parts
     C = C + mul_scalar(B1, r);
     C = C + mul_scalar(r_delta1, s).neg();
   }
-  C = C + acc_l;
-  C = C + acc_h;
+  C = C + acc_lh;  // sum_witness l_i + h
   return Proof<G1, G2>{A.to_affine(), B2.to_affine(), C.to_affine()};
 }
 

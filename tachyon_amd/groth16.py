@@ -92,7 +92,7 @@ class Groth16Prover:
         return lib().tachyon_mi355x_groth16_partials_size(self._h)
 
     def prove_partials(self, full, rank: int, world: int, with_b1: bool = False) -> bytes:
-        """This rank's shard of the five MSMs (after the full witness map) as an
+        """This rank's shard of the proof's MSMs (after the full witness map) as an
         opaque blob of partials_size() bytes; with_b1 is required when the
         proof will be assembled with r != 0."""
         p, n, keep = _ptr(full)
