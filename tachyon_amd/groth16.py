@@ -132,6 +132,8 @@ class Groth16Prover:
         lib().tachyon_mi355x_groth16_set_profile(self._h, 1 if on else 0)
 
     def last_timings(self) -> dict:
+        """ms per phase of the last prove with profiling on; msm_l is the merged
+        witness + h MSM (msm_h stays 0)."""
         out = (ctypes.c_float * 8)()
         lib().tachyon_mi355x_groth16_last_timings(self._h, out)
         return dict(zip(("upload", "qap", "msm_a", "msm_b2", "msm_b1", "msm_l", "msm_h", "total"), list(out)))
