@@ -152,3 +152,55 @@ def test_all_gather_bytes_world3():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == b"".join(bytes((r * 37 + i) & 0xFF for i in range(1000)) for r in range(3))
+
+
+def _g16_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tachyon_amd.groth16 import Groth16Prover
+
+        class HostOnly(Groth16Prover):
+            """prove_sharded's host logic with the library calls stubbed out."""
+            def __init__(self):
+                self._h = None
+                self.calls = []
+
+            def partials_size(self):
+                return 48
+
+            def prove_partials(self, full, rank, world, with_b1=False):
+                self.calls.append(("partials", rank, world, with_b1))
+                return bytes([rank]) * 48
+
+            def assemble(self, parts, r=None, s=None):
+                self.calls.append(("assemble", parts, r, s))
+                return (b"A", b"B", b"C")
+
+        p = HostOnly()
+        r = (7).to_bytes(32, "little")
+        proof = p.prove_sharded(b"\0" * 64, r, r)
+        q.put((rank, proof, p.calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_groth16_prove_sharded_world2():
+    """Groth16Prover.prove_sharded: each rank computes its own shard (rank,
+    world, B1 when r != 0), one all-gather hands every rank the blobs in rank
+    order, every rank assembles the same proof."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_g16_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r = (7).to_bytes(32, "little")
+    for rank, proof, calls in got:
+        assert proof == (b"A", b"B", b"C")
+        assert calls[0] == ("partials", rank, 2, True)
+        assert calls[1] == ("assemble", bytes([0]) * 48 + bytes([1]) * 48, r, r)
