@@ -329,18 +329,6 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     TA_HIP(hipStreamSynchronize(stream_));
     timings_.upload = ms_since(t0);
   }
-  auto t1 = Clock::now();
-  // scalars of the merged witness + h MSM: [witness values | h]
-  const size_t nw = key_.num_witness();
-  Fr* d_lh = lh_.as<Fr>();
-  if (nw)
-    TA_HIP(hipMemcpyAsync(d_lh, d_full + key_.num_instance(), nw * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
-  witness_map(d_full, d_lh + nw);
-  if (profile_) {
-    TA_HIP(hipStreamSynchronize(stream_));
-    timings_.qap = ms_since(t1);
-  }
-
   // this rank's chunk [lo, lo + len) of an MSM over `total` points
   auto shard = [&](size_t total, size_t* lo) {
     const size_t chunk = (total + world - 1) / world;
@@ -358,10 +346,11 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   const Affine<F2>* b2 = b2_.as<Affine<F2>>();
   size_t q_lo = 0;  // queries 1 .. m-1 (index 0 is added on the host)
   const size_t q_len = m > 1 ? shard(m - 1, &q_lo) : 0;
-  // The G2 MSM (about 3x the work of a G1 one) runs on its own stream from a
-  // second host thread while the G1 MSMs run here; each MSM is synchronous on
-  // its host thread (its read-back of the chain lengths).  The witness and h
-  // are ready once stream_ drains.
+  // The G2 MSM (about 3x the work of a G1 one) needs only the witness: it
+  // starts on its own stream from a second host thread as soon as the
+  // witness is on the device, beside the witness map and the G1 MSMs here;
+  // each MSM is synchronous on its host thread (its read-back of the chain
+  // lengths).
   TA_HIP(hipStreamSynchronize(stream_));
   P2 acc_b2 = P2::zero();
   std::exception_ptr g2_error;
@@ -381,6 +370,18 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     std::thread& t;
     ~Joiner() { if (t.joinable()) t.join(); }
   } joiner{g2_thread};
+
+  auto t1 = Clock::now();
+  // scalars of the merged witness + h MSM: [witness values | h]
+  const size_t nw = key_.num_witness();
+  Fr* d_lh = lh_.as<Fr>();
+  if (nw)
+    TA_HIP(hipMemcpyAsync(d_lh, d_full + key_.num_instance(), nw * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+  witness_map(d_full, d_lh + nw);
+  if (profile_) {
+    TA_HIP(hipStreamSynchronize(stream_));
+    timings_.qap = ms_since(t1);
+  }
   auto t2 = Clock::now();
   out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
   timings_.msm_a = ms_since(t2);
