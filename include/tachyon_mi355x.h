@@ -169,6 +169,17 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_dense_polynomial_get_value
 TACHYON_C_EXPORT tachyon_bn254_fr* tachyon_mi355x_bn254_univariate_dense_polynomial_data(
     tachyon_bn254_univariate_dense_polynomial* poly);
 
+/* halo2 BN254 Fr generator set (math::halo2, bn/bn254/halo2/bn254.h:9-17):
+ * _override = OverrideSubgroupGenerator() (bn254.cc:7-30: generator 7 and
+ * halo2curves' two-adic / large-subgroup roots of unity), _restore = the
+ * ScopedSubgroupGeneratorOverrider destructor (bn254.cc:40-44, back to the
+ * arkworks-compatible generator 5).  Process-wide; domains, four-step plans
+ * and KZG setups created afterwards use the active set (Domain::Create
+ * captures the root).  _active returns 1 while the halo2 set is installed. */
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_halo2_override_subgroup_generator(void);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_halo2_restore_subgroup_generator(void);
+TACHYON_C_EXPORT int tachyon_mi355x_bn254_halo2_subgroup_generator_active(void);
+
 /* Domain queries and the coset hook (UnivariateEvaluationDomain::GetCoset,
  * univariate_evaluation_domain.h:102-117): set_offset turns the domain into
  * its coset h*<w>; offset 1 restores it. */
@@ -211,7 +222,18 @@ TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timi
  *   stage(1, in -> send); all-to-all(send -> recv) by the caller; stage(2, recv -> out)
  * with send/recv = G chunks of local_size/G elements (chunk h to/from rank h).
  * The inverse maps the output layout back to the input layout (n^-1 included).
- * Work is enqueued on `stream` (hipStream_t; NULL = a stream owned by the plan). */
+ *
+ * Ordering contract.  Every stage is enqueued on the plan's stream (`stream`
+ * at create, a hipStream_t; NULL = a non-blocking stream the plan owns;
+ * _stream returns it) and returns without synchronising.  The stages wait for
+ * nothing else: the caller (1) makes the plan's stream wait for whatever
+ * produced d_in (hipEventRecord on the producer + hipStreamWaitEvent, or
+ * produce it on the plan's stream), (2) runs its all-to-all on the plan's
+ * stream -- e.g. ncclAllToAll / RCCL with that stream -- or orders it after
+ * stage 1 with an event, and (3) does the same before reading d_out.  A
+ * non-blocking stream does not order against the legacy NULL stream, so
+ * "same stream" must be meant literally.  tachyon_amd.dist.sharded_ntt keeps
+ * the contract (tests/test_gpu_dist.py produces the input on another stream). */
 typedef struct tachyon_mi355x_bn254_ntt4 tachyon_mi355x_bn254_ntt4;
 TACHYON_C_EXPORT tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create(uint32_t log_n, uint32_t log_world,
                                                                             uint32_t rank, void* stream);
@@ -220,6 +242,7 @@ TACHYON_C_EXPORT size_t tachyon_mi355x_bn254_ntt4_local_size(const tachyon_mi355
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4* plan, int stage, int inverse,
                                                       const tachyon_bn254_fr* d_in, tachyon_bn254_fr* d_out);
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_synchronize(tachyon_mi355x_bn254_ntt4* plan);
+TACHYON_C_EXPORT void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn254_ntt4* plan);
 
 /* G2 MSM contexts (Groth16's B-in-G2, BLS12-381 config 4); same semantics as
  * the G1 *_msm_gpu entry points. */
@@ -243,8 +266,10 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const 
                                                     size_t size, void* out_affine);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
-/* kernel-variant bits for A/B tuning in one process (0 = default schedule) */
-TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
+/* kernel-variant bits for A/B tuning in one process (0 = default schedule).
+ * Every accepted variant computes the same MSM; returns 0 (nothing changed)
+ * for bits outside 0x3BF. */
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
  * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total,
  * accumulation launches (8 floats; of the last point chunk when the run was divided) */
@@ -341,8 +366,11 @@ TACHYON_C_EXPORT size_t tachyon_mi355x_wtns_parse(int curve, const uint8_t* wtns
  *     the size-n domain (UnsafeSetup :173-207), built and kept on the device;
  *   downsize: returns 0 if n >= N (Downsize :210-215);
  *   get_srs: the N points (lagrange = 0 powers of tau, 1 Lagrange) to host;
- *   commit: MSM of the first min(N, len) SRS points with `scalars` (host or
- *     device pointer) -- Commit (lagrange = 0) / CommitLagrange (1), :217-258. */
+ *   commit: MSM of the first len SRS points with `scalars` (host or device
+ *     pointer) -- Commit (lagrange = 0) / CommitLagrange (1), :217-258.
+ *     Returns 1, or 0 with out_affine untouched when len > N (the reference
+ *     returns false: DoMSM trims the bases to min(N, len), then the MSM
+ *     refuses bases/scalars of different sizes, :267-290). */
 typedef struct tachyon_mi355x_kzg tachyon_mi355x_kzg;
 TACHYON_C_EXPORT tachyon_mi355x_kzg* tachyon_mi355x_kzg_create(int curve);
 TACHYON_C_EXPORT void tachyon_mi355x_kzg_destroy(tachyon_mi355x_kzg* kzg);
@@ -350,8 +378,8 @@ TACHYON_C_EXPORT void tachyon_mi355x_kzg_unsafe_setup(tachyon_mi355x_kzg* kzg, s
 TACHYON_C_EXPORT size_t tachyon_mi355x_kzg_n(const tachyon_mi355x_kzg* kzg);
 TACHYON_C_EXPORT int tachyon_mi355x_kzg_downsize(tachyon_mi355x_kzg* kzg, size_t n);
 TACHYON_C_EXPORT void tachyon_mi355x_kzg_get_srs(const tachyon_mi355x_kzg* kzg, int lagrange, void* out);
-TACHYON_C_EXPORT void tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* kzg, int lagrange, const void* scalars,
-                                                size_t len, void* out_affine);
+TACHYON_C_EXPORT int tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* kzg, int lagrange, const void* scalars,
+                                               size_t len, void* out_affine);
 
 /* delete a Jacobian returned by an *_msm / *_msm_gpu entry point (for callers
  * that cannot use C++ delete, e.g. ctypes). */

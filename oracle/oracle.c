@@ -150,9 +150,22 @@
 #undef SF_BITS
 
 /* ---- NTT ------------------------------------------------------------------ */
+/* math::halo2::OverrideSubgroupGenerator() (bn/bn254/halo2/bn254.cc:7-30)
+ * replaces BN254 Fr's kSubgroupGenerator (5 -> 7), kTwoAdicRootOfUnity and
+ * kLargeSubgroupRootOfUnity with halo2curves' values (Montgomery limbs, as
+ * the reference writes them).  GetRootOfUnity (prime_field_base.h:90-130)
+ * takes the large-subgroup branch for BN254 Fr: w = large^(3^2) squared
+ * (28 - log n) times; large^9 equals the two-adic root for both constant
+ * sets (checked by tests/test_halo2_golden.py), so the two-adic root below
+ * is that same w.  Domains capture the root when they are created. */
+static const uint64_t BN254_FR_HALO2_TWO_ADIC_ROOT_MONT[4] = {
+    10822932506504462008ULL, 10978899855858987673ULL, 12888607242213977304ULL, 2119232853909229097ULL};
+static const uint64_t BN254_FR_HALO2_LARGE_SUBGROUP_ROOT_MONT[4] = {
+    9055134861510678988ULL, 3166494206591041163ULL, 11983946130272577941ULL, 1690279781341100183ULL};
+static int g_bn254_fr_halo2 = 0;
 #define FF bn254_fr
 #define FF_TWO_ADICITY BN254_FR_TWO_ADICITY
-#define FF_TWO_ADIC_ROOT BN254_FR_TWO_ADIC_ROOT_MONT
+#define FF_TWO_ADIC_ROOT (g_bn254_fr_halo2 ? BN254_FR_HALO2_TWO_ADIC_ROOT_MONT : BN254_FR_TWO_ADIC_ROOT_MONT)
 #include "ntt_impl.h"
 #undef FF
 #undef FF_TWO_ADICITY
@@ -408,6 +421,35 @@ EXPORT long oracle_ifft(int field, size_t domain_num_coeffs, const void* offset,
 }
 
 /* Domain scalars for tests: writes group_gen, group_gen_inv, size_inv. */
+/* 1: install the halo2 generator / roots (OverrideSubgroupGenerator), 0: restore
+ * (~ScopedSubgroupGeneratorOverrider).  Returns the previous state. */
+EXPORT int oracle_bn254_fr_set_halo2(int on) {
+  int prev = g_bn254_fr_halo2;
+  g_bn254_fr_halo2 = on != 0;
+  return prev;
+}
+
+/* out: kLargeSubgroupRootOfUnity of the active constant set (Montgomery limbs) */
+EXPORT void oracle_bn254_fr_large_subgroup_root(void* out) {
+  if (g_bn254_fr_halo2) {
+    memcpy(out, BN254_FR_HALO2_LARGE_SUBGROUP_ROOT_MONT, 32);
+  } else {
+    /* generator 5: 5^(t / 3^2), t = (p - 1) / 2^28 (prime_field_generator.cc:292-316) */
+    uint64_t t[4];
+    memcpy(t, BN254_FR_P, sizeof t);
+    t[0] -= 1;
+    for (int i = 0; i < 4; ++i) t[i] = (t[i] >> 28) | (i < 3 ? t[i + 1] << 36 : 0);
+    unsigned __int128 rem = 0;
+    for (int i = 3; i >= 0; --i) {
+      unsigned __int128 cur = (rem << 64) | t[i];
+      t[i] = (uint64_t)(cur / 9);
+      rem = cur % 9;
+    }
+    bn254_fr_t r = bn254_fr_pow(bn254_fr_from_u64(5), t, 4);
+    memcpy(out, r.l, 32);
+  }
+}
+
 EXPORT int oracle_domain_info(int field, size_t num_coeffs, void* out3) {
   if (field == 1) {
     bn254_fr_domain_t* d = bn254_fr_domain_create(num_coeffs);

@@ -59,6 +59,10 @@ def lib():
         L.oracle_domain_info.argtypes = [i, sz, vp]
         L.oracle_domain_info.restype = i
         L.oracle_max_threads.restype = i
+        L.oracle_bn254_fr_set_halo2.argtypes = [i]
+        L.oracle_bn254_fr_set_halo2.restype = i
+        L.oracle_bn254_fr_large_subgroup_root.argtypes = [vp]
+        L.oracle_bn254_fr_large_subgroup_root.restype = None
         _lib = L
     return _lib
 
@@ -163,3 +167,27 @@ def ec_op(curve, op, p: bytes, q: bytes = None):
 
 def max_threads():
     return lib().oracle_max_threads()
+
+
+def bn254_fr_set_halo2(on: bool) -> bool:
+    """OverrideSubgroupGenerator (on) / restore (off) for domains created
+    afterwards (bn/bn254/halo2/bn254.cc:7-30).  Returns the previous state."""
+    return bool(lib().oracle_bn254_fr_set_halo2(1 if on else 0))
+
+
+def bn254_fr_large_subgroup_root() -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().oracle_bn254_fr_large_subgroup_root(out)
+    return out.raw
+
+
+class halo2_domain:
+    """with halo2_domain(): ...  -- ScopedSubgroupGeneratorOverrider (bn254.cc:32-44)."""
+
+    def __enter__(self):
+        self._prev = bn254_fr_set_halo2(True)
+        return self
+
+    def __exit__(self, *exc):
+        bn254_fr_set_halo2(self._prev)
+        return False

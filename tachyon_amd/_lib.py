@@ -75,6 +75,9 @@ SIGNATURES = [
     ("tachyon_mi355x_bn254_univariate_dense_polynomial_set_value", None, [vp, sz, vp]),
     ("tachyon_mi355x_bn254_univariate_dense_polynomial_get_value", None, [vp, sz, vp]),
     ("tachyon_mi355x_bn254_univariate_dense_polynomial_data", vp, [vp]),
+    ("tachyon_mi355x_bn254_halo2_override_subgroup_generator", None, []),
+    ("tachyon_mi355x_bn254_halo2_restore_subgroup_generator", None, []),
+    ("tachyon_mi355x_bn254_halo2_subgroup_generator_active", i32, []),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_size", sz, [vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_group_gen", None, [vp, vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset", None, [vp, vp]),
@@ -89,6 +92,7 @@ SIGNATURES = [
     ("tachyon_mi355x_bn254_ntt4_local_size", sz, [vp]),
     ("tachyon_mi355x_bn254_ntt4_stage", None, [vp, i32, i32, vp, vp]),
     ("tachyon_mi355x_bn254_ntt4_synchronize", None, [vp]),
+    ("tachyon_mi355x_bn254_ntt4_stream", vp, [vp]),
     ("tachyon_bn254_g2_create_msm_gpu", vp, [u8]),
     ("tachyon_bn254_g2_destroy_msm_gpu", None, [vp]),
     ("tachyon_bn254_g2_affine_msm_gpu", vp, [vp, vp, vp, sz]),
@@ -98,7 +102,7 @@ SIGNATURES = [
     ("tachyon_mi355x_msm_gpu_affine", None, [i32, vp, vp, vp, sz, vp]),
     ("tachyon_mi355x_msm_gpu_set_window_bits", None, [i32, vp, ctypes.c_uint]),
     ("tachyon_mi355x_msm_gpu_set_profile", None, [i32, vp, i32]),
-    ("tachyon_mi355x_msm_gpu_set_variant", None, [i32, vp, i32]),
+    ("tachyon_mi355x_msm_gpu_set_variant", i32, [i32, vp, i32]),
     ("tachyon_mi355x_msm_gpu_last_divisions", sz, [i32, vp]),
     ("tachyon_mi355x_msm_gpu_last_timings", None, [i32, vp, fp]),
     ("tachyon_mi355x_msm_plan", None, [i32, sz, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]),
@@ -126,7 +130,7 @@ SIGNATURES = [
     ("tachyon_mi355x_kzg_n", sz, [vp]),
     ("tachyon_mi355x_kzg_downsize", i32, [vp, sz]),
     ("tachyon_mi355x_kzg_get_srs", None, [vp, i32, vp]),
-    ("tachyon_mi355x_kzg_commit", None, [vp, i32, vp, sz, vp]),
+    ("tachyon_mi355x_kzg_commit", i32, [vp, i32, vp, sz, vp]),
     ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
     ("tachyon_mi355x_version", ctypes.c_char_p, []),
     ("tachyon_mi355x_device_count", i32, []),

@@ -304,8 +304,10 @@ void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c) {
 void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on) {
   GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_profile(on != 0)) GUARD_END
 }
-void tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant) {
+int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant) {
+  if (variant < 0 || (variant & ~msm::kMsmVariantMask)) return 0;  // unknown bits: refused, nothing changed
   GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_variant(variant)) GUARD_END
+  return 1;
 }
 void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8) {
   GUARD_BEGIN CURVE_DISPATCH(curve, {
@@ -521,6 +523,10 @@ tachyon_bn254_fr* tachyon_mi355x_bn254_univariate_dense_polynomial_data(tachyon_
   return poly->v.data();
 }
 
+void tachyon_mi355x_bn254_halo2_override_subgroup_generator(void) { ntt::set_bn254_fr_halo2_generator(true); }
+void tachyon_mi355x_bn254_halo2_restore_subgroup_generator(void) { ntt::set_bn254_fr_halo2_generator(false); }
+int tachyon_mi355x_bn254_halo2_subgroup_generator_active(void) { return ntt::bn254_fr_halo2_generator() ? 1 : 0; }
+
 size_t tachyon_mi355x_bn254_univariate_evaluation_domain_size(const tachyon_bn254_univariate_evaluation_domain* d) {
   return d->impl->size();
 }
@@ -603,6 +609,9 @@ void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4* plan, int stage,
   if (!inverse) (stage == 1) ? plan->impl->forward_stage1(in, out) : plan->impl->forward_stage2(in, out);
   else (stage == 1) ? plan->impl->inverse_stage1(in, out) : plan->impl->inverse_stage2(in, out);
   GUARD_END
+}
+void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn254_ntt4* plan) {
+  return static_cast<void*>(plan->impl->stream());
 }
 void tachyon_mi355x_bn254_ntt4_synchronize(tachyon_mi355x_bn254_ntt4* plan) {
   GUARD_BEGIN

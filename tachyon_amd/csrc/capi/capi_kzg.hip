@@ -82,13 +82,15 @@ void tachyon_mi355x_kzg_get_srs(const tachyon_mi355x_kzg* p, int lagrange, void*
   GUARD_END
 }
 
-void tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* p, int lagrange, const void* scalars, size_t len,
-                               void* out_affine) {
+int tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* p, int lagrange, const void* scalars, size_t len,
+                              void* out_affine) {
   GUARD_BEGIN
   KZG_DISPATCH(p, {
     using K = std::remove_pointer_t<decltype(impl)>;
-    auto a = impl->commit(static_cast<const typename K::Fr*>(scalars), len, lagrange != 0);
+    typename K::Aff a;
+    if (!impl->commit(static_cast<const typename K::Fr*>(scalars), len, lagrange != 0, &a)) return 0;
     memcpy(out_affine, &a, sizeof(a));
+    return 1;
   });
   GUARD_END
 }

@@ -44,8 +44,11 @@ struct Proof {
 // together are the single-GPU MSM results, whatever the split.
 template <class G1, class G2>
 struct ProofPartials {
-  uint32_t magic = 0x31363247;  // "G261": layout tag of the C-ABI blob
-  uint32_t with_b1 = 0;         // the B-in-G1 MSM was run (needed when r != 0)
+  // layout tag of the C-ABI blob: bump the magic whenever the fields change
+  // ("G262": a, b1, merged lh, b2); `bytes` catches a size mismatch as well
+  uint32_t magic = 0x32363247;
+  uint32_t bytes = sizeof(ProofPartials);
+  uint32_t with_b1 = 0;  // the B-in-G1 MSM was run (needed when r != 0)
   uint32_t rank = 0, world = 1;
   XYZZ<typename G1::F> a, b1, lh;  // lh: the witness (C1) and h (H1) MSMs, merged
   XYZZ<typename G2::F> b2;

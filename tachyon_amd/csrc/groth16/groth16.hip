@@ -416,7 +416,9 @@ Proof<G1, G2> Groth16Prover<G1, G2>::assemble(const ProofPartials<G1, G2>* parts
   std::vector<bool> seen(world, false);
   for (size_t k = 0; k < world; ++k) {
     const auto& p = parts[k];
-    if (p.magic != ProofPartials<G1, G2>().magic || p.world != world || p.rank >= world || seen[p.rank])
+    if (p.magic != ProofPartials<G1, G2>().magic || p.bytes != sizeof(ProofPartials<G1, G2>))
+      throw std::runtime_error("tachyon_mi355x: Groth16 partials blob has another layout (library version mismatch)");
+    if (p.world != world || p.rank >= world || seen[p.rank])
       throw std::runtime_error("tachyon_mi355x: Groth16 partials are not one rank each of the same world");
     if (!r.is_zero() && !p.with_b1)
       throw std::runtime_error("tachyon_mi355x: Groth16 partials lack the B1 MSM that r != 0 needs");

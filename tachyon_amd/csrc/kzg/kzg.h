@@ -38,8 +38,11 @@ class Kzg {
   size_t n() const { return n_; }
   bool downsize(size_t n);
 
-  // MSM of the first min(N, len) SRS points with `scalars` (host or device).
-  Aff commit(const Fr* scalars, size_t len, bool lagrange);
+  // MSM of the first len SRS points with `scalars` (host or device).  False,
+  // with *out untouched, when len > N (the reference's DoMSM trims the bases
+  // to min(|bases|, |scalars|) and PippengerAdapter then refuses unequal
+  // sizes, so Commit / CommitLagrange return false, kzg.h:217-258,267-290).
+  bool commit(const Fr* scalars, size_t len, bool lagrange, Aff* out);
 
   const Aff* d_srs(bool lagrange) const { return lagrange ? lagrange_.as<Aff>() : powers_.as<Aff>(); }
   void copy_srs(bool lagrange, Aff* host_out) const;

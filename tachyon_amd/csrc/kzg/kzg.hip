@@ -136,9 +136,10 @@ bool Kzg<Curve>::downsize(size_t n) {
 }
 
 template <class Curve>
-typename Kzg<Curve>::Aff Kzg<Curve>::commit(const Fr* scalars, size_t len, bool lagrange) {
-  const size_t m = std::min(n_, len);
-  return msm_->run(d_srs(lagrange), scalars, m).to_affine();
+bool Kzg<Curve>::commit(const Fr* scalars, size_t len, bool lagrange, Aff* out) {
+  if (len > n_) return false;
+  *out = msm_->run(d_srs(lagrange), scalars, len).to_affine();
+  return true;
 }
 
 template <class Curve>

@@ -25,6 +25,9 @@
 
 namespace tachyon_amd::msm {
 
+// MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
+constexpr int kMsmVariantMask = 0x3BF;
+
 struct MsmPlan {
   unsigned c = 0;        // window bits
   unsigned windows = 0;  // W
@@ -127,7 +130,13 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  void set_variant(int v) { variant_ = v; }
+  // A/B tuning knobs (bits 0-5, 7-9; see run_windows).  Every variant computes
+  // the same MSM; bit 6 (once a wrong-result gather-locality experiment) and
+  // anything above bit 9 are refused.
+  void set_variant(int v) {
+    if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
+    variant_ = v;
+  }
   void set_profile(bool on) { profile_ = on; }
   const MsmTimings& timings() const { return timings_; }
   hipStream_t stream() const { return stream_; }
@@ -159,7 +168,7 @@ class MsmGpu {
   std::vector<hipEvent_t> gev_sorted_, gev_acc0_, gev_acc1_;
   unsigned acc_launches_ = 0;
   unsigned sort_bits_ = 0;
-  uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (experiments only)
+  uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode
   bool scatter_lds_set_ = false;

@@ -717,9 +717,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
     case 3: plan.group = plan.windows; break;
     default: break;
   }
-  // bit 6: gather-locality experiment -- every base index masked to 2^20
-  // points (a 64 MiB slice that stays in the Infinity Cache); results are wrong
-  idx_mask_ = (variant_ & 64) ? ((1u << 20) - 1) : ~kSignBit;
+  idx_mask_ = ~kSignBit;
   fuse_recode_ = !(variant_ & 128);  // bit 7: the separate recode + full sort (A/B)
   static constexpr uint32_t kSpt[] = {kRecodeSpt, 1, 4, 3};
   recode_spt_ = kSpt[(variant_ >> 8) & 3];  // bits 8-9: scalars per thread of the fused recode

@@ -96,9 +96,20 @@ extern template class NttDomain<Bn254Fr>;
 extern template class NttDomain<Bls381Fr>;
 
 // w_(2^log_n), Montgomery form: the two-adic root squared down
-// (PrimeFieldBase::GetRootOfUnity, prime_field_base.h:90-130).
+// (PrimeFieldBase::GetRootOfUnity, prime_field_base.h:90-130).  For BN254 Fr
+// the root comes from the active generator set (below).
 template <class Fr>
 Fr root_of_unity(uint32_t log_n);
+
+// BN254 Fr generator set used by domains created from now on:
+// math::halo2::OverrideSubgroupGenerator() (bn/bn254/halo2/bn254.cc:7-30)
+// installs halo2curves' generator 7 and its two-adic / large-subgroup roots
+// in place of the arkworks-compatible generator 5; the scoped overrider's
+// destructor (bn254.cc:32-44) restores them.  A domain, a four-step plan and a
+// KZG setup capture the root when they are built, as the reference's
+// Domain::Create does.  Returns the previous state.
+bool set_bn254_fr_halo2_generator(bool on);
+bool bn254_fr_halo2_generator();
 // n as a field element (Montgomery form)
 template <class Fr>
 Fr field_from_u64(uint64_t v);

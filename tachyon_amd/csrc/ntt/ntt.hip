@@ -4,8 +4,10 @@
 #include "ntt.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 namespace tachyon_amd::ntt {
 
@@ -217,10 +219,21 @@ Fr fr_from_u64(uint64_t v) {
   return x.to_mont();
 }
 
+// halo2curves' BN254 Fr two-adic root of unity 7^((r-1)/2^28), Montgomery limbs
+// exactly as OverrideSubgroupGenerator writes kTwoAdicRootOfUnity
+// (bn/bn254/halo2/bn254.cc:18-23).  GetRootOfUnity's large-subgroup branch
+// (large^(3^2), bn254.cc:24-29) lands on the same element.
+constexpr uint64_t kBn254FrHalo2TwoAdicRootMont64[4] = {10822932506504462008ULL, 10978899855858987673ULL,
+                                                        12888607242213977304ULL, 2119232853909229097ULL};
+std::atomic<bool> g_bn254_fr_halo2{false};
+
 template <class Fr>
 Fr two_adic_root() {
   Fr r;
   const uint64_t* src = Fr::Config::kTwoAdicRootMont64;
+  if constexpr (std::is_same_v<Fr, Bn254Fr>) {
+    if (g_bn254_fr_halo2.load()) src = kBn254FrHalo2TwoAdicRootMont64;
+  }
   for (int i = 0; i < Fr::N / 2; ++i) {
     r.v[2 * i] = (uint32_t)src[i];
     r.v[2 * i + 1] = (uint32_t)(src[i] >> 32);
@@ -571,6 +584,9 @@ Fr root_of_unity(uint32_t log_n) {
   for (uint32_t i = log_n; i < (uint32_t)Fr::Config::kTwoAdicity; ++i) w = w.sqr();
   return w;
 }
+bool set_bn254_fr_halo2_generator(bool on) { return g_bn254_fr_halo2.exchange(on); }
+bool bn254_fr_halo2_generator() { return g_bn254_fr_halo2.load(); }
+
 template <class Fr>
 Fr field_from_u64(uint64_t v) {
   return fr_from_u64<Fr>(v);

@@ -60,18 +60,21 @@ class KZG:
     def g1_powers_of_tau_lagrange(self) -> bytes:
         return self._srs(True)
 
-    def _commit(self, scalars, lagrange: bool) -> bytes:
+    def _commit(self, scalars, lagrange: bool):
         p, n, keep = _ptr(scalars)
         out = ctypes.create_string_buffer(self.point_bytes)
-        lib().tachyon_mi355x_kzg_commit(self._h, 1 if lagrange else 0, p, n // 32, out)
+        if not lib().tachyon_mi355x_kzg_commit(self._h, 1 if lagrange else 0, p, n // 32, out):
+            return None
         return out.raw
 
-    def commit(self, coeffs) -> bytes:
-        """Commit(poly coefficients) -> affine commitment bytes."""
+    def commit(self, coeffs):
+        """Commit(poly coefficients) -> affine commitment bytes, or None where
+        the reference returns false (more coefficients than N, kzg.h:217-226)."""
         return self._commit(coeffs, False)
 
-    def commit_lagrange(self, evals) -> bytes:
-        """CommitLagrange(evaluations over the size-N domain) -> affine bytes."""
+    def commit_lagrange(self, evals):
+        """CommitLagrange(evaluations over the size-N domain) -> affine bytes,
+        or None when |evals| > N (kzg.h:239-248)."""
         return self._commit(evals, True)
 
     def commit_batch(self, polys, lagrange: bool = False) -> list:

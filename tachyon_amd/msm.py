@@ -100,7 +100,8 @@ class VariableBaseMSMGpu:
         lib().tachyon_mi355x_msm_gpu_set_profile(self.curve_id, self._ctx, 1 if on else 0)
 
     def set_variant(self, variant: int):
-        lib().tachyon_mi355x_msm_gpu_set_variant(self.curve_id, self._ctx, variant)
+        if not lib().tachyon_mi355x_msm_gpu_set_variant(self.curve_id, self._ctx, variant):
+            raise ValueError(f"unknown MSM variant bits in {variant:#x}")
 
     def last_divisions(self) -> int:
         """Point chunks the last run was split into (device memory or host-upload pipeline)."""

@@ -13,6 +13,35 @@ from ._lib import lib
 FR_BYTES = 32
 
 
+def override_subgroup_generator():
+    """math::halo2::OverrideSubgroupGenerator() (bn/bn254/halo2/bn254.cc:7-30):
+    BN254 Fr domains created afterwards use halo2curves' generator 7."""
+    lib().tachyon_mi355x_bn254_halo2_override_subgroup_generator()
+
+
+def restore_subgroup_generator():
+    lib().tachyon_mi355x_bn254_halo2_restore_subgroup_generator()
+
+
+def halo2_subgroup_generator_active() -> bool:
+    return bool(lib().tachyon_mi355x_bn254_halo2_subgroup_generator_active())
+
+
+class ScopedSubgroupGeneratorOverrider:
+    """math::halo2::ScopedSubgroupGeneratorOverrider (bn254.cc:32-44) as a
+    context manager: installs the halo2 set, restores the previous one on exit."""
+
+    def __enter__(self):
+        self._prev = halo2_subgroup_generator_active()
+        override_subgroup_generator()
+        return self
+
+    def __exit__(self, *exc):
+        if not self._prev:
+            restore_subgroup_generator()
+        return False
+
+
 class Radix2EvaluationDomain:
     def __init__(self, num_coeffs: int, _handle=None):
         L = lib()

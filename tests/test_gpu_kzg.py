@@ -67,7 +67,21 @@ def test_batch_and_downsize():
     assert not kzg.downsize(n)
     assert kzg.downsize(n // 2) and kzg.N() == n // 2
     assert len(kzg.g1_powers_of_tau()) == (n // 2) * 64
+    # more scalars than N: the reference's Commit / CommitLagrange return false
+    assert kzg.commit(polys[0]) is None and kzg.commit_lagrange(polys[0]) is None
+    assert kzg.commit(polys[0][:32 * (n // 2)]) is not None
     del Fr
+    kzg.close()
+
+
+def test_commit_longer_than_srs_and_before_setup():
+    from tachyon_amd.kzg import KZG
+    kzg = KZG("bn254_g1")
+    one = pyref.Field("bn254_fr").to_bytes(1)
+    assert kzg.commit(one) is None  # no setup: N = 0
+    kzg.unsafe_setup(4, pyref.Field("bn254_fr").to_bytes(5))
+    assert kzg.commit(one * 5) is None and kzg.commit_lagrange(one * 5) is None
+    assert kzg.commit(one * 4) is not None
     kzg.close()
 
 
