@@ -8,15 +8,20 @@ with the BN254 Fr NTT elems/s at 2^24 (configs[2]) reported beside it.
 A step is one full MSM over 2^26 points whose bases/scalars are already in
 HBM (generated on the device, seeded).  With N GPUs the 2^26 points are split
 into N contiguous shards (the reference's kParallelTerm chunking,
-pippenger_adapter.h:82-113); every rank runs the MI355X MSM on its shard and
-the per-rank partial points are combined with one RCCL all-gather plus a host
-group sum (EC addition is not an RCCL reduction op).  `value` = 2^26 / the
-slowest rank's time per step (strong scaling).
+pippenger_adapter.h:82-113) of ONE global input (every rank generates its
+slice of the same seeded sequence); every rank runs the MI355X MSM on its
+shard and the per-rank partial points are combined with one RCCL all-gather
+plus a host group sum (EC addition is not an RCCL reduction op).  `value` =
+2^26 / the slowest rank's time per step (strong scaling); at N > 1 rank 0
+also runs the unsharded MSM once and the line says whether they agree.
 
 The roofline object prices the dominant kernel (bucket accumulation) with
-HIP events recorded on the MSM stream around that launch; the cpu_baseline
-object times the oracle's CPU restatement of PippengerAdapter (rank 0, N=1
-only) on a bounded sample.
+HIP events recorded on the MSM stream around that launch.  `host_resident`
+times the reference semantics (pageable host inputs, H2D + kernels + D2H
+inside the call, msm_runner.h:54-58 / fft_runner.h:53-58).  The cpu_baseline
+object times the oracle's CPU restatement of PippengerAdapter kParallelTerm
+and Radix2EvaluationDomain (rank 0, N=1 only) at the headline sizes on the
+same inputs, and checks that the GPU results equal the CPU ones.
 """
 import argparse
 import json
@@ -51,8 +56,9 @@ def pmc_traffic(kernel):
         except (OSError, ValueError):
             continue
         if kernel in t:
-            return t[kernel]["traffic_bytes"] / 1e9, os.path.relpath(f, ROOT)
-    return None, None
+            k = t[kernel]
+            return k["traffic_bytes"] / 1e9, os.path.relpath(f, ROOT), k.get("fetch_bytes_raw", 0) / 1e9
+    return None, None, None
 
 
 def parse():
@@ -65,7 +71,9 @@ def parse():
     ap.add_argument("--window-bits", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ntt", action="store_true")
-    ap.add_argument("--cpu-sample-log-n", type=int, default=22)
+    ap.add_argument("--cpu-log-n", type=int, default=0,
+                    help="CPU baseline MSM size (0 = the headline --log-n)")
+    ap.add_argument("--no-host-resident", action="store_true")
     ap.add_argument("--bls-log-n", type=int, default=24,
                     help="BLS12-381 G1 + G2 MSM size (BASELINE configs[3]); 0 = skip")
     ap.add_argument("--groth16-log-n", type=int, default=20,
@@ -83,31 +91,53 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_baseline(args):
-    """Oracle restatement of the reference CPU path, bounded sample."""
+def cpu_threads():
+    """Host threads this job may use: the box's CPU share (OMP_NUM_THREADS is
+    set to it on the GPU pool) or else the affinity mask."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(avail, int(env))) if env and env.isdigit() else avail
+
+
+def cpu_baseline(args, h_bases, h_scalars, gpu_affine, ntt_in, gpu_ntt_out):
+    """The oracle's C restatement of the reference CPU path, timed on the host
+    cores at the headline sizes on the SAME inputs as the GPU legs (copied
+    from HBM), one run per size as the reference's runners do; it also
+    cross-checks the GPU results.  configs[0] (2^16, benchmark/msm's CPU
+    path) is timed beside it."""
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    n = 1 << args.cpu_sample_log_n
-    bases = O.gen_bases("bn254_g1", SEED, n, max(1, n // threads))
-    scalars = O.gen_scalars("bn254_fr", SEED, n)
+    threads = cpu_threads()
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    n = h_scalars.nbytes // 32
     t0 = time.perf_counter()
-    O.msm_np("bn254_g1", bases, scalars, method="parallel_term", threads=threads)
+    cpu_point = O.msm_np("bn254_g1", h_bases, h_scalars, method="parallel_term", threads=threads)
     dt = time.perf_counter() - t0
+    m16 = 1 << 16
+    t1 = time.perf_counter()
+    O.msm_np("bn254_g1", h_bases[:m16 * 64], h_scalars[:m16 * 32], method="parallel_term", threads=threads)
+    dt16 = time.perf_counter() - t1
     out = {"value": n / dt, "unit": "scalars/s", "cores": threads, "kind": "port",
-           "sample": f"BN254 G1 MSM 2^{args.cpu_sample_log_n} points, PippengerAdapter kParallelTerm restated "
-                     f"in C (oracle/), {threads} OpenMP threads, {cpu_model()}; portable CIOS field "
-                     f"(the reference's x86 ffiasm asm field is unavailable)",
-           "seconds": dt}
-    if not args.no_ntt:
+           "sample": f"BN254 G1 MSM 2^{n.bit_length() - 1} points (the headline size, the bench's own inputs), "
+                     f"PippengerAdapter kParallelTerm restated in C (oracle/), {threads} OpenMP threads "
+                     f"(the job's CPU share; {os.cpu_count()} CPUs visible), {cpu_model()}; portable CIOS "
+                     f"field (the reference's x86 ffiasm asm field is unavailable)",
+           "seconds": dt, "gpu_equals_cpu": cpu_point == gpu_affine,
+           "configs0": {"workload": "BN254 G1 MSM 2^16, CPU path (BASELINE configs[0])", "seconds": dt16,
+                        "value": m16 / dt16, "unit": "scalars/s"}}
+    if ntt_in is not None:
         import numpy as np
-        m = 1 << min(args.ntt_log_n, 22)
-        v = O.gen_scalars("bn254_fr", SEED + 1, m)
+        v = ntt_in.copy()
+        m = v.nbytes // 32
         t0 = time.perf_counter()
-        O.fft_np(v)
+        O.fft_np(v.view(np.uint64))
         dt2 = time.perf_counter() - t0
-        out["ntt"] = {"value": m / dt2, "unit": "elems/s", "sample": f"BN254 Fr FFT 2^{int(np.log2(m))}, "
-                      f"Radix2EvaluationDomain restated in C, {threads} threads", "seconds": dt2}
+        out["ntt"] = {"value": m / dt2, "unit": "elems/s", "seconds": dt2,
+                      "sample": f"BN254 Fr FFT 2^{m.bit_length() - 1} (the headline size, the bench's input), "
+                                f"Radix2EvaluationDomain restated in C, {threads} threads",
+                      "gpu_equals_cpu": gpu_ntt_out is not None and v.tobytes() == gpu_ntt_out.tobytes()}
     return out
 
 
@@ -178,7 +208,7 @@ def bench_bls(args, rank, world, barrier, dist, backend):
     for curve, pb in (("bls12_381_g1", 96), ("bls12_381_g2", 192)):
         d_b = torch.empty(max(1, n) * pb, dtype=torch.uint8, device="cuda")
         d_s = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
-        M.gen_bases(curve, SEED + rank, n, 1 << 10, d_b.data_ptr())
+        M.gen_bases(curve, SEED, n, 1 << 10, d_b.data_ptr(), start=start)  # this rank's slice of one input
         M.gen_scalars("bls12_381_fr", SEED, n, d_s.data_ptr(), start=start)
         torch.cuda.synchronize()
         msm = M.VariableBaseMSMGpu(curve)
@@ -202,9 +232,35 @@ def bench_bls(args, rank, world, barrier, dist, backend):
                                      "consistent": res == ref, "points_per_gpu": n}
         msm.close()
         del d_b, d_s
+        if world > 1:  # the sharded MSM must equal the unsharded one
+            out[curve.split("_")[-1]]["consistent_with_1gpu"] = full_msm_equals(curve, n_total, res, rank, dist)
     out["workload"] = (f"BLS12-381 G1 and G2 VariableBaseMSM 2^{args.bls_log_n} (BASELINE configs[3]), "
                        f"device-resident inputs, point shards x{world} + all-gather of partials")
     return out
+
+
+def full_msm_equals(curve, n_total, sharded, rank, dist):
+    """Rank 0 runs the unsharded MSM of the same global input once; every rank
+    learns whether the sharded result equals it."""
+    import torch
+    from tachyon_amd import msm as M
+    from tachyon_amd._lib import CURVE_INFO
+    ok = 1
+    if rank == 0:
+        pb, sf = CURVE_INFO[curve]
+        d_b = torch.empty(n_total * pb, dtype=torch.uint8, device="cuda")
+        d_s = torch.empty(n_total * 32, dtype=torch.uint8, device="cuda")
+        M.gen_bases(curve, SEED, n_total, 1 << 10, d_b.data_ptr())
+        M.gen_scalars(sf, SEED, n_total, d_s.data_ptr())
+        torch.cuda.synchronize()
+        m = M.VariableBaseMSMGpu(curve)
+        ok = int(m.run(d_b, d_s, n_total) == sharded)
+        m.close()
+        del d_b, d_s
+        torch.cuda.empty_cache()
+    t = torch.tensor([ok], dtype=torch.int32, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.broadcast(t, 0)
+    return bool(t.item())
 
 
 def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backend=None):
@@ -297,7 +353,8 @@ def main():
     d_bases = torch.empty(max(1, n) * 64, dtype=torch.uint8, device="cuda")
     d_scalars = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
     chunk = 1 << 10
-    M.gen_bases("bn254_g1", SEED + rank, n, chunk, d_bases.data_ptr())  # per-rank seeded doubling chains
+    # this rank's slice [start, start + n) of ONE seeded global input
+    M.gen_bases("bn254_g1", SEED, n, chunk, d_bases.data_ptr(), start=start)
     M.gen_scalars("bn254_fr", SEED, n, d_scalars.data_ptr(), start=start)
     torch.cuda.synchronize()
 
@@ -322,6 +379,7 @@ def main():
     consistent = all(r == results[0] for r in results) and (args.warmup == 0 or results[0] == ref)
     ms_per_step = elapsed / args.steps * 1e3
     value = n_total / (elapsed / args.steps)
+    consistent_1gpu = full_msm_equals("bn254_g1", n_total, results[0], rank, dist) if world > 1 else None
 
     # ---- dominant-kernel timing (HIP events on the MSM stream) ----
     msm.set_profile(True)
@@ -332,13 +390,15 @@ def main():
     msm.set_profile(False)
     phases = {k: round(sorted(p[k] for p in prof)[1], 4) for k in prof[0]}
     launches = max(1, int(prof[0]["acc_launches"]))
-    # the accumulation runs as `launches` equal launches (one per window);
-    # each processes every point's digit of its window: n/launches point-units
     acc_ms = sorted(p["acc"] for p in prof)[1] / launches
-    acc_gbs = n / launches * MSM_BYTES_PER_POINT / (acc_ms * 1e-3) / 1e9
     c, windows = M.plan("bn254_g1", n)
-    acc_traffic, acc_traffic_src = pmc_traffic("seg_acc_kernel")
-    acc_gmulmod = n * windows / launches * MADD_MULMODS / (acc_ms * 1e-3) / 1e9
+    # one launch accumulates every (point, window) digit of the windows it
+    # covers: n x windows / launches point-window units of 96 B each (the
+    # point's base + scalar bytes, consumed once per window)
+    units = n * windows / launches
+    acc_gbs = units * MSM_BYTES_PER_POINT / (acc_ms * 1e-3) / 1e9
+    acc_traffic, acc_traffic_src, acc_traffic_raw = pmc_traffic("seg_acc_kernel")
+    acc_gmulmod = units * MADD_MULMODS / (acc_ms * 1e-3) / 1e9
 
     out = {
         "metric": METRIC,
@@ -359,13 +419,19 @@ def main():
                    "msm_log_n": args.log_n, "points_per_gpu": n, "window_bits": c, "windows": windows,
                    "parallelism": f"msm point shards x{world} + RCCL all-gather of partial points"},
         "consistent_across_steps": consistent,
+        "consistent_with_1gpu": consistent_1gpu,
         "roofline": {"bound": "hbm", "achieved": acc_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": acc_gbs / HBM_PEAK_GBS,
                      "traffic": acc_traffic, "traffic_unit": "GB per launch", "traffic_source": acc_traffic_src,
-                     "kernel": "seg_acc_kernel (bucket accumulation, madd-2008-s)", "kernel_ms": acc_ms,
-                     "launches_per_msm": launches,
-                     "note": "algorithmic bytes = 96 B/point x n/launches point-units per launch (one window "
-                             "per launch); the kernel is VALU-bound (v_mad_u64_u32), see DESIGN.md"},
+                     "traffic_fetch_raw": acc_traffic_raw,
+                     "traffic_correction": "FETCH_SIZE x2 (the guide's factor for wide coalesced streaming reads) "
+                                           "+ WRITE_SIZE; the 64-B base gathers are an uncalibrated width, so the "
+                                           "uncorrected FETCH_SIZE is given as traffic_fetch_raw",
+                     "pmc_gbs": (acc_traffic / (acc_ms * 1e-3)) if acc_traffic else None,
+                     "kernel": "seg_acc_kernel (bucket accumulation)", "kernel_ms": acc_ms,
+                     "launches_per_msm": launches, "units_per_launch": units,
+                     "note": "algorithmic bytes = 96 B per (point, window) unit x n x windows / launches; the "
+                             "kernel is VALU-bound (v_mad_u64_u32), see DESIGN.md"},
         "msm_phase_ms": phases,
         "valu_roofline": {"bound": "valu", "kernel": "seg_acc_kernel", "achieved": acc_gmulmod,
                           "peak": MULMOD_PEAK_G, "unit": "G mulmod/s", "frac": acc_gmulmod / MULMOD_PEAK_G,
@@ -428,11 +494,14 @@ def main():
         round_trip_ok = bool(torch.equal(x, orig))
         dom.set_profile(True)
         dom.transform_device(x.data_ptr(), inverse=False)
+        s.synchronize()
         tot, passes = dom.last_timings()
         dom.set_profile(False)
+        ntt_in = orig.cpu().numpy()
+        ntt_gpu_out = x.cpu().numpy()  # FFT of the input (the round trips left x == orig)
         avg_pass = sum(passes) / len(passes)
         pass_gbs = nn * NTT_BYTES_PER_ELEM / (avg_pass * 1e-3) / 1e9
-        ntt_traffic, ntt_traffic_src = pmc_traffic("dif_pass_kernel")
+        ntt_traffic, ntt_traffic_src, _ = pmc_traffic("dif_pass_kernel")
         # algorithmic butterflies (one Montgomery product each) per pass: n/2 x log n / passes
         ntt_gmulmod = nn // 2 * args.ntt_log_n / len(passes) / (avg_pass * 1e-3) / 1e9
         out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
@@ -446,6 +515,21 @@ def main():
                                         "frac": ntt_gmulmod / MULMOD_PEAK_G,
                                         "note": "n/2 x log n butterflies per transform / passes, one product "
                                                 "each (the add/sub of a butterfly are not counted)"}}
+        if not args.no_host_resident:
+            # reference semantics (fft_runner.h:53-58): host vector in, H2D + transform + D2H
+            hv = ntt_in.copy()
+            dom.transform_host(hv)
+            same = hv.tobytes() == ntt_gpu_out.tobytes()
+            ts = []
+            for _ in range(3):
+                hv[:] = ntt_in
+                t0 = time.perf_counter()
+                dom.transform_host(hv)
+                ts.append(time.perf_counter() - t0)
+            out["ntt"]["host_resident"] = {"value": nn / min(ts), "unit": "elems/s", "ms": min(ts) * 1e3,
+                                           "ms_median": sorted(ts)[1] * 1e3, "equals_device_path": same,
+                                           "path": "IcicleNTT::Run semantics on a pageable host vector "
+                                                   "(..._evaluation_domain_transform_host)"}
         dom.close()
 
     if args.bls_log_n:
@@ -454,8 +538,31 @@ def main():
     if args.groth16_log_n:
         out["groth16"] = bench_groth16(args, rank, world, barrier, dist, backend)
 
+    h_bases = h_scalars = None
+    if world == 1 and not (args.no_host_resident and args.no_cpu_baseline):
+        h_bases, h_scalars = d_bases.cpu().numpy(), d_scalars.cpu().numpy()
+    if world == 1 and not args.no_host_resident:
+        # reference semantics (msm_runner.h:54-58): pageable host vectors through
+        # tachyon_bn254_g1_affine_msm_gpu, H2D + kernels + D2H inside the call
+        jac = msm.run_jacobian(h_bases, h_scalars, n)
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            msm.run_jacobian(h_bases, h_scalars, n)
+            ts.append(time.perf_counter() - t0)
+        out["host_resident"] = {"value": n_total / min(ts), "unit": "scalars/s", "ms": min(ts) * 1e3,
+                                "ms_median": sorted(ts)[1] * 1e3,
+                                "equals_device_path": M.jacobian_to_affine("bn254_g1", jac) == results[0],
+                                "path": "tachyon_bn254_g1_affine_msm_gpu on pageable host vectors "
+                                        "(reference C-ABI, H2D inside the timed call)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args)
+        nb, ns = h_bases, h_scalars
+        if args.cpu_log_n and args.cpu_log_n < args.log_n:
+            nb, ns = h_bases[:(1 << args.cpu_log_n) * 64], h_scalars[:(1 << args.cpu_log_n) * 32]
+        gpu_point = results[0] if nb is h_bases else msm.run(nb, ns)
+        nin = ntt_in if not args.no_ntt else None
+        nout = ntt_gpu_out if not args.no_ntt else None
+        out["cpu_baseline"] = cpu_baseline(args, nb, ns, gpu_point, nin, nout)
 
     if rank == 0:
         print(json.dumps(out), flush=True)

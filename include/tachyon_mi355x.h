@@ -264,6 +264,19 @@ TACHYON_C_EXPORT tachyon_bls12_381_g2_jacobian* tachyon_bls12_381_g2_affine_msm_
 /* Affine result written to out_affine (identity = all zero bytes). */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const void* bases, const void* scalars,
                                                     size_t size, void* out_affine);
+/* Contexts for the C++ plugin boundary (include/tachyon_mi355x_msm.h):
+ * VariableBaseMSMGpu<Point>(mem_pool, stream) (variable_base_msm_gpu.h:16-18)
+ * over any of the four groups, its work on `stream` (hipStream_t; NULL = a
+ * stream the context owns; the call returns with the stream synchronised).
+ * _run: the MSM of bases[0..n) and scalars[0..n) (host or device pointers)
+ * written as `form` -- 0 affine {x,y}; 1 projective / 2 jacobian {x,y,z},
+ * identity (1,1,0); 3 xyzz {x,y,zz,zzz}, identity (1,1,0,0).  Returns 1, or
+ * 0 (out untouched) when bases_size != scalars_size, as IcicleMSM::Run
+ * (icicle_msm_bn254_g1.cc:30-33) and PippengerAdapter (:55-59) return false. */
+TACHYON_C_EXPORT void* tachyon_mi355x_msm_gpu_create(int curve, void* stream);
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_destroy(int curve, void* ctx);
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void* bases, size_t bases_size,
+                                               const void* scalars, size_t scalars_size, int form, void* out);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule).
@@ -295,6 +308,10 @@ TACHYON_C_EXPORT void tachyon_mi355x_gen_scalars(int field, uint64_t seed, size_
                                                  void* stream);
 TACHYON_C_EXPORT void tachyon_mi355x_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* d_out,
                                                void* stream);
+/* points [start, start + n) of that same sequence (start a multiple of chunk):
+ * a rank's shard of the global input, so N ranks compute the N = 1 MSM. */
+TACHYON_C_EXPORT void tachyon_mi355x_gen_bases_at(int curve, uint64_t seed, size_t start, size_t n, size_t chunk,
+                                                  void* d_out, void* stream);
 
 /* Elementwise device parity kernels (prime_field_correctness_gpu_test.cc,
  * (non_)affine_point_correctness_gpu_test.cc).  field: 0 bn254_fq, 1 bn254_fr,

@@ -100,6 +100,9 @@ SIGNATURES = [
     ("tachyon_bls12_381_g2_destroy_msm_gpu", None, [vp]),
     ("tachyon_bls12_381_g2_affine_msm_gpu", vp, [vp, vp, vp, sz]),
     ("tachyon_mi355x_msm_gpu_affine", None, [i32, vp, vp, vp, sz, vp]),
+    ("tachyon_mi355x_msm_gpu_create", vp, [i32, vp]),
+    ("tachyon_mi355x_msm_gpu_destroy", None, [i32, vp]),
+    ("tachyon_mi355x_msm_gpu_run", i32, [i32, vp, vp, sz, vp, sz, i32, vp]),
     ("tachyon_mi355x_msm_gpu_set_window_bits", None, [i32, vp, ctypes.c_uint]),
     ("tachyon_mi355x_msm_gpu_set_profile", None, [i32, vp, i32]),
     ("tachyon_mi355x_msm_gpu_set_variant", i32, [i32, vp, i32]),
@@ -110,6 +113,7 @@ SIGNATURES = [
     ("tachyon_mi355x_jacobian_to_affine", None, [i32, vp, vp]),
     ("tachyon_mi355x_gen_scalars", None, [i32, u64, sz, sz, vp, vp]),
     ("tachyon_mi355x_gen_bases", None, [i32, u64, sz, sz, vp, vp]),
+    ("tachyon_mi355x_gen_bases_at", None, [i32, u64, sz, sz, sz, vp, vp]),
     ("tachyon_mi355x_field_op", None, [i32, i32, vp, vp, vp, sz]),
     ("tachyon_mi355x_ec_op", None, [i32, i32, vp, vp, vp, sz]),
     ("tachyon_mi355x_groth16_prover_create", vp, [vp, sz]),

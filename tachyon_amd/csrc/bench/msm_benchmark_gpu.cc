@@ -3,6 +3,7 @@
 //
 //   msm_benchmark_gpu -k 16 -k 20 ... [--test_set random|non_uniform]
 //                     [--check_results] [--device_resident] [--curve bn254|bls12_381]
+//                     [--expect FILE]
 //
 // Kept from the reference (msm_benchmark_gpu.cc:20-75, msm_config.cc:39-82,
 // msm_runner.h:45-61): sizes 2^k sorted ascending, one timed call per size
@@ -16,10 +17,14 @@
 // Stated differences: one untimed warm-up call at the largest size precedes
 // the sweep (module load, buffer growth); --device_resident times the same
 // entry point on HBM inputs (the reference's device-pointer path,
-// icicle_msm_bn254_g1.cc:37-45); --check_results cannot compare with a CPU MSM
-// (the library has none) and checks the chunk-sum invariance of
-// pippenger_adapter_unittest.cc instead: MSM(first half) + MSM(second half)
-// == MSM(all).  The oracle-backed tests pin the MSM itself.
+// icicle_msm_bn254_g1.cc:37-45).  --check_results: the reference compares the
+// GPU point with its CPU MSM of the same inputs (msm_benchmark_gpu.cc:57-70).
+// The product links no CPU MSM, so the CPU results come in through --expect
+// FILE: per size (ascending) the affine CPU result of the first 2^k inputs
+// (tests/test_gpu_harness.py writes it with the CPU oracle, which it also
+// times).  Without --expect, --check_results checks the chunk-sum invariance
+// of pippenger_adapter_unittest.cc: MSM(first half) + MSM(second half) ==
+// MSM(all).  Inputs: seed 0x7AC40001, base chains of 2^10 (gen_bases).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,7 +49,7 @@ void hip_check(hipError_t e, const char* what) {
 
 int usage() {
   std::cerr << "usage: msm_benchmark_gpu -k K [-k K ...] [--test_set random|non_uniform] [--check_results]\n"
-               "                         [--device_resident] [--curve bn254|bls12_381]\n";
+               "                         [--device_resident] [--curve bn254|bls12_381] [--expect FILE]\n";
   return 1;
 }
 
@@ -64,7 +69,7 @@ void* reference_msm(bool bls, void* msm, const void* bases, const void* scalars,
 int main(int argc, char** argv) {
   std::vector<unsigned> ks;
   bool non_uniform = false, check = false, device_resident = false;
-  std::string curve = "bn254";
+  std::string curve = "bn254", expect_path;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "-k" && i + 1 < argc) ks.push_back((unsigned)std::stoul(argv[++i]));
@@ -75,6 +80,7 @@ int main(int argc, char** argv) {
     } else if (a == "--check_results") check = true;
     else if (a == "--device_resident") device_resident = true;
     else if (a == "--curve" && i + 1 < argc) curve = argv[++i];
+    else if (a == "--expect" && i + 1 < argc) expect_path = argv[++i];
     else return usage();
   }
   if (ks.empty() || (curve != "bn254" && curve != "bls12_381")) return usage();
@@ -83,6 +89,18 @@ int main(int argc, char** argv) {
   const int curve_id = bls ? 2 : 0, field_id = bls ? 3 : 1;
   const size_t pb = bls ? 96 : 64, sb = 32;
   const size_t n_max = size_t(1) << ks.back();
+  std::vector<uint8_t> expect;
+  if (!expect_path.empty()) {
+    FILE* f = fopen(expect_path.c_str(), "rb");
+    if (!f) return usage();
+    expect.resize(ks.size() * pb);
+    const size_t got = fread(expect.data(), 1, expect.size(), f);
+    fclose(f);
+    if (got != expect.size()) {
+      std::cerr << "--expect file must hold " << ks.size() << " affine points" << std::endl;
+      return 1;
+    }
+  }
 
   std::cout << "Generating random points..." << std::endl;
   void *d_bases = nullptr, *d_scalars = nullptr;
@@ -115,14 +133,20 @@ int main(int argc, char** argv) {
 
   std::vector<double> secs;
   bool ok = true;
-  for (unsigned k : ks) {
+  for (size_t ki = 0; ki < ks.size(); ++ki) {
+    const unsigned k = ks[ki];
     const size_t n = size_t(1) << k;
     auto t0 = std::chrono::steady_clock::now();
     void* r = reference_msm(bls, msm, bases, scalars, n);
     secs.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     tachyon_mi355x_jacobian_to_affine(curve_id, r, res.data());
     tachyon_mi355x_jacobian_destroy(curve_id, r);
-    if (check) {
+    if (check && !expect.empty()) {  // CHECK_EQ(cpu result, gpu result)
+      if (memcmp(res.data(), expect.data() + ki * pb, pb) != 0) {
+        std::cerr << "Results not matched at 2^" << k << std::endl;
+        ok = false;
+      }
+    } else if (check) {
       const size_t h = n / 2;
       tachyon_mi355x_msm_gpu_affine(curve_id, msm, bases, scalars, h, half.data());
       tachyon_mi355x_msm_gpu_affine(curve_id, msm, bases + h * pb, scalars + h * sb, n - h, half.data() + pb);
@@ -143,9 +167,9 @@ int main(int argc, char** argv) {
   printf("\n%-22s", "scalars/s");
   for (size_t i = 0; i < ks.size(); ++i) printf("%14.4g", (double)(size_t(1) << ks[i]) / secs[i]);
   printf("\n{\"benchmark\": \"msm\", \"curve\": \"%s_g1\", \"test_set\": \"%s\", \"device_resident\": %s, "
-         "\"check_results\": %s, \"results\": [",
+         "\"check_results\": %s, \"checked_against\": \"%s\", \"results\": [",
          curve.c_str(), non_uniform ? "non_uniform" : "random", device_resident ? "true" : "false",
-         check ? (ok ? "\"pass\"" : "\"FAIL\"") : "null");
+         check ? (ok ? "\"pass\"" : "\"FAIL\"") : "null", expect.empty() ? "chunk_sum" : "expect_file");
   for (size_t i = 0; i < ks.size(); ++i) printf("%s{\"k\": %u, \"seconds\": %.6f}", i ? ", " : "", ks[i], secs[i]);
   printf("]}\n");
 

@@ -44,7 +44,7 @@ struct MsmCtx {
   std::string input_dir;  // TACHYON_MSM_GPU_INPUT_DIR
   bool log = false;       // TACHYON_LOG_MSM=1
   size_t idx = 0;
-  MsmCtx() {
+  explicit MsmCtx(hipStream_t stream = nullptr) : impl(stream) {
     if (const char* d = getenv("TACHYON_MSM_GPU_INPUT_DIR")) input_dir = d;
     if (const char* l = getenv("TACHYON_LOG_MSM")) log = (std::string(l) == "1");
   }
@@ -140,6 +140,36 @@ void msm_affine_out(void* ctx, const void* bases, const void* scalars, size_t n,
   auto* c = static_cast<MsmCtx<Curve>*>(ctx);
   Affine<F> a = c->impl.run(bases, scalars, n).to_affine();
   memcpy(out, &a, sizeof(a));
+}
+
+// The MSM in the point form a C++ caller asks for (include/tachyon_mi355x_msm.h):
+// 0 affine {x, y} ((0, 0) = identity); 1 projective / 2 Jacobian {x, y, z}
+// (identity (1, 1, 0), projective_point.h:34-36, jacobian_point.h; otherwise
+// z = 1); 3 XYZZ {x, y, zz, zzz} (identity (1, 1, 0, 0), point_xyzz.h:37-39) --
+// the Bucket of VariableBaseMSM<AffinePoint> (pippenger_base.h:24-28).
+template <class Curve>
+void msm_form_out(void* ctx, const void* bases, const void* scalars, size_t n, int form, void* out) {
+  using F = typename Curve::F;
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  const Affine<F> a = c->impl.run(bases, scalars, n).to_affine();
+  switch (form) {
+    case 0:
+      memcpy(out, &a, sizeof(a));
+      break;
+    case 1:
+    case 2: {
+      const Jacobian<F> j = a.is_zero() ? Jacobian<F>::zero() : Jacobian<F>{a.x, a.y, F::one()};
+      memcpy(out, &j, sizeof(j));
+      break;
+    }
+    case 3: {
+      const XYZZ<F> p = XYZZ<F>::from_affine(a);
+      memcpy(out, &p, sizeof(p));
+      break;
+    }
+    default:
+      throw std::runtime_error("point form must be 0 (affine), 1 (projective), 2 (jacobian) or 3 (xyzz)");
+  }
 }
 
 template <class Curve>
@@ -298,6 +328,20 @@ void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const void* bases, cons
                                    void* out_affine) {
   GUARD_BEGIN CURVE_DISPATCH(curve, msm_affine_out<C>(ctx, bases, scalars, size, out_affine)) GUARD_END
 }
+void* tachyon_mi355x_msm_gpu_create(int curve, void* stream) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, return new MsmCtx<C>(static_cast<hipStream_t>(stream))) GUARD_END
+  return nullptr;
+}
+void tachyon_mi355x_msm_gpu_destroy(int curve, void* ctx) {
+  if (!ctx) return;
+  GUARD_BEGIN CURVE_DISPATCH(curve, delete static_cast<MsmCtx<C>*>(ctx)) GUARD_END
+}
+int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void* bases, size_t bases_size, const void* scalars,
+                               size_t scalars_size, int form, void* out) {
+  if (bases_size != scalars_size) return 0;  // IcicleMSM::Run / PippengerAdapter: sizes must match
+  GUARD_BEGIN CURVE_DISPATCH(curve, msm_form_out<C>(ctx, bases, scalars, scalars_size, form, out)) GUARD_END
+  return 1;
+}
 void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c) {
   GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_force_window_bits(c)) GUARD_END
 }
@@ -338,7 +382,11 @@ void tachyon_mi355x_gen_scalars(int field, uint64_t seed, size_t start, size_t n
   GUARD_BEGIN util::gen_scalars(field, seed, start, n, d_out, static_cast<hipStream_t>(stream)); GUARD_END
 }
 void tachyon_mi355x_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* d_out, void* stream) {
-  GUARD_BEGIN util::gen_bases(curve, seed, n, chunk, d_out, static_cast<hipStream_t>(stream)); GUARD_END
+  GUARD_BEGIN util::gen_bases(curve, seed, 0, n, chunk, d_out, static_cast<hipStream_t>(stream)); GUARD_END
+}
+void tachyon_mi355x_gen_bases_at(int curve, uint64_t seed, size_t start, size_t n, size_t chunk, void* d_out,
+                                 void* stream) {
+  GUARD_BEGIN util::gen_bases(curve, seed, start, n, chunk, d_out, static_cast<hipStream_t>(stream)); GUARD_END
 }
 void tachyon_mi355x_field_op(int field, int op, const void* a, const void* b, void* out, size_t count) {
   GUARD_BEGIN util::field_op(field, op, a, b, out, count); GUARD_END

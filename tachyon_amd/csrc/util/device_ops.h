@@ -10,7 +10,8 @@
 namespace tachyon_amd::util {
 
 void gen_scalars(int field, uint64_t seed, size_t start, size_t n, void* d_out, hipStream_t stream);
-void gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* d_out, hipStream_t stream);
+// points [start, start + n) of the seeded sequence (start a multiple of chunk)
+void gen_bases(int curve, uint64_t seed, size_t start, size_t n, size_t chunk, void* d_out, hipStream_t stream);
 void field_op(int field, int op, const void* a, const void* b, void* out, size_t count);
 void ec_op(int curve, int op, const void* a, const void* b, void* out, size_t count);
 

@@ -95,7 +95,7 @@ struct Gen<Bls381G2> {
 // each point normalised to affine (per-point inversion; a one-off setup cost).
 template <class Curve>
 __global__ __launch_bounds__(kBlock) void gen_bases_kernel(uint64_t seed, uint64_t n, uint64_t chunk,
-                                                           Affine<typename Curve::F>* out) {
+                                                           uint64_t chunk0, Affine<typename Curve::F>* out) {
   using F = typename Curve::F;
   using Fr = typename Curve::Fr;
   uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -104,7 +104,7 @@ __global__ __launch_bounds__(kBlock) void gen_bases_kernel(uint64_t seed, uint64
   uint64_t len = min(chunk, n - start);
   Affine<F> G{load_generator_coord<F>(Gen<Curve>::x()), load_generator_coord<F>(Gen<Curve>::y())};
   uint64_t k[4];
-  rand_scalar<Fr>(seed ^ kBaseSeedXor, j, k);
+  rand_scalar<Fr>(seed ^ kBaseSeedXor, chunk0 + j, k);  // chunk0: global index of this call's first chunk
   XYZZ<F> r = XYZZ<F>::zero();
   for (int limb = 3; limb >= 0; --limb)
     for (int bit = 63; bit >= 0; --bit) {
@@ -194,19 +194,21 @@ void gen_scalars(int field, uint64_t seed, size_t start, size_t n, void* d_out, 
   TA_HIP(hipGetLastError());
 }
 
-void gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* d_out, hipStream_t stream) {
+void gen_bases(int curve, uint64_t seed, size_t start, size_t n, size_t chunk, void* d_out, hipStream_t stream) {
   if (n == 0) return;
   if (chunk == 0) throw std::runtime_error("tachyon_mi355x_gen_bases: chunk must be > 0");
+  if (start % chunk) throw std::runtime_error("tachyon_mi355x_gen_bases_at: start must be a multiple of chunk");
+  const uint64_t chunk0 = start / chunk;
   size_t chunks = (n + chunk - 1) / chunk;
   dim3 g(ceil_div(chunks, kBlock)), b(kBlock);
   switch (curve) {
-    case 0: hipLaunchKernelGGL(gen_bases_kernel<Bn254G1>, g, b, 0, stream, seed, n, chunk,
+    case 0: hipLaunchKernelGGL(gen_bases_kernel<Bn254G1>, g, b, 0, stream, seed, n, chunk, chunk0,
                                static_cast<Affine<Bn254Fq>*>(d_out)); break;
-    case 1: hipLaunchKernelGGL(gen_bases_kernel<Bn254G2>, g, b, 0, stream, seed, n, chunk,
+    case 1: hipLaunchKernelGGL(gen_bases_kernel<Bn254G2>, g, b, 0, stream, seed, n, chunk, chunk0,
                                static_cast<Affine<Bn254Fq2>*>(d_out)); break;
-    case 2: hipLaunchKernelGGL(gen_bases_kernel<Bls381G1>, g, b, 0, stream, seed, n, chunk,
+    case 2: hipLaunchKernelGGL(gen_bases_kernel<Bls381G1>, g, b, 0, stream, seed, n, chunk, chunk0,
                                static_cast<Affine<Bls381Fq>*>(d_out)); break;
-    case 3: hipLaunchKernelGGL(gen_bases_kernel<Bls381G2>, g, b, 0, stream, seed, n, chunk,
+    case 3: hipLaunchKernelGGL(gen_bases_kernel<Bls381G2>, g, b, 0, stream, seed, n, chunk, chunk0,
                                static_cast<Affine<Bls381Fq2>*>(d_out)); break;
     default: throw std::runtime_error("tachyon_mi355x_gen_bases: unknown curve");
   }

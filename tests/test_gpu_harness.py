@@ -28,6 +28,72 @@ def test_msm_benchmark_gpu(flags):
     assert [r["k"] for r in res["results"]] == [10, 12]
 
 
+SEED = 0x7AC40001
+
+
+@pytest.mark.parametrize("curve,ks,flags", [
+    ("bn254", [10, 16], []),                          # 2^16 = BASELINE configs[0]'s size
+    ("bn254", [12], ["--test_set", "non_uniform"]),
+    ("bn254", [11], ["--device_resident"]),
+    ("bls12_381", [10], []),
+])
+def test_msm_benchmark_gpu_vs_cpu_oracle(tmp_path, curve, ks, flags):
+    """--check_results as the reference does it (msm_benchmark_gpu.cc:57-70):
+    the GPU point of every size equals the CPU MSM (here the oracle's
+    kParallelTerm Pippenger on the same inputs, timed beside it)."""
+    import time
+    from oracle import oracle as O
+    g1 = f"{curve}_g1"
+    pb, sf = O.CURVE_INFO[g1]
+    n_max = 1 << max(ks)
+    bases = O.gen_bases(g1, SEED, n_max, 1 << 10).tobytes()
+    scalars = O.gen_scalars(sf, SEED, n_max).tobytes()
+    if "non_uniform" in flags:
+        scalars = scalars[:32] * n_max
+    expect, cpu_s = b"", {}
+    for k in sorted(ks):
+        n = 1 << k
+        t0 = time.perf_counter()
+        expect += O.msm(g1, bases[:n * pb], scalars[:n * 32])[0]
+        cpu_s[k] = time.perf_counter() - t0
+    (tmp_path / "expect.bin").write_bytes(expect)
+    args = ["msm_benchmark_gpu", "--check_results", "--expect", str(tmp_path / "expect.bin"), "--curve", curve]
+    for k in ks:
+        args += ["-k", str(k)]
+    _, res = run(args + flags)
+    assert res["check_results"] == "pass" and res["checked_against"] == "expect_file", res
+    gpu_s = {r["k"]: r["seconds"] for r in res["results"]}
+    print(json.dumps({"curve": g1, "flags": flags, "cpu_oracle_s": cpu_s, "gpu_s": gpu_s,
+                      "cpu_threads": O.max_threads()}))
+    # a wrong CPU point fails the check (exit 1, "FAIL")
+    bad = bytearray(expect)
+    bad[5] ^= 1
+    (tmp_path / "bad.bin").write_bytes(bytes(bad))
+    p = subprocess.run([os.path.join(BIN, args[0])] + args[1:3] + [str(tmp_path / "bad.bin")] + args[4:] + flags,
+                       timeout=120, capture_output=True, text=True)
+    assert p.returncode == 1 and json.loads(p.stdout.strip().splitlines()[-1])["check_results"] == "FAIL"
+
+
+@pytest.mark.parametrize("ks,flags", [([10, 14], []), ([12], ["--run_ifft"]), ([13], ["--device_resident"]),
+                                      ([11], ["--run_ifft", "--device_resident"])])
+def test_fft_benchmark_gpu_vs_cpu_oracle(tmp_path, ks, flags):
+    """--check_results as the reference does it (fft_benchmark_gpu.cc:81-83):
+    the timed GPU transform equals the CPU transform of the same input."""
+    from oracle import oracle as O
+    expect = b""
+    for k in sorted(ks):
+        n = 1 << k
+        x = O.gen_scalars("bn254_fr", SEED + k, n).tobytes()
+        y = O.ifft(x, n) if "--run_ifft" in flags else O.fft(x, n)
+        expect += y.ljust(32 * n, b"\0")
+    (tmp_path / "expect.bin").write_bytes(expect)
+    args = ["fft_benchmark_gpu", "--check_results", "--expect", str(tmp_path / "expect.bin")]
+    for k in ks:
+        args += ["-k", str(k)]
+    _, res = run(args + flags)
+    assert res["check_results"] == "pass" and res["checked_against"] == "expect_file", res
+
+
 @pytest.mark.parametrize("flags", [[], ["--run_ifft"], ["--device_resident"]])
 def test_fft_benchmark_gpu(flags):
     out, res = run(["fft_benchmark_gpu", "-k", "14", "-k", "10", "--check_results"] + flags)
@@ -90,3 +156,36 @@ def test_ntt_holder_cpp_hook(tmp_path, log_n):
     five = O.field_op("bn254_fr", "to_mont", (5).to_bytes(32, "little"))
     assert fft == O.fft(inp, n)
     assert coset == O.fft(inp, n, five)
+
+
+@pytest.mark.parametrize("log_n", [0, 8, 12])
+def test_msm_cpp_plugin_boundary(log_n):
+    """include/tachyon_mi355x_msm.h -- VariableBaseMSMGpu<Point>::Run
+    (ProjectivePoint result; host vectors and device-resident bases) and
+    VariableBaseMSM<Point>::Run (XYZZ bucket; containers and iterators) -- for
+    the four groups from a C++ client: the results equal the CPU oracle's MSM
+    of the same seeded inputs, mismatched sizes return false, an empty MSM is
+    the XYZZ identity (1, 1, 0, 0)."""
+    from oracle import oracle as O
+    from oracle import pyref
+    seed = 0x5EED + log_n
+    out = subprocess.run([os.path.join(BIN, "msm_plugin_check"), str(log_n), str(seed)], timeout=300,
+                         capture_output=True, text=True)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0, res
+    n = 1 << log_n
+    for gid, curve in enumerate(("bn254_g1", "bn254_g2", "bls12_381_g1", "bls12_381_g2")):
+        g = res["groups"][str(gid)]
+        assert g["ok"] and g["mismatch_false"], (curve, g)
+        C = pyref.Curve(curve)
+        cb = C.K.nbytes
+        one, zero = C.K.to_bytes(C.K.const(1)), b"\0" * cb
+        sf = O.CURVE_INFO[curve][1]
+        want = O.msm(curve, O.gen_bases(curve, seed, n, 16).tobytes(), O.gen_scalars(sf, seed, n).tobytes())[0]
+        proj, xyzz = bytes.fromhex(g["projective"]), bytes.fromhex(g["xyzz"])
+        if want == b"\0" * (2 * cb):
+            assert proj == one + one + zero and xyzz == one + one + zero + zero
+        else:
+            assert proj == want + one
+            assert xyzz == want + one + one
+        assert bytes.fromhex(g["empty_xyzz"]) == one + one + zero + zero

@@ -130,6 +130,15 @@ def test_device_generator_matches_oracle():
         torch.cuda.synchronize()
         assert d_b.cpu().numpy().tobytes() == O.gen_bases(curve, 31, n, chunk).tobytes(), curve
         assert d_s.cpu().numpy().tobytes() == O.gen_scalars(sf, 31, n).tobytes(), curve
+        # a shard [start, start + m) of the same sequence (bench.py's per-rank inputs)
+        start, m = 14 * chunk, 100
+        d_p = torch.empty(m * pb, dtype=torch.uint8, device="cuda")
+        d_q = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
+        M.gen_bases(curve, 31, m, chunk, d_p.data_ptr(), start=start)
+        M.gen_scalars(sf, 31, m, d_q.data_ptr(), start=start)
+        torch.cuda.synchronize()
+        assert d_p.cpu().numpy().tobytes() == d_b.cpu().numpy().tobytes()[start * pb:(start + m) * pb], curve
+        assert d_q.cpu().numpy().tobytes() == d_s.cpu().numpy().tobytes()[start * 32:(start + m) * 32], curve
 
 
 def test_device_resident_inputs_and_shard_sum():
