@@ -275,7 +275,6 @@ def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backen
     zkey, full = synth_groth16_zkey(args.groth16_log_n)
     prover = Groth16Prover(zkey)
     setup_s = time.perf_counter() - t0
-    del zkey
 
     def step():
         if world == 1:
@@ -303,9 +302,14 @@ def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backen
     phases = {k: round(v, 3) for k, v in prover.last_timings().items()}
     if world > 1:  # the sharded proof must equal the single-GPU one
         consistent_1gpu = prover.prove(full) == proof
+    equals_oracle = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import groth16 as OG  # checker only: the CPU restatement of the same proof
+        equals_oracle = tuple(OG.prove_np(zkey, full)) == tuple(proof)
     out = {"ms_per_proof": dt * 1e3, "proofs_per_s": 1 / dt, "constraints": 1 << args.groth16_log_n,
            "num_vars": prover.num_vars, "mode": "NoZK, host-resident witness, device-resident proving key",
-           "consistent": proof == ref, "phase_ms": phases, "setup_s": round(setup_s, 1),
+           "consistent": proof == ref, "equals_cpu_oracle": equals_oracle, "phase_ms": phases,
+           "setup_s": round(setup_s, 1),
            "workload": f"synthetic circom zkey, 2^{args.groth16_log_n} constraints, 2+2 A/B terms per row "
                        f"(BASELINE configs[4] shape; seeded points, no trapdoor)"}
     if world > 1:

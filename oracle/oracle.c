@@ -420,7 +420,6 @@ EXPORT long oracle_ifft(int field, size_t domain_num_coeffs, const void* offset,
   return -1;
 }
 
-/* Domain scalars for tests: writes group_gen, group_gen_inv, size_inv. */
 /* 1: install the halo2 generator / roots (OverrideSubgroupGenerator), 0: restore
  * (~ScopedSubgroupGeneratorOverrider).  Returns the previous state. */
 EXPORT int oracle_bn254_fr_set_halo2(int on) {
@@ -450,6 +449,7 @@ EXPORT void oracle_bn254_fr_large_subgroup_root(void* out) {
   }
 }
 
+/* Domain scalars for tests: writes group_gen, group_gen_inv, size_inv. */
 EXPORT int oracle_domain_info(int field, size_t num_coeffs, void* out3) {
   if (field == 1) {
     bn254_fr_domain_t* d = bn254_fr_domain_create(num_coeffs);
@@ -459,6 +459,62 @@ EXPORT int oracle_domain_info(int field, size_t num_coeffs, void* out3) {
     bn254_fr_domain_destroy(d);
     return 0;
   }
+  return -1;
+}
+
+/* QuadraticArithmeticProgram::WitnessMapFromMatrices
+ * (vendors/circom/circomlib/circuit/quadratic_arithmetic_program.h:24-113):
+ *   a[c] += value * full[s] (matrix 0) / b[c] likewise (:38-63, serial here:
+ *   field addition is exact, so the reference's lock order does not matter);
+ *   c = a * b (:65-71); a, b, c = IFFT (:77-82); DistributePowers by the
+ *   2n-th root of unity (:84-91); FFT (:93-98); h = a * b - c (:100-108).
+ * coefs: ncoef packed zkey records {u32 matrix, u32 constraint, u32 signal,
+ * 32-byte word}; the value is FromMontgomery(word) as the zkey reader stores
+ * it (zkey.h:211-223).  full: m Montgomery elements.  h_out: n elements. */
+#define WITNESS_MAP(F)                                                                      \
+  {                                                                                         \
+    F##_t* abc = (F##_t*)calloc(3 * n, sizeof(F##_t));                                      \
+    if (!abc) return -1;                                                                    \
+    F##_t *a = abc, *b = abc + n, *c = abc + 2 * n;                                         \
+    const F##_t* w = (const F##_t*)full;                                                    \
+    const uint8_t* rec = (const uint8_t*)coefs;                                             \
+    for (size_t i = 0; i < ncoef; ++i, rec += 44) {                                         \
+      uint32_t mc[3];                                                                       \
+      memcpy(mc, rec, 12);                                                                  \
+      if (mc[1] >= n || mc[2] >= m) { free(abc); return -2; }                               \
+      F##_t word, val;                                                                      \
+      memcpy(word.l, rec + 12, 32);                                                         \
+      F##_to_bigint(&word, val.l);                                                          \
+      F##_t t = F##_mul(val, w[mc[2]]);                                                     \
+      F##_t* dst = mc[0] == 0 ? &a[mc[1]] : &b[mc[1]];                                      \
+      *dst = F##_add(*dst, t);                                                              \
+    }                                                                                       \
+    for (size_t i = 0; i < n; ++i) c[i] = F##_mul(a[i], b[i]);                              \
+    F##_domain_t* d = F##_domain_create(n);                                                 \
+    F##_domain_t* d2 = F##_domain_create(2 * n);                                            \
+    if (!d || !d2) { free(abc); return -3; }                                                \
+    F##_domain_set_offset(d, d2->group_gen); /* DistributePowers(g_2n) + FFT = coset FFT */ \
+    F##_t one = F##_one();                                                                  \
+    for (int k = 0; k < 3; ++k) {                                                           \
+      F##_t* v = abc + (size_t)k * n;                                                       \
+      F##_domain_t tmp = *d;                                                                \
+      tmp.has_offset = 0; tmp.offset = one; tmp.offset_inv = one;                           \
+      size_t len = F##_domain_ifft(&tmp, v, n);                                             \
+      if (F##_domain_fft(d, v, len) == 0)                                                   \
+        for (size_t i = 0; i < n; ++i) v[i] = F##_zero();                                   \
+    }                                                                                       \
+    F##_t* h = (F##_t*)h_out;                                                               \
+    for (size_t i = 0; i < n; ++i) h[i] = F##_sub(F##_mul(a[i], b[i]), c[i]);               \
+    F##_domain_destroy(d);                                                                  \
+    F##_domain_destroy(d2);                                                                 \
+    free(abc);                                                                              \
+    return 0;                                                                               \
+  }
+
+EXPORT int oracle_groth16_witness_map(int field, size_t n, const void* coefs, size_t ncoef, const void* full,
+                                      size_t m, void* h_out) {
+  if (field == 1) WITNESS_MAP(bn254_fr)
+  if (field == 3) WITNESS_MAP(bls12_381_fr)
   return -1;
 }
 

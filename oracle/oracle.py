@@ -59,6 +59,8 @@ def lib():
         L.oracle_domain_info.argtypes = [i, sz, vp]
         L.oracle_domain_info.restype = i
         L.oracle_max_threads.restype = i
+        L.oracle_groth16_witness_map.argtypes = [i, sz, vp, sz, vp, sz, vp]
+        L.oracle_groth16_witness_map.restype = i
         L.oracle_bn254_fr_set_halo2.argtypes = [i]
         L.oracle_bn254_fr_set_halo2.restype = i
         L.oracle_bn254_fr_large_subgroup_root.argtypes = [vp]

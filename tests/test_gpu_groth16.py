@@ -71,6 +71,47 @@ def test_synthetic_parity(curve, log_n, num_public, seed):
     prover.close()
 
 
+def test_adder_fixture_gpu():
+    """The reference's second circom fixture (examples/adder.zkey) with the
+    witness of adder_data.json: the GPU proof equals the oracle's and passes
+    the pairing check, NoZK and ZK."""
+    from tachyon_amd.groth16 import Groth16Prover
+    from test_groth16_oracle import adder_witness
+    zbytes = open(os.path.join(GOLDEN, "adder.zkey"), "rb").read()
+    zk = CF.parse_zkey(zbytes)
+    w = adder_witness(3, 4)
+    prover = Groth16Prover(zbytes)
+    fb = fr_bytes("bn254", w)
+    G1, G2 = pyref.Curve("bn254_g1"), pyref.Curve("bn254_g2")
+    vk = {k: (G2 if k.endswith("g2") else G1).from_bytes(v) for k, v in zk["vk"].items()}
+    ic = [G1.from_bytes(b) for b in zk["ic"]]
+    Fr = G1.Fr
+    for r, s in ((0, 0), (0xC0DE, Fr.p - 77)):
+        proof = prover.prove(fb) if r == 0 else prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))
+        assert list(proof) == list(OG.prove(zk, w, r, s))
+        A, B, C = proof
+        assert BP.groth16_verify(vk, ic, [7], (G1.from_bytes(A), G2.from_bytes(B), G1.from_bytes(C)))
+    prover.close()
+
+
+def test_configs4_size_parity():
+    """BASELINE configs[4] at its own size: the bench's synthetic 2^20-constraint
+    circom key (bench.synth_groth16_zkey); the GPU proof equals the CPU
+    oracle's (witness map and MSMs in oracle/, prove_np), NoZK and ZK."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from tachyon_amd.groth16 import Groth16Prover
+    zkey, full = bench.synth_groth16_zkey(20)
+    prover = Groth16Prover(zkey)
+    fb = full.tobytes()
+    assert tuple(prover.prove(fb)) == tuple(OG.prove_np(zkey, full))
+    Fr = pyref.Field("bn254_fr")
+    r, s = 0x1234_5678_9ABC, Fr.p - 2
+    assert tuple(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == tuple(OG.prove_np(zkey, full, r, s))
+    prover.close()
+
+
 def test_all_public_no_witness():
     """num_vars = num_public + 1: the witness (l / C1) MSM is empty."""
     from tachyon_amd.groth16 import Groth16Prover
