@@ -113,6 +113,7 @@ TACHYON_C_EXPORT tachyon_bls12_381_g1_jacobian* tachyon_bls12_381_g1_affine_msm_
 typedef struct tachyon_bn254_univariate_evaluation_domain tachyon_bn254_univariate_evaluation_domain;
 typedef struct tachyon_bn254_univariate_evaluations tachyon_bn254_univariate_evaluations;
 typedef struct tachyon_bn254_univariate_dense_polynomial tachyon_bn254_univariate_dense_polynomial;
+typedef struct tachyon_bn254_univariate_rational_evaluations tachyon_bn254_univariate_rational_evaluations;
 
 /* bn254_univariate_evaluation_domain.h:38-136 */
 TACHYON_C_EXPORT tachyon_bn254_univariate_evaluation_domain* tachyon_bn254_univariate_evaluation_domain_create(
@@ -123,6 +124,9 @@ TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_
     const tachyon_bn254_univariate_evaluation_domain* domain);
 TACHYON_C_EXPORT tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_empty_poly(
     const tachyon_bn254_univariate_evaluation_domain* domain);
+/* size() rational zeros 0/1 (bn254_univariate_evaluation_domain.h:70-79) */
+TACHYON_C_EXPORT tachyon_bn254_univariate_rational_evaluations*
+tachyon_bn254_univariate_evaluation_domain_empty_rational_evals(const tachyon_bn254_univariate_evaluation_domain* domain);
 TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_fft(
     const tachyon_bn254_univariate_evaluation_domain* domain, const tachyon_bn254_univariate_dense_polynomial* poly);
 TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain_fft_inplace(
@@ -140,6 +144,33 @@ TACHYON_C_EXPORT void tachyon_bn254_univariate_evaluations_destroy(tachyon_bn254
 TACHYON_C_EXPORT size_t tachyon_bn254_univariate_evaluations_len(const tachyon_bn254_univariate_evaluations* evals);
 TACHYON_C_EXPORT void tachyon_bn254_univariate_evaluations_set_value(tachyon_bn254_univariate_evaluations* evals,
                                                                      size_t i, const tachyon_bn254_fr* value);
+
+/* bn254_univariate_rational_evaluations.h: UnivariateEvaluations<RationalField<bn254::Fr>>
+ * (numerator / denominator pairs, zero = 0/1; boundary checks are the caller's).
+ * _evaluate: numerator / denominator of element i (aborts on a zero
+ * denominator, like RationalField::Evaluate's unwrap); _batch_evaluate: a new
+ * evaluations container of every quotient, zero where the denominator is zero
+ * (RationalField::BatchEvaluate + DoBatchInverse, groups.h:124-180), computed
+ * on the GPU (Montgomery's batch-inversion trick). */
+TACHYON_C_EXPORT tachyon_bn254_univariate_rational_evaluations* tachyon_bn254_univariate_rational_evaluations_create(
+    void);
+TACHYON_C_EXPORT tachyon_bn254_univariate_rational_evaluations* tachyon_bn254_univariate_rational_evaluations_clone(
+    const tachyon_bn254_univariate_rational_evaluations* evals);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_rational_evaluations_destroy(
+    tachyon_bn254_univariate_rational_evaluations* evals);
+TACHYON_C_EXPORT size_t tachyon_bn254_univariate_rational_evaluations_len(
+    const tachyon_bn254_univariate_rational_evaluations* evals);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_rational_evaluations_set_zero(
+    tachyon_bn254_univariate_rational_evaluations* evals, size_t i);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_rational_evaluations_set_trivial(
+    tachyon_bn254_univariate_rational_evaluations* evals, size_t i, const tachyon_bn254_fr* numerator);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_rational_evaluations_set_rational(
+    tachyon_bn254_univariate_rational_evaluations* evals, size_t i, const tachyon_bn254_fr* numerator,
+    const tachyon_bn254_fr* denominator);
+TACHYON_C_EXPORT void tachyon_bn254_univariate_rational_evaluations_evaluate(
+    const tachyon_bn254_univariate_rational_evaluations* evals, size_t i, tachyon_bn254_fr* value);
+TACHYON_C_EXPORT tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_rational_evaluations_batch_evaluate(
+    const tachyon_bn254_univariate_rational_evaluations* evals);
 
 /* bn254_univariate_dense_polynomial.h (create/clone/destroy) */
 TACHYON_C_EXPORT tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_dense_polynomial_create(void);
@@ -168,6 +199,13 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_dense_polynomial_get_value
     const tachyon_bn254_univariate_dense_polynomial* poly, size_t i, tachyon_bn254_fr* value);
 TACHYON_C_EXPORT tachyon_bn254_fr* tachyon_mi355x_bn254_univariate_dense_polynomial_data(
     tachyon_bn254_univariate_dense_polynomial* poly);
+
+/* rational container access the reference performs through native_cast */
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_rational_evaluations_resize(
+    tachyon_bn254_univariate_rational_evaluations* evals, size_t len);
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_rational_evaluations_get(
+    const tachyon_bn254_univariate_rational_evaluations* evals, size_t i, tachyon_bn254_fr* numerator,
+    tachyon_bn254_fr* denominator);
 
 /* halo2 BN254 Fr generator set (math::halo2, bn/bn254/halo2/bn254.h:9-17):
  * _override = OverrideSubgroupGenerator() (bn254.cc:7-30: generator 7 and

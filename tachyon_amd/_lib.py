@@ -63,6 +63,16 @@ SIGNATURES = [
     ("tachyon_bn254_univariate_evaluations_destroy", None, [vp]),
     ("tachyon_bn254_univariate_evaluations_len", sz, [vp]),
     ("tachyon_bn254_univariate_evaluations_set_value", None, [vp, sz, vp]),
+    ("tachyon_bn254_univariate_evaluation_domain_empty_rational_evals", vp, [vp]),
+    ("tachyon_bn254_univariate_rational_evaluations_create", vp, []),
+    ("tachyon_bn254_univariate_rational_evaluations_clone", vp, [vp]),
+    ("tachyon_bn254_univariate_rational_evaluations_destroy", None, [vp]),
+    ("tachyon_bn254_univariate_rational_evaluations_len", sz, [vp]),
+    ("tachyon_bn254_univariate_rational_evaluations_set_zero", None, [vp, sz]),
+    ("tachyon_bn254_univariate_rational_evaluations_set_trivial", None, [vp, sz, vp]),
+    ("tachyon_bn254_univariate_rational_evaluations_set_rational", None, [vp, sz, vp, vp]),
+    ("tachyon_bn254_univariate_rational_evaluations_evaluate", None, [vp, sz, vp]),
+    ("tachyon_bn254_univariate_rational_evaluations_batch_evaluate", vp, [vp]),
     ("tachyon_bn254_univariate_dense_polynomial_create", vp, []),
     ("tachyon_bn254_univariate_dense_polynomial_clone", vp, [vp]),
     ("tachyon_bn254_univariate_dense_polynomial_destroy", None, [vp]),
@@ -75,6 +85,8 @@ SIGNATURES = [
     ("tachyon_mi355x_bn254_univariate_dense_polynomial_set_value", None, [vp, sz, vp]),
     ("tachyon_mi355x_bn254_univariate_dense_polynomial_get_value", None, [vp, sz, vp]),
     ("tachyon_mi355x_bn254_univariate_dense_polynomial_data", vp, [vp]),
+    ("tachyon_mi355x_bn254_univariate_rational_evaluations_resize", None, [vp, sz]),
+    ("tachyon_mi355x_bn254_univariate_rational_evaluations_get", None, [vp, sz, vp, vp]),
     ("tachyon_mi355x_bn254_halo2_override_subgroup_generator", None, []),
     ("tachyon_mi355x_bn254_halo2_restore_subgroup_generator", None, []),
     ("tachyon_mi355x_bn254_halo2_subgroup_generator_active", i32, []),

@@ -202,7 +202,13 @@ struct Vec {
 struct Domain {
   std::unique_ptr<ntt::NttDomain<Bn254Fr>> impl;
 };
+// UnivariateEvaluations<RationalField<bn254::Fr>>: {numerator, denominator}
+// pairs; Zero() = 0 / 1 (math/base/rational_field.h:33,199-200)
+struct RationalVec {
+  std::vector<FrC> num, den;
+};
 }  // namespace tachyon_amd::capi_detail
+using tachyon_amd::capi_detail::RationalVec;
 using tachyon_amd::capi_detail::Domain;
 using tachyon_amd::capi_detail::FrC;
 using tachyon_amd::capi_detail::Vec;
@@ -210,6 +216,7 @@ using tachyon_amd::capi_detail::Vec;
 struct tachyon_bn254_univariate_evaluations : Vec {};
 struct tachyon_bn254_univariate_dense_polynomial : Vec {};
 struct tachyon_bn254_univariate_evaluation_domain : Domain {};
+struct tachyon_bn254_univariate_rational_evaluations : RationalVec {};
 
 struct tachyon_bn254_g1_msm : MsmCtx<Bn254G1> {};
 struct tachyon_bn254_g1_msm_gpu : MsmCtx<Bn254G1> {};
@@ -431,6 +438,89 @@ tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_evaluation_domain
   return e;
   GUARD_END
 }
+tachyon_bn254_univariate_rational_evaluations* tachyon_bn254_univariate_evaluation_domain_empty_rational_evals(
+    const tachyon_bn254_univariate_evaluation_domain* domain) {
+  GUARD_BEGIN
+  auto* e = new tachyon_bn254_univariate_rational_evaluations();
+  const Bn254Fr one = Bn254Fr::one();
+  FrC one_c;
+  memcpy(&one_c, &one, sizeof(one_c));
+  e->num.assign(domain->impl->size(), FrC{});
+  e->den.assign(domain->impl->size(), one_c);
+  return e;
+  GUARD_END
+}
+
+// ---- bn254_univariate_rational_evaluations.h (reference .cc:18-88) ----
+tachyon_bn254_univariate_rational_evaluations* tachyon_bn254_univariate_rational_evaluations_create(void) {
+  GUARD_BEGIN return new tachyon_bn254_univariate_rational_evaluations(); GUARD_END
+}
+tachyon_bn254_univariate_rational_evaluations* tachyon_bn254_univariate_rational_evaluations_clone(
+    const tachyon_bn254_univariate_rational_evaluations* evals) {
+  GUARD_BEGIN return new tachyon_bn254_univariate_rational_evaluations(*evals); GUARD_END
+}
+void tachyon_bn254_univariate_rational_evaluations_destroy(tachyon_bn254_univariate_rational_evaluations* evals) {
+  delete evals;
+}
+size_t tachyon_bn254_univariate_rational_evaluations_len(const tachyon_bn254_univariate_rational_evaluations* evals) {
+  return evals->num.size();
+}
+// boundary checks are the caller's, as in the reference (.cc:42)
+void tachyon_bn254_univariate_rational_evaluations_set_zero(tachyon_bn254_univariate_rational_evaluations* evals,
+                                                            size_t i) {
+  const Bn254Fr one = Bn254Fr::one();
+  evals->num[i] = FrC{};
+  memcpy(&evals->den[i], &one, sizeof(FrC));
+}
+void tachyon_bn254_univariate_rational_evaluations_set_trivial(tachyon_bn254_univariate_rational_evaluations* evals,
+                                                               size_t i, const tachyon_bn254_fr* numerator) {
+  const Bn254Fr one = Bn254Fr::one();
+  evals->num[i] = *numerator;
+  memcpy(&evals->den[i], &one, sizeof(FrC));
+}
+void tachyon_bn254_univariate_rational_evaluations_set_rational(tachyon_bn254_univariate_rational_evaluations* evals,
+                                                                size_t i, const tachyon_bn254_fr* numerator,
+                                                                const tachyon_bn254_fr* denominator) {
+  evals->num[i] = *numerator;
+  evals->den[i] = *denominator;
+}
+// RationalField::Evaluate (rational_field.h:115): numerator / denominator;
+// a zero denominator fails like the reference's unwrap (abort)
+void tachyon_bn254_univariate_rational_evaluations_evaluate(
+    const tachyon_bn254_univariate_rational_evaluations* evals, size_t i, tachyon_bn254_fr* value) {
+  GUARD_BEGIN
+  Bn254Fr d;
+  memcpy(&d, &evals->den[i], sizeof(d));
+  if (d.is_zero()) throw std::runtime_error("RationalField::Evaluate: zero denominator");
+  util::batch_evaluate_bn254_fr(&evals->num[i], &evals->den[i], value, 1);
+  GUARD_END
+}
+tachyon_bn254_univariate_evaluations* tachyon_bn254_univariate_rational_evaluations_batch_evaluate(
+    const tachyon_bn254_univariate_rational_evaluations* evals) {
+  GUARD_BEGIN
+  auto* out = new tachyon_bn254_univariate_evaluations();
+  out->v.resize(evals->num.size());
+  util::batch_evaluate_bn254_fr(evals->num.data(), evals->den.data(), out->v.data(), out->v.size());
+  return out;
+  GUARD_END
+}
+void tachyon_mi355x_bn254_univariate_rational_evaluations_resize(tachyon_bn254_univariate_rational_evaluations* evals,
+                                                                 size_t len) {
+  GUARD_BEGIN
+  const Bn254Fr one = Bn254Fr::one();
+  FrC one_c;
+  memcpy(&one_c, &one, sizeof(one_c));
+  evals->num.resize(len, FrC{});
+  evals->den.resize(len, one_c);
+  GUARD_END
+}
+void tachyon_mi355x_bn254_univariate_rational_evaluations_get(
+    const tachyon_bn254_univariate_rational_evaluations* evals, size_t i, tachyon_bn254_fr* numerator,
+    tachyon_bn254_fr* denominator) {
+  *numerator = evals->num[i];
+  *denominator = evals->den[i];
+}
+
 tachyon_bn254_univariate_dense_polynomial* tachyon_bn254_univariate_evaluation_domain_empty_poly(
     const tachyon_bn254_univariate_evaluation_domain* domain) {
   GUARD_BEGIN

@@ -166,6 +166,40 @@ void run_field_op(int op, const void* a, const void* b, void* out, size_t count)
   TA_HIP(hipMemcpy(out, dout.as<F>(), bytes, hipMemcpyDeviceToHost));
 }
 
+// RationalField<F>::BatchEvaluate (math/base/rational_field.h:51-76):
+// out[i] = num[i] / den[i], with MultiplicativeGroup::DoBatchInverse's rule for
+// a zero denominator (groups.h:124-180: its inverse is 0, so out[i] = 0).
+// Montgomery's trick per thread over `chunk` consecutive elements: prefix
+// products of the non-zero denominators go to `prefix`, one Fermat inverse
+// per chunk, then the backward pass.  Results are canonical, so any chunking
+// gives the reference's bytes.
+template <class F>
+__global__ __launch_bounds__(kBlock) void batch_evaluate_kernel(const F* __restrict__ num, const F* __restrict__ den,
+                                                                F* __restrict__ out, F* __restrict__ prefix, size_t n,
+                                                                uint32_t chunk) {
+  const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const size_t s = t * chunk;
+  if (s >= n) return;
+  const size_t e = s + chunk < n ? s + chunk : n;
+  F prod = F::one();
+  for (size_t i = s; i < e; ++i) {
+    const F d = den[i];
+    if (!d.is_zero()) prod = prod * d;
+    prefix[i] = prod;
+  }
+  F inv = prod.inverse();  // product of non-zero values: invertible
+  for (size_t i = e; i-- > s;) {
+    const F d = den[i];
+    if (d.is_zero()) {
+      out[i] = F::zero();
+      continue;
+    }
+    const F before = i > s ? prefix[i - 1] : F::one();  // product of the non-zero den[s..i)
+    out[i] = (num[i] * (inv * before)).canonical();
+    inv = inv * d;
+  }
+}
+
 template <class F>
 void run_ec_op(int op, const void* a, const void* b, void* out, size_t count) {
   if (count == 0) return;
@@ -180,6 +214,21 @@ void run_ec_op(int op, const void* a, const void* b, void* out, size_t count) {
 }
 
 }  // namespace
+
+void batch_evaluate_bn254_fr(const void* num, const void* den, void* out, size_t n) {
+  if (n == 0) return;
+  using F = Bn254Fr;
+  constexpr uint32_t kChunk = 32;
+  DeviceBuffer dn, dd, dout, dpre;
+  const size_t bytes = n * sizeof(F);
+  TA_HIP(hipMemcpy(dn.ensure(bytes), num, bytes, hipMemcpyHostToDevice));
+  TA_HIP(hipMemcpy(dd.ensure(bytes), den, bytes, hipMemcpyHostToDevice));
+  const size_t threads = (n + kChunk - 1) / kChunk;
+  hipLaunchKernelGGL(batch_evaluate_kernel<F>, dim3(ceil_div(threads, kBlock)), dim3(kBlock), 0, 0, dn.as<F>(),
+                     dd.as<F>(), static_cast<F*>(dout.ensure(bytes)), static_cast<F*>(dpre.ensure(bytes)), n, kChunk);
+  TA_HIP(hipGetLastError());
+  TA_HIP(hipMemcpy(out, dout.as<F>(), bytes, hipMemcpyDeviceToHost));
+}
 
 void gen_scalars(int field, uint64_t seed, size_t start, size_t n, void* d_out, hipStream_t stream) {
   if (n == 0) return;

@@ -227,3 +227,67 @@ class FourStepNtt:
         k1 = rank * rg + np.arange(rg)[:, None]
         k2 = np.arange(C)[None, :]
         return (k1 + R * k2).reshape(-1)
+
+
+class RationalEvaluations:
+    """UnivariateEvaluations<RationalField<bn254::Fr>> over the C-ABI
+    (tachyon/c/math/polynomials/univariate/bn254_univariate_rational_evaluations.h):
+    numerator / denominator pairs; batch_evaluate() runs on the GPU."""
+
+    def __init__(self, _handle=None):
+        self._h = _handle or lib().tachyon_bn254_univariate_rational_evaluations_create()
+
+    @classmethod
+    def empty(cls, domain: "Radix2EvaluationDomain"):
+        """domain->Empty<RationalEvals>(): size() zeros (0 / 1)."""
+        return cls(lib().tachyon_bn254_univariate_evaluation_domain_empty_rational_evals(domain._d))
+
+    def close(self):
+        if self._h:
+            lib().tachyon_bn254_univariate_rational_evaluations_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return lib().tachyon_bn254_univariate_rational_evaluations_len(self._h)
+
+    def clone(self):
+        return RationalEvaluations(lib().tachyon_bn254_univariate_rational_evaluations_clone(self._h))
+
+    def resize(self, n: int):
+        lib().tachyon_mi355x_bn254_univariate_rational_evaluations_resize(self._h, n)
+
+    def set_zero(self, i: int):
+        lib().tachyon_bn254_univariate_rational_evaluations_set_zero(self._h, i)
+
+    def set_trivial(self, i: int, numerator: bytes):
+        lib().tachyon_bn254_univariate_rational_evaluations_set_trivial(
+            self._h, i, ctypes.create_string_buffer(numerator, FR_BYTES))
+
+    def set_rational(self, i: int, numerator: bytes, denominator: bytes):
+        lib().tachyon_bn254_univariate_rational_evaluations_set_rational(
+            self._h, i, ctypes.create_string_buffer(numerator, FR_BYTES),
+            ctypes.create_string_buffer(denominator, FR_BYTES))
+
+    def get(self, i: int):
+        n, d = ctypes.create_string_buffer(FR_BYTES), ctypes.create_string_buffer(FR_BYTES)
+        lib().tachyon_mi355x_bn254_univariate_rational_evaluations_get(self._h, i, n, d)
+        return n.raw, d.raw
+
+    def evaluate(self, i: int) -> bytes:
+        out = ctypes.create_string_buffer(FR_BYTES)
+        lib().tachyon_bn254_univariate_rational_evaluations_evaluate(self._h, i, out)
+        return out.raw
+
+    def batch_evaluate(self) -> bytes:
+        L = lib()
+        e = L.tachyon_bn254_univariate_rational_evaluations_batch_evaluate(self._h)
+        n = L.tachyon_bn254_univariate_evaluations_len(e)
+        out = ctypes.string_at(L.tachyon_mi355x_bn254_univariate_evaluations_data(e), n * FR_BYTES) if n else b""
+        L.tachyon_bn254_univariate_evaluations_destroy(e)
+        return out
