@@ -443,6 +443,22 @@ def main():
                                   "peak = measured BN254 mulmod ceiling (tools/microbench/mulmod_rates.hip)"},
     }
 
+    # ---- configs[1] sweep (2^16, 2^20 .. 2^24: prefixes of the same device-resident input) ----
+    if world == 1 and args.log_n >= 24:
+        sweep = {}
+        for k in (16, 20, 22, 24):
+            m = 1 << k
+            msm.run(d_bases, d_scalars, m)
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                msm.run(d_bases, d_scalars, m)
+                ts.append(time.perf_counter() - t0)
+            best = sorted(ts)[2]
+            sweep[str(k)] = {"ms": round(best * 1e3, 3), "scalars_per_s": m / best}
+        sweep[str(args.log_n)] = {"ms": round(ms_per_step, 3), "scalars_per_s": value}
+        out["msm_sweep"] = sweep
+
     # ---- NTT 2^24: one GPU, or the four-step sharded transform (one RCCL all-to-all) ----
     if not args.no_ntt and world > 1:
         from tachyon_amd.ntt import FourStepNtt
@@ -535,6 +551,31 @@ def main():
                                            "path": "IcicleNTT::Run semantics on a pageable host vector "
                                                    "(..._evaluation_domain_transform_host)"}
         dom.close()
+        # configs[2] sweep: 2^20 and 2^22 on prefixes of the same input (forward + inverse per rep)
+        nsweep = {}
+        for k in (20, 22):
+            if k >= args.ntt_log_n:
+                continue
+            m = 1 << k
+            dk = Radix2EvaluationDomain(m)
+            sk = torch.cuda.ExternalStream(dk.stream)
+            y = x[:m * 32].clone()
+            torch.cuda.synchronize()
+            dk.transform_device(y.data_ptr(), inverse=False)
+            dk.transform_device(y.data_ptr(), inverse=True)
+            sk.synchronize()
+            reps_k = 10
+            t0 = time.perf_counter()
+            for _ in range(reps_k):
+                dk.transform_device(y.data_ptr(), inverse=False)
+                dk.transform_device(y.data_ptr(), inverse=True)
+            sk.synchronize()
+            dtk = (time.perf_counter() - t0) / (2 * reps_k)
+            nsweep[str(k)] = {"ms": round(dtk * 1e3, 4), "elems_per_s": m / dtk,
+                              "round_trip_ok": bool(torch.equal(y, x[:m * 32]))}
+            dk.close()
+        nsweep[str(args.ntt_log_n)] = {"ms": round(dt * 1e3, 4), "elems_per_s": nn / dt}
+        out["ntt"]["sweep"] = nsweep
 
     if args.bls_log_n:
         out["bls12_381"] = bench_bls(args, rank, world, barrier, dist, backend)

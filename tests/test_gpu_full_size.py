@@ -77,3 +77,33 @@ def test_bls_shard_vs_oracle(curve, pb):
     got = m.run(d_b, d_s)
     m.close()
     assert O.msm_np(curve, d_b.cpu().numpy(), d_s.cpu().numpy()) == got
+
+
+@pytest.mark.timeout(300)
+def test_ntt_halo2_domain_vs_oracle():
+    """The halo2 BN254 Fr domain (generator 7, OverrideSubgroupGenerator) at
+    2^22: the HIP FFT and IFFT equal the oracle's on that domain."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    from tachyon_amd.ntt import Radix2EvaluationDomain, ScopedSubgroupGeneratorOverrider
+    n = 1 << 22
+    x = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    M.gen_scalars("bn254_fr", SEED + 2, n, x.data_ptr())
+    torch.cuda.synchronize()
+    coeffs = x.cpu().numpy().view(np.uint64).copy()
+    with ScopedSubgroupGeneratorOverrider():
+        d = Radix2EvaluationDomain(n)
+    s = torch.cuda.ExternalStream(d.stream)
+    d.transform_device(x.data_ptr(), inverse=False)
+    s.synchronize()
+    evals = x.cpu().numpy().view(np.uint64).copy()
+    d.transform_device(x.data_ptr(), inverse=True)
+    s.synchronize()
+    back = x.cpu().numpy().view(np.uint64)
+    d.close()
+    expect = coeffs.copy()
+    with O.halo2_domain():
+        O.fft_np(expect)
+        assert np.array_equal(evals, expect)
+        O.fft_np(expect, inverse=True)
+    assert np.array_equal(back, coeffs) and np.array_equal(expect, coeffs)
