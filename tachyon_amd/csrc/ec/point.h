@@ -15,6 +15,8 @@ template <class F>
 struct Affine {
   F x, y;
   TA_HD bool is_zero() const { return x.is_zero() && y.is_zero(); }
+  // identity test of an input point (canonical coordinates)
+  TA_HD bool is_zero_canonical() const { return x.is_zero_canonical() && y.is_zero_canonical(); }
   TA_HD static Affine zero() { return {F::zero(), F::zero()}; }
   TA_HD Affine neg() const { return is_zero() ? *this : Affine{x, -y}; }
   TA_HD Affine canonical() const { return {x.canonical(), y.canonical()}; }
@@ -76,6 +78,28 @@ struct XYZZ {
     F p = b.x * zz - x;
     F r = b.y * zzz - y;
     if (p.is_zero() && r.is_zero()) return dbl_slowpath();
+    F pp = p.sqr();
+    F ppp = p * pp;
+    F q = x * pp;
+    XYZZ c;
+    c.x = r.sqr() - ppp - q.dbl();
+    c.y = r * (q - c.x) - y * ppp;
+    c.zz = zz * pp;
+    c.zzz = zzz * ppp;
+    return c;
+  }
+
+  // madd-2008-s for the bucket accumulation's common case: neither *this nor
+  // b is the identity (the caller tracks an identity accumulator itself), so
+  // the only test left is P == +-this; *now_zero is set when b == -this.
+  TA_HD XYZZ madd_nz(const Affine<F>& b, bool* now_zero) const {
+    F p = b.x * zz - x;
+    F r = b.y * zzz - y;
+    if (p.is_zero()) {
+      if (r.is_zero()) return dbl_slowpath();
+      *now_zero = true;
+      return zero();
+    }
     F pp = p.sqr();
     F ppp = p * pp;
     F q = x * pp;

@@ -118,6 +118,34 @@ struct Fp {
     }
     return acc == 0;
   }
+  // zero test of a value known to be canonical (< p), e.g. an input point
+  TA_HD bool is_zero_canonical() const {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc |= v[i];
+    return acc == 0;
+  }
+  // -x for a canonical x as p - x: no borrow test, a lazy representative in
+  // (0, p] (p stands for zero); device fields with the [0, 2p) representation
+  TA_HD Fp neg_canonical() const {
+    if constexpr (!kLazy) {
+      return -*this;
+    } else {
+      Fp r;
+      uint32_t br = 0;
+#pragma unroll
+      for (int i = 0; i < N; ++i) r.v[i] = subb(Cfg::kP32[i], v[i], br, &br);
+      return r;
+    }
+  }
+  // x or -x by a run-time flag, as limb selects (no branch)
+  TA_HD Fp cond_neg_canonical(bool neg) const {
+    const Fp m = neg_canonical();
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = neg ? m.v[i] : v[i];
+    return r;
+  }
   TA_HD bool operator==(const Fp& o) const {
     Fp a = canonical(), b = o.canonical();
     uint32_t acc = 0;
@@ -286,6 +314,8 @@ struct Fp2 {
   TA_HD static Fp2 one() { return {F::one(), F::zero()}; }
   TA_HD Fp2 canonical() const { return {c0.canonical(), c1.canonical()}; }
   TA_HD bool is_zero() const { return c0.is_zero() && c1.is_zero(); }
+  TA_HD bool is_zero_canonical() const { return c0.is_zero_canonical() && c1.is_zero_canonical(); }
+  TA_HD Fp2 cond_neg_canonical(bool neg) const { return {c0.cond_neg_canonical(neg), c1.cond_neg_canonical(neg)}; }
   TA_HD bool is_one() const { return c0.is_one() && c1.is_zero(); }
   TA_HD bool operator==(const Fp2& o) const { return c0 == o.c0 && c1 == o.c1; }
   TA_HD bool operator!=(const Fp2& o) const { return !(*this == o); }
@@ -333,6 +363,7 @@ struct HotFp : F {
   TA_HD HotFp dbl() const { return F::dbl(); }
   TA_HD HotFp sqr() const { return F::mul_inline(*this); }
   TA_HD HotFp inverse() const { return F::inverse(); }
+  TA_HD HotFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
   TA_HD HotFp canonical() const { return F::canonical(); }
 };
 

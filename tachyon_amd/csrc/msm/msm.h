@@ -3,8 +3,9 @@
 // Drop-in for tachyon::math::VariableBaseMSMGpu<Point> (variable_base_msm_gpu.h:11-30)
 // whose GPU work the reference delegates to icicle (icicle_msm.h:19-100).
 // Pipeline (one HIP stream, no host sync until the final window sums):
-//   recode   scalars (Montgomery -> canonical -> signed c-bit digits), one key
-//            per (window, point): |digit| and point index | sign<<31
+//   recode   scalars (Montgomery -> canonical -> signed c-bit digits), one
+//            64-bit entry per (window, point): key (window, |digit|) << 32 |
+//            point index | sign<<31
 //   sort     per-window radix sort of the (bucket, point) pairs (rocPRIM)
 //   bounds   bucket [start, end) from the sorted keys
 //   acc      bucket sums as XYZZ, split into chunks of <= K entries so that a
@@ -152,8 +153,8 @@ class MsmGpu {
   size_t held_bytes() const;
   size_t memory_divisions(size_t n, size_t resident_bytes) const;
   void ensure_group_events(unsigned groups);
-  hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const uint32_t* vin,
-                        uint32_t* vout, size_t count, unsigned begin_bit, unsigned end_bit, hipStream_t s);
+  hipError_t sort_entries(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, size_t count,
+                          unsigned begin_bit, unsigned end_bit, hipStream_t s);
 
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;
@@ -161,13 +162,13 @@ class MsmGpu {
   unsigned force_c_ = 0;
   int variant_ = 0;
   MsmTimings timings_;
-  DeviceBuffer bases_, scalars_, keys_, vals_, keys2_, vals2_, sort_tmp_, scan_tmp_;
+  DeviceBuffer bases_, scalars_, ents_, ents2_, sort_tmp_, scan_tmp_;
   DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_, buckets_;
   hipEvent_t ev_[8] = {};
   hipStream_t sort_stream_ = nullptr;  // group sorts run here, overlapping the accumulation on stream_
   std::vector<hipEvent_t> gev_sorted_, gev_acc0_, gev_acc1_;
   unsigned acc_launches_ = 0;
-  unsigned sort_bits_ = 0;
+  unsigned sort_cfg_ = 0;  // onesweep tile shape (set_variant bits 4-5)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode

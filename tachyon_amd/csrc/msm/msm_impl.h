@@ -35,6 +35,9 @@ enum : uint32_t { kHead = 1, kTail = 2, kSingle = 4 };
 // key = window << c | |digit| (digit 0 = no contribution), so one radix sort
 // over all windows orders the entries by (window, bucket) and every window
 // keeps its slice [w*n, (w+1)*n); val = point index | sign << 31.
+// An entry is one 64-bit word, key << 32 | val: the radix passes sort words
+// on bits [32, 32 + key bits) (keys-only, one array) and the accumulation
+// reads one 8-byte word per entry.
 // Signed c-bit digits of one scalar, window by window: emit(w, key, val).
 template <class Fr, class Emit>
 __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsigned c, unsigned W, Emit emit) {
@@ -66,17 +69,18 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
   }
 }
 
+__device__ __forceinline__ uint64_t make_entry(uint32_t key, uint32_t val) { return (uint64_t)key << 32 | val; }
+__device__ __forceinline__ uint32_t entry_key(uint64_t e) { return (uint32_t)(e >> 32); }
+__device__ __forceinline__ uint32_t entry_val(uint64_t e) { return (uint32_t)e; }
+
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
                                                         unsigned c, unsigned W,
-                                                        uint32_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ vals) {
+                                                        uint64_t* __restrict__ ents) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   recode_scalar(scalars[i], i, c, W, [&](unsigned w, uint32_t key, uint32_t val) {
-    size_t o = (size_t)w * n + i;
-    keys[o] = key;
-    vals[o] = val;
+    ents[(size_t)w * n + i] = make_entry(key, val);
   });
 }
 
@@ -113,13 +117,11 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
                                                                 unsigned c, unsigned W, uint32_t nblocks, uint32_t spt,
                                                                 const uint32_t* __restrict__ hist,
                                                                 const uint32_t* __restrict__ off,
-                                                                uint32_t* __restrict__ keys,
-                                                                uint32_t* __restrict__ vals) {
+                                                                uint64_t* __restrict__ ents) {
   // the block's entries are binned in LDS first, then written out bin run by
   // bin run, so consecutive lanes store to consecutive addresses
-  extern __shared__ uint32_t lds_u32[];
-  uint32_t* lkeys = lds_u32;                      // spt * kBlock * W
-  uint32_t* lvals = lds_u32 + spt * kBlock * W;   // spt * kBlock * W
+  extern __shared__ uint64_t lds_u64[];
+  uint64_t* lents = lds_u64;                      // spt * kBlock * W
   __shared__ uint32_t base[256], loff[256], cur[256];
   const uint32_t t = threadIdx.x;
   base[t] = off[(size_t)t * nblocks + blockIdx.x];
@@ -144,18 +146,15 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
       recode_scalar(scalars[i], i, c, W, [&](unsigned, uint32_t key, uint32_t val) {
         const uint32_t bin = key & 255;
         const uint32_t p = loff[bin] + atomicAdd(&cur[bin], 1u);
-        lkeys[p] = key;
-        lvals[p] = val;
+        lents[p] = make_entry(key, val);
       });
   }
   __syncthreads();
   const uint32_t total = loff[255] + cur[255];
   for (uint32_t p = t; p < total; p += kBlock) {
-    const uint32_t key = lkeys[p];
-    const uint32_t bin = key & 255;
-    const uint32_t g = base[bin] + (p - loff[bin]);
-    keys[g] = key;
-    vals[g] = lvals[p];
+    const uint64_t e = lents[p];
+    const uint32_t bin = entry_key(e) & 255;
+    ents[base[bin] + (p - loff[bin])] = e;
   }
 }
 
@@ -192,8 +191,7 @@ struct AccWaves<Bls381G2> {
 
 template <class Curve>
 __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
-                                                         const uint32_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ vals, uint32_t c,
+                                                         const uint64_t* __restrict__ ents, uint32_t c,
                                                          uint64_t gbeg, uint64_t gend, uint64_t tbase,
                                                          uint32_t K, uint32_t idx_mask,
                                                          XYZZ<typename Curve::F>* __restrict__ bucket_sum,
@@ -217,38 +215,61 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
   };
   // neighbours outside this launch's entry range belong to other windows
   // (possibly not sorted yet): they never share a bucket
-  const uint32_t prev_b = g0 > gbeg ? bucket_of_key(keys[g0 - 1]) : kNoBucket;
-  const uint32_t next_b = (g1 < gend) ? bucket_of_key(keys[g1]) : kNoBucket;
+  const uint32_t prev_b = g0 > gbeg ? bucket_of_key(entry_key(ents[g0 - 1])) : kNoBucket;
+  const uint32_t next_b = (g1 < gend) ? bucket_of_key(entry_key(ents[g1])) : kNoBucket;
 
   uint32_t flags = 0, runs = 0, cur = kNoBucket;
   XYZZ<F> acc = XYZZ<F>::zero();
+  // The identity accumulator is a flag, not a test of zz: a run starts from
+  // its first non-identity base (no madd), identity bases (0, 0) -- canonical
+  // input, so a plain limb OR -- add nothing, and madd_nz reports the rare
+  // cancellation P = -acc.  Signed digits negate y as p - y by limb selects.
+  bool acc_zero = true;
   // two-deep software pipeline: (key, val) for g+2 and the base for g+1 are
   // in flight while the madd for g runs
-  uint32_t k0 = keys[g0], v0 = vals[g0];
+  const uint64_t e0 = ents[g0];
+  uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
   uint32_t k1 = 0, v1 = 0;
-  if (g0 + 1 < g1) { k1 = keys[g0 + 1]; v1 = vals[g0 + 1]; }
+  if (g0 + 1 < g1) { const uint64_t e = ents[g0 + 1]; k1 = entry_key(e); v1 = entry_val(e); }
   Affine<F> P = hbases[v0 & idx_mask];
   for (uint64_t g = g0; g < g1; ++g) {
     uint32_t k2 = 0, v2 = 0;
-    if (g + 2 < g1) { k2 = keys[g + 2]; v2 = vals[g + 2]; }
+    if (g + 2 < g1) { const uint64_t e = ents[g + 2]; k2 = entry_key(e); v2 = entry_val(e); }
     Affine<F> Pn = hbases[v1 & idx_mask];
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
       if (b != cur) {
         if (cur != kNoBucket) {  // close a run that is not the last one
+          if (acc_zero) acc = XYZZ<F>::zero();
           if (runs == 1 && cur == prev_b) { hpieces[2 * t] = acc; flags |= kHead; }
           else hsum[cur] = acc;
         }
         cur = b;
         ++runs;
-        acc = XYZZ<F>::zero();
+        acc_zero = true;
       }
-      if ((v0 & kSignBit) && !P.is_zero()) P.y = -P.y;
-      acc = acc.madd(P);
+      if constexpr (sizeof(F) <= 48) {
+        if (!P.is_zero_canonical()) {
+          P.y = P.y.cond_neg_canonical(v0 & kSignBit);
+          if (acc_zero) {
+            acc = XYZZ<F>{P.x, P.y, F::one(), F::one()};
+            acc_zero = false;
+          } else {
+            acc = acc.madd_nz(P, &acc_zero);
+          }
+        }
+      } else {
+        // Fq2 (G2): the generic identity-aware madd measured faster here
+        // (BN254 G2 2^20 accumulation 5.40 vs 5.73 ms with the flag path)
+        if (acc_zero) { acc = XYZZ<F>::zero(); acc_zero = false; }
+        if ((v0 & kSignBit) && !P.is_zero()) P.y = -P.y;
+        acc = acc.madd(P);
+      }
     }
     k0 = k1; v0 = v1; k1 = k2; v1 = v2;
     P = Pn;
   }
+  if (acc_zero) acc = XYZZ<F>::zero();
   if (cur != kNoBucket) {  // the last run
     const bool head = runs == 1 && cur == prev_b;
     const bool tail = cur == next_b;
@@ -463,27 +484,33 @@ void MsmGpu<Curve>::ensure_group_events(unsigned groups) {
   }
 }
 
-// rocPRIM pairs sort of [0, end_bit) key bits; sort_bits_ != 0 selects a
-// onesweep digit width (A/B tuning, set_variant bits 4-5)
-template <unsigned Bits>
+// rocPRIM keys-only onesweep sort of the 64-bit entries on the key bits
+// [begin_bit, end_bit) (entry bits 32 + those).  8-bit digits; the tile
+// shape is set_variant bits 4-5 (A/B): 0 = 1024 threads x 8 items, 1 =
+// rocPRIM's gfx950 default for 64-bit keys, 2 = 512 x 16, 3 = 1024 x 12.
+// 2^26 sort: 11.0 / 12.2 / 11.7 ms (2^24: 2.72 / 3.07 / 2.95).  Sorting
+// (key, val) u32 pairs took 12.7 ms and the accumulation read two words per
+// entry: 2^26 MSM 95.0 -> 92.0 ms with the 64-bit entries.
+template <unsigned Threads, unsigned Items>
 using OnesweepCfg = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, Bits,
-                                        rocprim::block_radix_rank_algorithm::match>>;
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<Threads, Items>, rocprim::kernel_config<Threads, Items>,
+                                        8, rocprim::block_radix_rank_algorithm::match>>;
 
 template <class Curve>
-hipError_t MsmGpu<Curve>::sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout,
-                                     const uint32_t* vin, uint32_t* vout, size_t count, unsigned begin_bit,
-                                     unsigned end_bit, hipStream_t s) {
-  switch (sort_bits_) {
-    case 10:
-      return rocprim::radix_sort_pairs<OnesweepCfg<10>>(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
-    case 11:
-      return rocprim::radix_sort_pairs<OnesweepCfg<11>>(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
-    case 7:
-      return rocprim::radix_sort_pairs<OnesweepCfg<7>>(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
+hipError_t MsmGpu<Curve>::sort_entries(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, size_t count,
+                                       unsigned begin_bit, unsigned end_bit, hipStream_t s) {
+  begin_bit += 32;
+  end_bit += 32;
+  switch (sort_cfg_) {
+    case 1:
+      return rocprim::radix_sort_keys(tmp, bytes, in, out, count, begin_bit, end_bit, s);
+    case 2:
+      return rocprim::radix_sort_keys<OnesweepCfg<512, 16>>(tmp, bytes, in, out, count, begin_bit, end_bit, s);
+    case 3:
+      return rocprim::radix_sort_keys<OnesweepCfg<1024, 12>>(tmp, bytes, in, out, count, begin_bit, end_bit, s);
     default:
-      return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, count, begin_bit, end_bit, s);
+      return rocprim::radix_sort_keys<OnesweepCfg<1024, 8>>(tmp, bytes, in, out, count, begin_bit, end_bit, s);
   }
 }
 
@@ -514,10 +541,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   if (ngroups > 1 && !sort_stream_) TA_HIP(hipStreamCreateWithFlags(&sort_stream_, hipStreamNonBlocking));
   hipStream_t sort_stream = ngroups > 1 ? sort_stream_ : stream_;
 
-  uint32_t* keys = static_cast<uint32_t*>(keys_.ensure(entries * 4));
-  uint32_t* vals = static_cast<uint32_t*>(vals_.ensure(entries * 4));
-  uint32_t* keys2 = static_cast<uint32_t*>(keys2_.ensure(entries * 4));
-  uint32_t* vals2 = static_cast<uint32_t*>(vals2_.ensure(entries * 4));
+  uint64_t* ents = static_cast<uint64_t*>(ents_.ensure(entries * 8));
+  uint64_t* ents2 = static_cast<uint64_t*>(ents2_.ensure(entries * 8));
   Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * sizeof(Point)));
   Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * sizeof(Point)));
   Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / plan.K2 + T + 2) * sizeof(Point)));
@@ -540,7 +565,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // recode fused with the first (low byte) radix pass; one sort group only
   // (the scatter stages a block's spt x 256 x W entries in LDS, <= 128 KiB)
   const uint32_t spt = recode_spt_;
-  const size_t scatter_lds = (size_t)2 * spt * kBlock * W * sizeof(uint32_t);
+  const size_t scatter_lds = (size_t)spt * kBlock * W * sizeof(uint64_t);
   const bool fused = fuse_recode_ && G == W && scatter_lds <= 128 * 1024;
   const unsigned sort_begin = fused ? std::min(8u, key_bits) : 0u;
 
@@ -558,18 +583,17 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     void* hscan_tmp = hscan_tmp_.ensure(hscan_bytes);
     TA_HIP(rocprim::exclusive_scan(hscan_tmp, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
     // the scattered entries are fully sorted when the key has <= 8 bits
-    uint32_t* kdst = sort_begin < key_bits ? keys : keys2;
-    uint32_t* vdst = sort_begin < key_bits ? vals : vals2;
+    uint64_t* dst = sort_begin < key_bits ? ents : ents2;
     if (scatter_lds > 64 * 1024 && !scatter_lds_set_) {
       TA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&recode_scatter_kernel<Fr>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
       scatter_lds_set_ = true;
     }
     hipLaunchKernelGGL(recode_scatter_kernel<Fr>, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars,
-                       (uint32_t)n, c, W, nblocks, spt, hist, hoff, kdst, vdst);
+                       (uint32_t)n, c, W, nblocks, spt, hist, hoff, dst);
   } else {
     hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       W, keys, vals);
+                       W, ents);
   }
   TA_HIP(hipGetLastError());
   // every bucket without an entry stays the identity
@@ -581,8 +605,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // ---- per group: radix sort of its (window, bucket, point) entries, then accumulation ----
   const size_t max_group_entries = (size_t)G * n;
   size_t sort_bytes = 0;
-  TA_HIP(sort_pairs(nullptr, sort_bytes, keys, keys2, vals, vals2, max_group_entries, sort_begin, key_bits,
-                    sort_stream));
+  TA_HIP(sort_entries(nullptr, sort_bytes, ents, ents2, max_group_entries, sort_begin, key_bits, sort_stream));
   void* sort_tmp = sort_tmp_.ensure(sort_bytes);
   size_t tbase = 0;
   acc_launches_ = ngroups;
@@ -591,8 +614,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     const size_t e0 = (size_t)w0 * n, ecount = (size_t)(w1 - w0) * n;
     size_t bytes = sort_bytes;
     if (sort_begin < key_bits)
-      TA_HIP(sort_pairs(sort_tmp, bytes, keys + e0, keys2 + e0, vals + e0, vals2 + e0, ecount, sort_begin, key_bits,
-                        sort_stream));
+      TA_HIP(sort_entries(sort_tmp, bytes, ents + e0, ents2 + e0, ecount, sort_begin, key_bits, sort_stream));
     if (profile_ && g + 1 == ngroups) TA_HIP(hipEventRecord(ev_[3], sort_stream));  // last sort done
     if (sort_stream != stream_) {
       TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream));
@@ -612,7 +634,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
-    hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, keys2, vals2, c,
+    hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
                        (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                        tflags, tlast);
     TA_HIP(hipGetLastError());
@@ -721,8 +743,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   fuse_recode_ = !(variant_ & 128);  // bit 7: the separate recode + full sort (A/B)
   static constexpr uint32_t kSpt[] = {kRecodeSpt, 1, 4, 3};
   recode_spt_ = kSpt[(variant_ >> 8) & 3];  // bits 8-9: scalars per thread of the fused recode
-  static constexpr unsigned kSortBits[] = {0, 10, 11, 7};
-  sort_bits_ = kSortBits[(variant_ >> 4) & 3];
+  sort_cfg_ = (variant_ >> 4) & 3;  // bits 4-5: onesweep tile shape
   if (plan_out) *plan_out = plan;
   out->assign(plan.windows, Point::zero());
   if (n == 0) return;
@@ -872,7 +893,7 @@ size_t MsmGpu<Curve>::work_bytes(size_t n) const {
   const MsmPlan p = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_);
   const size_t entries = n * p.windows;
   const size_t T = (entries + p.K - 1) / p.K;
-  size_t bytes = entries * 16 + entries / 2;                 // keys, vals (x2) + onesweep scratch
+  size_t bytes = entries * 16 + entries / 2;                 // entries (x2) + onesweep scratch
   bytes += (2 * T + 2 * T / p.K2 + T + 2) * sizeof(Point);   // pieces + first join level
   bytes += (T + 2) * 4 * 9;                                  // flags, last bucket, chain tables
   bytes += (size_t)p.windows * p.buckets * sizeof(Point);    // bucket sums
@@ -882,7 +903,7 @@ size_t MsmGpu<Curve>::work_bytes(size_t n) const {
 
 template <class Curve>
 size_t MsmGpu<Curve>::held_bytes() const {
-  const DeviceBuffer* bufs[] = {&keys_,  &vals_,  &keys2_, &vals2_, &sort_tmp_, &scan_tmp_, &start_, &end_,
+  const DeviceBuffer* bufs[] = {&ents_,  &ents2_, &sort_tmp_, &scan_tmp_, &start_, &end_,
                                 &cnt_,   &off_a_, &off_b_, &part_a_, &part_b_,  &seg_a_,    &seg_b_, &buckets_,
                                 &hist_, &hscan_tmp_};
   size_t s = 0;
