@@ -236,6 +236,27 @@ struct Fp {
 #endif
   }
 
+  // Product by a constant w given as (w canonical plain, wq = floor(w 2^(32N)
+  // / p)): the Shoup product of mont_asm.h (8 limbs: 115 v_mad_u64_u32 + 99
+  // carry adds vs 128 + 128 + 8 v_mul_lo_u32 Montgomery digits in
+  // mul_inline).  For a Montgomery-form *this
+  // (any value < 2^(32N), e.g. an unreduced difference) it is the Montgomery
+  // form of a * w, lazy in [0, 2p).  Device: 8-limb fields with 3p < 2^256.
+  TA_HD Fp mul_shoup(const Fp& w, const Fp& wq) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    static_assert(N == 8 && kLazy, "Shoup products: 8-limb lazy fields only");
+    Fp r;
+    detail::shoup_mul_8<Cfg>(r.v, v, w.v, wq.v);
+    // r < 3p; r >= 2p only when the quotient estimate came out one short
+    // (probability ~2^-30 per product; the top-limb test rarely passes)
+    if (r.v[N - 1] >= Cfg::kP232[N - 1]) detail::cond_sub_8<Cfg, true>(r.v);
+    return r;
+#else
+    (void)wq;
+    return mul_cios(w.to_mont());
+#endif
+  }
+
   // CIOS no-carry Montgomery product (DoFastMul, prime_field_fallback.h:331-355);
   // the host path (final Horner step, conversions).
   TA_HD Fp mul_cios(const Fp& b) const {
@@ -364,6 +385,7 @@ struct HotFp : F {
   TA_HD HotFp sqr() const { return F::mul_inline(*this); }
   TA_HD HotFp inverse() const { return F::inverse(); }
   TA_HD HotFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
+  TA_HD HotFp mul_shoup(const HotFp& w, const HotFp& wq) const { return F::mul_shoup(w, wq); }
   TA_HD HotFp canonical() const { return F::canonical(); }
 };
 

@@ -87,6 +87,8 @@ class NttDomain {
   uint32_t pow_bits_ = 0;  // split point of the two-level power tables
   int radix_ = 2;          // DIF stages per register step of the pass kernel (see kMaxLdsElems)
   DeviceBuffer tw_fwd_, tw_inv_, scratch_, io_;
+  DeviceBuffer twm_fwd_, twm_inv_;  // Montgomery twiddles when tw_* hold Shoup entries (BN254 Fr)
+  int shoup_mode_ = 2;              // Shoup twiddles: 0 never, 1 every pass, 2 all but the first pass
   DeviceBuffer coset_lo_, coset_hi_, icoset_lo_, icoset_hi_;
   NttTimings timings_;
   std::vector<hipEvent_t> ev_;

@@ -24,6 +24,33 @@ constexpr uint32_t kMaxLdsElems = 1024;
 
 enum : uint32_t { kLoadCoset = 1, kStoreScale = 2, kStoreCoset = 4 };
 
+// Twiddle tables.  BN254 Fr butterflies multiply by a Shoup product
+// (Fp::mul_shoup, mont_asm.h shoup_mul_8): an entry is the plain twiddle and
+// its quotient floor(w 2^256 / p), 64 bytes -- 13 fewer v_mad_u64_u32, 29
+// fewer carry adds and no Montgomery digits per butterfly than a Montgomery
+// product by a 32-byte Montgomery twiddle.  BLS12-381 Fr (3p > 2^256) keeps
+// Montgomery twiddles.
+template <class Fr>
+struct ShoupTw {
+  Fr w, wq;
+};
+template <class Fr>
+struct NttTw {
+  using type = Fr;
+};
+template <>
+struct NttTw<Bn254Fr> {
+  using type = ShoupTw<Bn254Fr>;
+};
+template <class Fr>
+__device__ __forceinline__ Fr tw_mul(const Fr& x, const Fr& w) {
+  return x * w;
+}
+template <class Fr>
+__device__ __forceinline__ Fr tw_mul(const Fr& x, const ShoupTw<Fr>& t) {
+  return x.mul_shoup(t.w, t.wq);
+}
+
 template <class Fr>
 struct PassArgs {
   uint32_t L, s0, k, log_m, final_pass, mode, pow_bits;
@@ -49,8 +76,8 @@ __device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
 // Twiddle of the butterfly whose low element has global index i at global
 // stage s: w_s^(i mod 2^(L-s-1)) (the reference's Radix2TwiddleCache row s).
 // kLast: the transform's last R stages (final pass, t + R == k).
-template <int R, bool kLast, class Fr, class IndexFn>
-__device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __restrict__ tw, const PassArgs<Fr>& a,
+template <int R, bool kLast, class Fr, class Tw, class IndexFn>
+__device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Tw* __restrict__ tw, const PassArgs<Fr>& a,
                                            uint32_t t, IndexFn index) {
   constexpr int E = 1 << R;
   const uint32_t log_m = a.log_m, M = 1u << log_m;
@@ -64,13 +91,13 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __res
     const uint32_t a0 = ((rr >> qlog) << (qlog + R)) + off;
     // the step's twiddles first: their global loads overlap the LDS reads
     // and the first butterflies instead of stalling each product
-    Fr wv[R][E / 2];
+    Tw wv[R][E / 2];
     if constexpr (!kLast) {
 #pragma unroll
       for (int u = 0; u < R; ++u) {
         const uint32_t st = a.s0 + t + u;
         const uint32_t gap_mask = (1u << (a.L - st - 1)) - 1;
-        const Fr* tws = tw + (n - (n >> st));
+        const Tw* tws = tw + (n - (n >> st));
         const int half = E >> (u + 1);
         int c = 0;
 #pragma unroll
@@ -86,7 +113,7 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __res
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const uint32_t st = a.s0 + t + u;
-      const Fr* tws = tw + (n - (n >> st));
+      const Tw* tws = tw + (n - (n >> st));
       const int half = E >> (u + 1);
       int c = 0;
 #pragma unroll
@@ -100,10 +127,10 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __res
           // (a0 and the set base are multiples of 2^R), known at compile time;
           // index 0 is w = 1 -- the whole last stage and half the one before
           const uint32_t idx = (uint32_t)j & ((1u << (R - 1 - u)) - 1);
-          x[j + half] = idx ? lo.sub_unreduced(hi) * tws[idx] : (lo - hi);
+          x[j + half] = idx ? tw_mul(lo.sub_unreduced(hi), tws[idx]) : (lo - hi);
         } else {
           // twiddles are canonical, so lo - hi + 2p needs no borrow test
-          x[j + half] = lo.sub_unreduced(hi) * wv[u][c++];
+          x[j + half] = tw_mul(lo.sub_unreduced(hi), wv[u][c++]);
         }
       }
     }
@@ -112,9 +139,9 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Fr* __res
   }
 }
 
-template <class Fr, int MaxR>
+template <class Fr, class Tw, int MaxR>
 __global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__ in, Fr* __restrict__ out,
-                                                          const Fr* __restrict__ tw, PassArgs<Fr> a) {
+                                                          const Tw* __restrict__ tw, PassArgs<Fr> a) {
   extern __shared__ uint4 smem_raw[];
   Fr* lds = reinterpret_cast<Fr*>(smem_raw);
   const uint32_t L = a.L, k = a.k, log_m = a.log_m;
@@ -202,9 +229,53 @@ __global__ __launch_bounds__(kBlock) void twiddle_base_kernel(Fr* __restrict__ t
   t0[j] = (lo[j & ((1u << bits) - 1)] * hi[j >> bits]).canonical();  // canonical: see radix_step
 }
 
-// T_s[j] = T_0[j << s]  (the strided sub-sampling of radix2_twiddle_cache.h:105-117)
+// floor(w 2^(32N) / p) for a canonical w < p: long division, one quotient
+// bit per step (domain setup only; needs 2p < 2^(32N))
 template <class Fr>
-__global__ __launch_bounds__(kBlock) void twiddle_stage_kernel(Fr* __restrict__ ts, const Fr* __restrict__ t0,
+__device__ Fr shoup_quotient(const Fr& w) {
+  constexpr int N = Fr::N;
+  uint32_t rem[N], q[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    rem[i] = w.v[i];
+    q[i] = 0;
+  }
+  for (int bit = 32 * N - 1; bit >= 0; --bit) {
+    uint32_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint32_t nc = rem[i] >> 31;
+      rem[i] = (rem[i] << 1) | carry;
+      carry = nc;
+    }
+    uint32_t t[N], br = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = subb(rem[i], Fr::Config::kP32[i], br, &br);
+    if (!br) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) rem[i] = t[i];
+      q[bit >> 5] |= 1u << (bit & 31);
+    }
+  }
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = q[i];
+  return r;
+}
+
+// Montgomery twiddle table -> Shoup entries {plain w, floor(w 2^256 / p)}
+template <class Fr>
+__global__ __launch_bounds__(kBlock) void shoup_table_kernel(ShoupTw<Fr>* __restrict__ out,
+                                                             const Fr* __restrict__ in, uint32_t count) {
+  uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= count) return;
+  const Fr w = in[j].from_mont();
+  out[j] = ShoupTw<Fr>{w, shoup_quotient(w)};
+}
+
+// T_s[j] = T_0[j << s]  (the strided sub-sampling of radix2_twiddle_cache.h:105-117)
+template <class T>
+__global__ __launch_bounds__(kBlock) void twiddle_stage_kernel(T* __restrict__ ts, const T* __restrict__ t0,
                                                                uint32_t count, uint32_t s) {
   uint32_t j = blockIdx.x * kBlock + threadIdx.x;
   if (j >= count) return;
@@ -336,6 +407,7 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
   // stages per register step (1 = radix-2 through LDS every stage); the
   // TACHYON_NTT_RADIX_LOG override is for A/B measurements
   if (const char* e = getenv("TACHYON_NTT_RADIX_LOG")) radix_ = std::clamp(atoi(e), 1, 3);
+  if (const char* e = getenv("TACHYON_NTT_SHOUP")) shoup_mode_ = std::clamp(atoi(e), 0, 2);
   ev_.resize(plan_.size() + 1);
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
   build_twiddles();
@@ -354,7 +426,13 @@ void NttDomain<Fr>::build_twiddles() {
   const uint32_t lb = (log_n_ - 1 + 1) / 2;  // lo bits of the base table split
   const size_t lo_cnt = size_t(1) << lb;
   const size_t hi_cnt = std::max<size_t>(1, half >> lb);
-  Fr* tw[2] = {static_cast<Fr*>(tw_fwd_.ensure(n_ * sizeof(Fr))), static_cast<Fr*>(tw_inv_.ensure(n_ * sizeof(Fr)))};
+  using Tw = typename NttTw<Fr>::type;
+  constexpr bool kShoup = !std::is_same_v<Tw, Fr>;
+  // Montgomery tables (kept: the first pass multiplies by them, see run())
+  // and, for Shoup fields, the Shoup entries derived from them
+  Tw* tab[2] = {static_cast<Tw*>(tw_fwd_.ensure(n_ * sizeof(Tw))), static_cast<Tw*>(tw_inv_.ensure(n_ * sizeof(Tw)))};
+  Fr* monts[2] = {kShoup ? static_cast<Fr*>(twm_fwd_.ensure(n_ * sizeof(Fr))) : nullptr,
+                  kShoup ? static_cast<Fr*>(twm_inv_.ensure(n_ * sizeof(Fr))) : nullptr};
   DeviceBuffer lo_d, hi_d;
   Fr* lo = static_cast<Fr*>(lo_d.ensure(lo_cnt * sizeof(Fr)));
   Fr* hi = static_cast<Fr*>(hi_d.ensure(hi_cnt * sizeof(Fr)));
@@ -366,13 +444,21 @@ void NttDomain<Fr>::build_twiddles() {
     std::vector<Fr> hi_h = host_powers(w_step, Fr::one(), hi_cnt);
     TA_HIP(hipMemcpyAsync(lo, lo_h.data(), lo_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
     TA_HIP(hipMemcpyAsync(hi, hi_h.data(), hi_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
-    hipLaunchKernelGGL(twiddle_base_kernel<Fr>, dim3(ceil_div(half, kBlock)), dim3(kBlock), 0, stream_, tw[dir], half,
+    Fr* mont = monts[dir];
+    Fr* base = kShoup ? mont : reinterpret_cast<Fr*>(tab[dir]);
+    hipLaunchKernelGGL(twiddle_base_kernel<Fr>, dim3(ceil_div(half, kBlock)), dim3(kBlock), 0, stream_, base, half,
                        lo, hi, lb);
+    if constexpr (kShoup)
+      hipLaunchKernelGGL(shoup_table_kernel<Fr>, dim3(ceil_div(half, kBlock)), dim3(kBlock), 0, stream_, tab[dir],
+                         mont, half);
     for (uint32_t s = 1; s < log_n_; ++s) {
       uint32_t cnt = (uint32_t)(n_ >> (s + 1));
-      Fr* ts = tw[dir] + (n_ - (n_ >> s));
-      hipLaunchKernelGGL(twiddle_stage_kernel<Fr>, dim3(ceil_div(cnt, kBlock)), dim3(kBlock), 0, stream_, ts, tw[dir],
-                         cnt, s);
+      Tw* ts = tab[dir] + (n_ - (n_ >> s));
+      hipLaunchKernelGGL(twiddle_stage_kernel<Tw>, dim3(ceil_div(cnt, kBlock)), dim3(kBlock), 0, stream_, ts,
+                         tab[dir], cnt, s);
+      if (kShoup)
+        hipLaunchKernelGGL(twiddle_stage_kernel<Fr>, dim3(ceil_div(cnt, kBlock)), dim3(kBlock), 0, stream_,
+                           mont + (n_ - (n_ >> s)), mont, cnt, s);
     }
     TA_HIP(hipGetLastError());
     TA_HIP(hipStreamSynchronize(stream_));  // host vectors go out of scope
@@ -414,7 +500,10 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
     return;
   }
   if (batch > 65535) throw std::runtime_error("tachyon_mi355x: NTT batch exceeds the grid limit");
-  const Fr* tw = inverse ? tw_inv_.as<Fr>() : tw_fwd_.as<Fr>();
+  using Tw = typename NttTw<Fr>::type;
+  constexpr bool kShoup = !std::is_same_v<Tw, Fr>;
+  const Tw* tw = inverse ? tw_inv_.as<Tw>() : tw_fwd_.as<Tw>();
+  const Fr* twm = kShoup ? (inverse ? twm_inv_.as<Fr>() : twm_fwd_.as<Fr>()) : reinterpret_cast<const Fr*>(tw);
   Fr* scratch = plan_.size() > 1 ? static_cast<Fr*>(scratch_.ensure(batch * n_ * sizeof(Fr))) : d_data;
   if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
   for (size_t p = 0; p < plan_.size(); ++p) {
@@ -448,8 +537,20 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
     uint32_t elems = (1u << ps.log_m) << ps.k;
     uint32_t blocks = (uint32_t)(n_ / elems);
     size_t lds = (size_t)elems * sizeof(Fr);
-    auto kern = radix_ == 1 ? dif_pass_kernel<Fr, 1> : radix_ == 2 ? dif_pass_kernel<Fr, 2> : dif_pass_kernel<Fr, 3>;
-    hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw, a);
+    // Shoup twiddles (64 B) in the passes whose stage tables are small and
+    // cache-resident; Montgomery twiddles (32 B) where the tables stream from
+    // HBM -- the first pass reads the big tables of stages 0.. once each
+    // (TACHYON_NTT_SHOUP: 0 = Montgomery everywhere, 1 = Shoup everywhere)
+    const bool shoup = kShoup && (shoup_mode_ == 1 || (shoup_mode_ == 2 && p > 0));
+    if (shoup) {
+      auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Tw, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Tw, 2>
+                                                                         : dif_pass_kernel<Fr, Tw, 3>;
+      hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw, a);
+    } else {
+      auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Fr, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Fr, 2>
+                                                                         : dif_pass_kernel<Fr, Fr, 3>;
+      hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, twm, a);
+    }
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(ev_[p + 1], stream_));
   }

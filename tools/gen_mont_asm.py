@@ -34,11 +34,14 @@ OUT = os.path.join(ROOT, "tachyon_amd", "csrc", "field", "mont_asm.h")
 NCARRY = 3
 
 
-def mac_lines(pairs, fresh_c2):
+def mac_lines(pairs, fresh_c2, carries=True):
     """pairs: list of (x_operand, y_operand) names -> asm text lines.
     fresh_c2: the first collected carry defines c2 (v_addc_co_u32 c2, .., 0, zero)
-    instead of a separate zeroing move."""
+    instead of a separate zeroing move.  carries=False: a column whose carry
+    out is discarded (only the low word is kept) -- mads only."""
     out = []
+    if not carries:
+        return [f"v_mad_u64_u32 %[acc], %[s{k % NCARRY}], %[{x}], %[{y}], %[acc]" for k, (x, y) in enumerate(pairs)]
     pos = {}  # product index -> position of its mad in `out`
 
     def collect(j):
@@ -58,32 +61,33 @@ def mac_lines(pairs, fresh_c2):
     return out
 
 
-def asm_stmt(pairs, fresh_c2=False):
+def asm_operand(v):
+    """asm input for operand name v = kind + limb index: a, b, m, wq limbs in
+    VGPRs, modulus limbs p in SGPRs."""
+    kind, idx = v[0], int(v[1:])
+    src = {"a": f"a[{idx}]", "b": f"b[{idx}]", "m": f"m[{idx}]", "w": f"wq[{idx}]"}
+    if kind == "p":
+        return f'[{v}] "s"(Cfg::kP32[{idx}])'
+    return f'[{v}] "v"({src[kind]})'
+
+
+def asm_stmt(pairs, fresh_c2=False, carries=True):
     names = []
     for x, y in pairs:
         for v in (x, y):
             if v not in names:
                 names.append(v)
-    lines = mac_lines(pairs, fresh_c2)
+    lines = mac_lines(pairs, fresh_c2, carries)
     text = "\\n\\t".join(lines)
-    ins = []
-    for v in names:
-        kind, idx = v[0], int(v[1:])
-        if kind == "a":
-            ins.append(f'[{v}] "v"(a[{idx}])')
-        elif kind == "b":
-            ins.append(f'[{v}] "v"(b[{idx}])')
-        elif kind == "m":
-            ins.append(f'[{v}] "v"(m[{idx}])')
-        elif kind == "p":
-            ins.append(f'[{v}] "s"(Cfg::kP32[{idx}])')
-    if fresh_c2:
+    ins = [asm_operand(v) for v in names]
+    if fresh_c2 and carries:
         ins.append('[z] "v"(0u)')
     c2 = '[c2] "=&v"(c2)' if fresh_c2 else '[c2] "+&v"(c2)'
     nsg = min(NCARRY, len(pairs))
     sg = ", ".join(f'[s{i}] "=&s"(sc[{i}])' for i in range(nsg))
+    outs = f'[acc] "+&v"(acc), {c2}, {sg}' if carries else f'[acc] "+&v"(acc), {sg}'
     return (f'    asm("{text}"\n'
-            f'                 : [acc] "+&v"(acc), {c2}, {sg}\n'
+            f'                 : {outs}\n'
             f'                 : {", ".join(ins)}\n'
             f'                 : "vcc");\n')
 
@@ -126,6 +130,63 @@ def gen(N):
         lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
         lines.append("  }")
     lines.append(f"  r[{N - 1}] = (uint32_t)acc;  // < 2p < 2^{32 * N}: the top word is the last one")
+    lines.append("}")
+    return "\n".join(lines) + "\n"
+
+
+SHOUP_DROP = 6  # low columns of a*wq left out of the quotient estimate
+
+
+def gen_shoup(N):
+    """Shoup product by a precomputed constant: r = a*w - q*p with
+    q = floor(a * wq / 2^(32N)), wq = floor(w * 2^(32N) / p), w < p, any
+    a < 2^(32N).  The quotient's low SHOUP_DROP columns are left out (the
+    estimate is q or q - 1), and r = lo(a*w) - lo(q*p) in [0, 3p):
+    2N^2 - D(D+1)/2 + N(N+1) products and no Montgomery digits."""
+    D = SHOUP_DROP
+    nprod = sum(min(k, N - 1) - max(0, k - N + 1) + 1 for k in range(D, 2 * N - 1)) + N * (N + 1)
+    lines = [f"// N = {N}: r = a*w mod p in [0, 3p) (Shoup; {nprod} v_mad_u64_u32); see gen_shoup",
+             "template <class Cfg>",
+             f"__device__ __forceinline__ void shoup_mul_{N}(uint32_t* __restrict__ r, const uint32_t* __restrict__ a,",
+             f"                                             const uint32_t* __restrict__ b, const uint32_t* __restrict__ wq) {{",
+             f"  uint32_t m[{N}];  // quotient estimate",
+             "  uint64_t acc = 0;",
+             f"  uint64_t sc[{NCARRY}];",
+             "  uint32_t c2;"]
+    for k in range(D, 2 * N - 1):
+        pairs = [(f"a{i}", f"w{k - i}") for i in range(max(0, k - N + 1), min(k, N - 1) + 1)]
+        lines.append(f"  {{  // quotient column {k}")
+        lines.append(asm_stmt(pairs, fresh_c2=True).rstrip("\n"))
+        if k >= N:
+            lines.append(f"    m[{k - N}] = (uint32_t)acc;")
+        lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
+        lines.append("  }")
+    lines.append(f"  m[{N - 1}] = (uint32_t)acc;  // a*wq < 2^{64 * N}: the top word")
+    # r = lo(a*w) - lo(q*p): two low-half products (the modulus stays in the
+    # SGPRs the kernel's Montgomery products already hold) and one borrow chain
+    lines.append(f"  uint32_t t[{N}];")
+    for name, x, y in (("r", "a", "b"), ("t", "m", "p")):
+        lines.append("  acc = 0;")
+        for k in range(N):
+            pairs = [(f"{x}{i}", f"{y}{k - i}") for i in range(k + 1)]
+            last = k == N - 1
+            lines.append(f"  {{  // {name}: column {k}")
+            if k == 0:
+                lines.append(f'    asm("v_mad_u64_u32 %[acc], %[s0], %[{x}0], %[{y}0], %[acc]"\n'
+                             f'                 : [acc] "+&v"(acc), [s0] "=&s"(sc[0])\n'
+                             f'                 : {asm_operand(x + "0")}, {asm_operand(y + "0")});')
+                lines.append("    c2 = 0;")
+            else:
+                lines.append(asm_stmt(pairs, fresh_c2=True, carries=not last).rstrip("\n"))
+            lines.append(f"    {name}[{k}] = (uint32_t)acc;")
+            if not last:
+                lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
+            lines.append("  }")
+    L = ["v_sub_co_u32 %[r0], vcc, %[r0], %[t0]"]
+    for i in range(1, N):
+        L += ["s_nop 1", f"v_subb_co_u32 %[r{i}], vcc, %[r{i}], %[t{i}], vcc"]
+    lines.append(asm_block(L, [f'[r{i}] "+v"(r[{i}])' for i in range(N)],
+                           [f'[t{i}] "v"(t[{i}])' for i in range(N)]).rstrip("\n"))
     lines.append("}")
     return "\n".join(lines) + "\n"
 
@@ -272,6 +333,7 @@ def main():
     for N in (8, 12):
         text.append(gen(N))
         text.append(gen_addsub(N))
+    text.append(gen_shoup(8))
     text.append("}  // namespace tachyon_amd::detail")
     with open(OUT, "w") as f:
         f.write("\n".join(text) + "\n")
