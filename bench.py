@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--cpu-log-n", type=int, default=0,
                     help="CPU baseline MSM size (0 = the headline --log-n)")
     ap.add_argument("--no-host-resident", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the configs[1]/[2] size sweeps (profiling runs: one MSM and one NTT size only)")
     ap.add_argument("--bls-log-n", type=int, default=24,
                     help="BLS12-381 G1 + G2 MSM size (BASELINE configs[3]); 0 = skip")
     ap.add_argument("--groth16-log-n", type=int, default=20,
@@ -444,7 +446,7 @@ def main():
     }
 
     # ---- configs[1] sweep (2^16, 2^20 .. 2^24: prefixes of the same device-resident input) ----
-    if world == 1 and args.log_n >= 24:
+    if world == 1 and args.log_n >= 24 and not args.no_sweep:
         sweep = {}
         for k in (16, 20, 22, 24):
             m = 1 << k
@@ -554,7 +556,7 @@ def main():
         # configs[2] sweep: 2^20 and 2^22 on prefixes of the same input (forward + inverse per rep)
         nsweep = {}
         for k in (20, 22):
-            if k >= args.ntt_log_n:
+            if k >= args.ntt_log_n or args.no_sweep:
                 continue
             m = 1 << k
             dk = Radix2EvaluationDomain(m)

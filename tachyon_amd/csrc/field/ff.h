@@ -257,6 +257,38 @@ struct Fp {
 #endif
   }
 
+  // The Shoup quotient floor(w 2^(32N) / p) of a canonical w < p (2p <
+  // 2^(32N)): long division, one quotient bit per step (table setup only)
+  TA_HD static Fp shoup_quotient(const Fp& w) {
+    uint32_t rem[N], q[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      rem[i] = w.v[i];
+      q[i] = 0;
+    }
+    for (int bit = 32 * N - 1; bit >= 0; --bit) {
+      uint32_t carry = 0;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const uint32_t nc = rem[i] >> 31;
+        rem[i] = (rem[i] << 1) | carry;
+        carry = nc;
+      }
+      uint32_t t[N], br = 0;
+#pragma unroll
+      for (int i = 0; i < N; ++i) t[i] = subb(rem[i], Cfg::kP32[i], br, &br);
+      if (!br) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) rem[i] = t[i];
+        q[bit >> 5] |= 1u << (bit & 31);
+      }
+    }
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = q[i];
+    return r;
+  }
+
   // CIOS no-carry Montgomery product (DoFastMul, prime_field_fallback.h:331-355);
   // the host path (final Horner step, conversions).
   TA_HD Fp mul_cios(const Fp& b) const {

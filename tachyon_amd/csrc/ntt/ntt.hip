@@ -229,40 +229,6 @@ __global__ __launch_bounds__(kBlock) void twiddle_base_kernel(Fr* __restrict__ t
   t0[j] = (lo[j & ((1u << bits) - 1)] * hi[j >> bits]).canonical();  // canonical: see radix_step
 }
 
-// floor(w 2^(32N) / p) for a canonical w < p: long division, one quotient
-// bit per step (domain setup only; needs 2p < 2^(32N))
-template <class Fr>
-__device__ Fr shoup_quotient(const Fr& w) {
-  constexpr int N = Fr::N;
-  uint32_t rem[N], q[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    rem[i] = w.v[i];
-    q[i] = 0;
-  }
-  for (int bit = 32 * N - 1; bit >= 0; --bit) {
-    uint32_t carry = 0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const uint32_t nc = rem[i] >> 31;
-      rem[i] = (rem[i] << 1) | carry;
-      carry = nc;
-    }
-    uint32_t t[N], br = 0;
-#pragma unroll
-    for (int i = 0; i < N; ++i) t[i] = subb(rem[i], Fr::Config::kP32[i], br, &br);
-    if (!br) {
-#pragma unroll
-      for (int i = 0; i < N; ++i) rem[i] = t[i];
-      q[bit >> 5] |= 1u << (bit & 31);
-    }
-  }
-  Fr r;
-#pragma unroll
-  for (int i = 0; i < N; ++i) r.v[i] = q[i];
-  return r;
-}
-
 // Montgomery twiddle table -> Shoup entries {plain w, floor(w 2^256 / p)}
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void shoup_table_kernel(ShoupTw<Fr>* __restrict__ out,
@@ -270,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void shoup_table_kernel(ShoupTw<Fr>* __rest
   uint32_t j = blockIdx.x * kBlock + threadIdx.x;
   if (j >= count) return;
   const Fr w = in[j].from_mont();
-  out[j] = ShoupTw<Fr>{w, shoup_quotient(w)};
+  out[j] = ShoupTw<Fr>{w, Fr::shoup_quotient(w)};
 }
 
 // T_s[j] = T_0[j << s]  (the strided sub-sampling of radix2_twiddle_cache.h:105-117)

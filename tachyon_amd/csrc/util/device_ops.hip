@@ -132,6 +132,10 @@ __global__ __launch_bounds__(kBlock) void field_op_kernel(int op, const F* a, co
     case 6: r = x.to_mont(); break;
     case 7: r = x.from_mont(); break;
     case 8: r = x.dbl(); break;
+    case 9:  // x (any value < 2^(32N)) times the plain canonical constant y
+      if constexpr (F::N == 8 && F::kLazyCapable) r = x.mul_shoup(y, F::shoup_quotient(y));
+      else r = x * y.to_mont();
+      break;
     default: r = F::zero();
   }
   out[i] = r.canonical();

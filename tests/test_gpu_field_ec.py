@@ -12,7 +12,8 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-OPS = {"add": 0, "sub": 1, "mul": 2, "sqr": 3, "neg": 4, "inv": 5, "to_mont": 6, "from_mont": 7, "dbl": 8}
+OPS = {"add": 0, "sub": 1, "mul": 2, "sqr": 3, "neg": 4, "inv": 5, "to_mont": 6, "from_mont": 7, "dbl": 8,
+       "mul_const": 9}
 
 
 def gpu_field_op(field, op, a: bytes, b: bytes) -> bytes:
@@ -96,3 +97,34 @@ def _r_minus_1(curve):
     sf = O.CURVE_INFO[curve][1]
     r = P.FIELDS[sf][0]
     return (r - 1).to_bytes(32, "little")
+
+
+def test_twiddle_product_shoup_bn254_fr():
+    """Field op 9 = the NTT butterfly's twiddle product (Fp::mul_shoup on
+    BN254 Fr): x * w mod p for ANY 256-bit x (the butterfly feeds it the
+    unreduced lo - hi + 2p) and a plain canonical w.  The quotient estimate
+    leaves out the low columns of x * floor(w 2^256 / p); the crafted x below
+    make x * wq = t (mod 2^256) for small t, so the dropped columns carry into
+    the kept ones and the estimate is one short -- the branch that maps
+    [2p, 3p) back into the lazy range.  Pinned by Python big integers."""
+    import random
+    p = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+    rnd = random.Random(7)
+    xs, ws = [], []
+    for _ in range(2000):
+        xs.append(rnd.randrange(1 << 256))
+        ws.append(rnd.randrange(p))
+    for t in range(1, 2001):  # crafted: x * wq = t (mod 2^256)
+        while True:
+            w = rnd.randrange(p)
+            wq = (w << 256) // p
+            if wq & 1:
+                break
+        xs.append((t * pow(wq, -1, 1 << 256)) % (1 << 256))
+        ws.append(w)
+    xs += [0, (1 << 256) - 1, p, 4 * p - 1, 5 * p]
+    ws += [p - 1, p - 1, 1, p - 1, 0]
+    enc = lambda v: v.to_bytes(32, "little")
+    got = gpu_field_op("bn254_fr", "mul_const", b"".join(map(enc, xs)), b"".join(map(enc, ws)))
+    for k, (x, w) in enumerate(zip(xs, ws)):
+        assert int.from_bytes(got[32 * k:32 * k + 32], "little") == x * w % p, (k, hex(x), hex(w))

@@ -12,7 +12,7 @@ TAG=${1:-r01}; shift || true
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-resident --groth16-log-n 0 --bls-log-n 0 $*"
+B="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-resident --no-sweep --groth16-log-n 0 --bls-log-n 0 $*"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- $B > $OUT/bench_under_trace.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $B > $OUT/fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- $B > $OUT/write.log 2>&1
