@@ -189,8 +189,8 @@ struct AccWaves<Bls381G2> {
   static constexpr int value = 2;
 };
 
-template <class Curve>
-__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
+template <class Curve, int kDepth, int kWaves>
+__global__ __launch_bounds__(kBlock, kWaves) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
                                                          const uint64_t* __restrict__ ents, uint32_t c,
                                                          uint64_t gbeg, uint64_t gend, uint64_t tbase,
                                                          uint32_t K, uint32_t idx_mask,
@@ -225,17 +225,19 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
   // input, so a plain limb OR -- add nothing, and madd_nz reports the rare
   // cancellation P = -acc.  Signed digits negate y as p - y by limb selects.
   bool acc_zero = true;
-  // two-deep software pipeline: (key, val) for g+2 and the base for g+1 are
-  // in flight while the madd for g runs
-  const uint64_t e0 = ents[g0];
-  uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
-  uint32_t k1 = 0, v1 = 0;
-  if (g0 + 1 < g1) { const uint64_t e = ents[g0 + 1]; k1 = entry_key(e); v1 = entry_val(e); }
-  Affine<F> P = hbases[v0 & idx_mask];
+  // software pipeline kDepth deep: the entries of g+1 .. g+kDepth and the
+  // bases of g+1 .. g+kDepth-1 are in flight while the madd for g runs
+  uint64_t ew[kDepth + 1];
+  Affine<F> Pw[kDepth];
+#pragma unroll
+  for (int d = 0; d < kDepth; ++d) ew[d] = (g0 + d < g1) ? ents[g0 + d] : 0;
+#pragma unroll
+  for (int d = 0; d + 1 < kDepth; ++d) Pw[d] = hbases[entry_val(ew[d]) & idx_mask];
   for (uint64_t g = g0; g < g1; ++g) {
-    uint32_t k2 = 0, v2 = 0;
-    if (g + 2 < g1) { const uint64_t e = ents[g + 2]; k2 = entry_key(e); v2 = entry_val(e); }
-    Affine<F> Pn = hbases[v1 & idx_mask];
+    ew[kDepth] = (g + kDepth < g1) ? ents[g + kDepth] : 0;
+    Pw[kDepth - 1] = hbases[entry_val(ew[kDepth - 1]) & idx_mask];
+    const uint32_t k0 = entry_key(ew[0]), v0 = entry_val(ew[0]);
+    Affine<F> P = Pw[0];
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
       if (b != cur) {
@@ -266,8 +268,10 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
         acc = acc.madd(P);
       }
     }
-    k0 = k1; v0 = v1; k1 = k2; v1 = v2;
-    P = Pn;
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) ew[d] = ew[d + 1];
+#pragma unroll
+    for (int d = 0; d + 1 < kDepth; ++d) Pw[d] = Pw[d + 1];
   }
   if (acc_zero) acc = XYZZ<F>::zero();
   if (cur != kNoBucket) {  // the last run
@@ -634,9 +638,19 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
-    hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
-                       (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
-                       tflags, tlast);
+    // gather pipeline depth and minimum waves per SIMD (A/B: set_variant
+    // bits 10-11 = 1: depth 3, 2: depth 2 at >= 4 waves, 3: depth 3 at >= 4)
+    constexpr int kW = AccWaves<Curve>::value;
+    constexpr int kW4 = kW > 4 ? kW : 4;
+    auto acc_kernel = seg_acc_kernel<Curve, 2, kW>;
+    switch ((variant_ >> 10) & 3) {
+      case 1: acc_kernel = seg_acc_kernel<Curve, 3, kW>; break;
+      case 2: acc_kernel = seg_acc_kernel<Curve, 2, kW4>; break;
+      case 3: acc_kernel = seg_acc_kernel<Curve, 3, kW4>; break;
+      default: break;
+    }
+    hipLaunchKernelGGL(acc_kernel, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c, (uint64_t)e0,
+                       (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces, tflags, tlast);
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(gev_acc1_[g], stream_));
     tbase += Tg;

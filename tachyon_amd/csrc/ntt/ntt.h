@@ -89,6 +89,7 @@ class NttDomain {
   DeviceBuffer tw_fwd_, tw_inv_, scratch_, io_;
   DeviceBuffer twm_fwd_, twm_inv_;  // Montgomery twiddles when tw_* hold Shoup entries (BN254 Fr)
   int shoup_mode_ = 2;              // Shoup twiddles: 0 never, 1 every pass, 2 all but the first pass
+  int ntt_variant_ = 0;             // A/B kernel variants (TACHYON_NTT_VARIANT, see run())
   DeviceBuffer coset_lo_, coset_hi_, icoset_lo_, icoset_hi_;
   NttTimings timings_;
   std::vector<hipEvent_t> ev_;

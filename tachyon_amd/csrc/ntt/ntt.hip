@@ -76,7 +76,7 @@ __device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
 // Twiddle of the butterfly whose low element has global index i at global
 // stage s: w_s^(i mod 2^(L-s-1)) (the reference's Radix2TwiddleCache row s).
 // kLast: the transform's last R stages (final pass, t + R == k).
-template <int R, bool kLast, class Fr, class Tw, class IndexFn>
+template <int R, bool kLast, bool kPrefetch, class Fr, class Tw, class IndexFn>
 __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Tw* __restrict__ tw, const PassArgs<Fr>& a,
                                            uint32_t t, IndexFn index) {
   constexpr int E = 1 << R;
@@ -92,7 +92,7 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Tw* __res
     // the step's twiddles first: their global loads overlap the LDS reads
     // and the first butterflies instead of stalling each product
     Tw wv[R][E / 2];
-    if constexpr (!kLast) {
+    if constexpr (!kLast && kPrefetch) {
 #pragma unroll
       for (int u = 0; u < R; ++u) {
         const uint32_t st = a.s0 + t + u;
@@ -130,7 +130,12 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Tw* __res
           x[j + half] = idx ? tw_mul(lo.sub_unreduced(hi), tws[idx]) : (lo - hi);
         } else {
           // twiddles are canonical, so lo - hi + 2p needs no borrow test
-          x[j + half] = tw_mul(lo.sub_unreduced(hi), wv[u][c++]);
+          if constexpr (kPrefetch) {
+            x[j + half] = tw_mul(lo.sub_unreduced(hi), wv[u][c++]);
+          } else {
+            const uint32_t gap_mask = (1u << (a.L - st - 1)) - 1;
+            x[j + half] = tw_mul(lo.sub_unreduced(hi), tws[index(a0 + ((uint32_t)j << qlog), m) & gap_mask]);
+          }
         }
       }
     }
@@ -139,8 +144,8 @@ __device__ __forceinline__ void radix_step(Fr* __restrict__ lds, const Tw* __res
   }
 }
 
-template <class Fr, class Tw, int MaxR>
-__global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__ in, Fr* __restrict__ out,
+template <class Fr, class Tw, int MaxR, bool kPrefetch = true, int kWaves = 1>
+__global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __restrict__ in, Fr* __restrict__ out,
                                                           const Tw* __restrict__ tw, PassArgs<Fr> a) {
   extern __shared__ uint4 smem_raw[];
   Fr* lds = reinterpret_cast<Fr*>(smem_raw);
@@ -187,14 +192,14 @@ __global__ __launch_bounds__(kBlock) void dif_pass_kernel(const Fr* __restrict__
     const uint32_t R = min((uint32_t)MaxR, k - t);
     const bool last = a.final_pass && t + R == k;
     if (MaxR >= 3 && R == 3) {
-      if (last) radix_step<3, true>(lds, tw, a, t, index);
-      else radix_step<3, false>(lds, tw, a, t, index);
+      if (last) radix_step<3, true, kPrefetch>(lds, tw, a, t, index);
+      else radix_step<3, false, kPrefetch>(lds, tw, a, t, index);
     } else if (MaxR >= 2 && R == 2) {
-      if (last) radix_step<2, true>(lds, tw, a, t, index);
-      else radix_step<2, false>(lds, tw, a, t, index);
+      if (last) radix_step<2, true, kPrefetch>(lds, tw, a, t, index);
+      else radix_step<2, false, kPrefetch>(lds, tw, a, t, index);
     } else {
-      if (last) radix_step<1, true>(lds, tw, a, t, index);
-      else radix_step<1, false>(lds, tw, a, t, index);
+      if (last) radix_step<1, true, kPrefetch>(lds, tw, a, t, index);
+      else radix_step<1, false, kPrefetch>(lds, tw, a, t, index);
     }
     t += R;
     __syncthreads();
@@ -374,6 +379,7 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
   // TACHYON_NTT_RADIX_LOG override is for A/B measurements
   if (const char* e = getenv("TACHYON_NTT_RADIX_LOG")) radix_ = std::clamp(atoi(e), 1, 3);
   if (const char* e = getenv("TACHYON_NTT_SHOUP")) shoup_mode_ = std::clamp(atoi(e), 0, 2);
+  if (const char* e = getenv("TACHYON_NTT_VARIANT")) ntt_variant_ = atoi(e);
   ev_.resize(plan_.size() + 1);
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
   build_twiddles();
@@ -508,13 +514,18 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
     // HBM -- the first pass reads the big tables of stages 0.. once each
     // (TACHYON_NTT_SHOUP: 0 = Montgomery everywhere, 1 = Shoup everywhere)
     const bool shoup = kShoup && (shoup_mode_ == 1 || (shoup_mode_ == 2 && p > 0));
+    // (A/B, TACHYON_NTT_VARIANT: bit 0 = the Montgomery radix-4 pass at >= 5
+    // waves/SIMD, bit 1 = the Shoup radix-4 passes without the twiddle
+    // prefetch at >= 5 waves/SIMD)
     if (shoup) {
       auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Tw, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Tw, 2>
                                                                          : dif_pass_kernel<Fr, Tw, 3>;
+      if (radix_ == 2 && (ntt_variant_ & 2)) kern = dif_pass_kernel<Fr, Tw, 2, false, 5>;
       hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw, a);
     } else {
       auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Fr, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Fr, 2>
                                                                          : dif_pass_kernel<Fr, Fr, 3>;
+      if (radix_ == 2 && (ntt_variant_ & 1)) kern = dif_pass_kernel<Fr, Fr, 2, true, 5>;
       hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, twm, a);
     }
     TA_HIP(hipGetLastError());
