@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--cpu-log-n", type=int, default=0,
                     help="CPU baseline MSM size (0 = the headline --log-n)")
     ap.add_argument("--no-host-resident", action="store_true")
+    ap.add_argument("--msm-split", choices=("points", "windows"), default="points",
+                    help="N > 1 MSM partition: point shards (default), or window ranges with every rank holding "
+                         "all points (c = 16: W = 16 windows; measured slower per rank, tools/split_probe.py)")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the configs[1]/[2] size sweeps (profiling runs: one MSM and one NTT size only)")
     ap.add_argument("--bls-log-n", type=int, default=24,
@@ -355,7 +358,15 @@ def main():
     # ---- MSM inputs (device-resident, this rank's shard) ----
     from tachyon_amd import dist as D
     n_total = 1 << args.log_n
-    start, n = D.shard_range(n_total, rank, world)
+    # N > 1: point shards of one global input (each rank n/N points, all W
+    # windows; default) or the window split (each rank all n points, W/N of
+    # W = 16 windows) -- per-rank cost at 2^26 / 8 ranks 14.4 vs 16.2 ms: the
+    # split's recode of all n scalars per rank and its 2 x 2^26 additions
+    # (vs 15 x 2^23 at the shard's c = 17) outweigh the smaller bucket set
+    split = args.msm_split
+    if world == 1:
+        split = "points"
+    start, n = D.shard_range(n_total, rank, world) if split == "points" else (0, n_total)
     d_bases = torch.empty(max(1, n) * 64, dtype=torch.uint8, device="cuda")
     d_scalars = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
     chunk = 1 << 10
@@ -365,11 +376,22 @@ def main():
     torch.cuda.synchronize()
 
     msm = M.VariableBaseMSMGpu("bn254_g1")
-    if args.window_bits:
+    split_c = args.window_bits or 16
+    if split == "windows":
+        w_lo, w_hi = D.window_range(D._windows_for("bn254_g1", split_c), rank, world)
+        msm.set_window_bits(split_c)
+    elif args.window_bits:
         msm.set_window_bits(args.window_bits)
 
+    def local_run():
+        if split == "windows":
+            return msm.run_window_range(d_bases, d_scalars, w_lo, w_hi, n)
+        return msm.run(d_bases, d_scalars, n)
+
     def step():
-        return D.sharded_msm("bn254_g1", lambda: msm.run(d_bases, d_scalars, n), device="cuda")
+        if split == "windows":
+            return D.window_split_msm("bn254_g1", msm, d_bases, d_scalars, n, split_c, device="cuda")
+        return D.sharded_msm("bn254_g1", local_run, device="cuda")
 
     for _ in range(args.warmup):
         ref = step()
@@ -391,17 +413,24 @@ def main():
     msm.set_profile(True)
     prof = []
     for _ in range(3):
-        msm.run(d_bases, d_scalars, n)
+        local_run()
         prof.append(msm.last_timings())
     msm.set_profile(False)
     phases = {k: round(sorted(p[k] for p in prof)[1], 4) for k in prof[0]}
     launches = max(1, int(prof[0]["acc_launches"]))
     acc_ms = sorted(p["acc"] for p in prof)[1] / launches
     c, windows = M.plan("bn254_g1", n)
+    rank_windows = windows
+    if split == "windows":
+        c, windows = split_c, D._windows_for("bn254_g1", split_c)
+        rank_windows = w_hi - w_lo
+    elif args.window_bits:
+        c, windows = args.window_bits, D._windows_for("bn254_g1", args.window_bits)
+        rank_windows = windows
     # one launch accumulates every (point, window) digit of the windows it
     # covers: n x windows / launches point-window units of 96 B each (the
     # point's base + scalar bytes, consumed once per window)
-    units = n * windows / launches
+    units = n * rank_windows / launches
     acc_gbs = units * MSM_BYTES_PER_POINT / (acc_ms * 1e-3) / 1e9
     acc_traffic, acc_traffic_src, acc_traffic_raw = pmc_traffic("seg_acc_kernel")
     acc_gmulmod = units * MADD_MULMODS / (acc_ms * 1e-3) / 1e9
@@ -423,7 +452,10 @@ def main():
         "config": {"workload": f"BN254 G1 VariableBaseMSM 2^{args.log_n} (BASELINE configs[1]), device-resident "
                                f"inputs, result normalised to affine on the host",
                    "msm_log_n": args.log_n, "points_per_gpu": n, "window_bits": c, "windows": windows,
-                   "parallelism": f"msm point shards x{world} + RCCL all-gather of partial points"},
+                   "windows_per_gpu": rank_windows,
+                   "parallelism": (f"msm window ranges x{world} (every rank all points, {rank_windows} of {windows} "
+                                   f"windows) + RCCL all-gather of partial points" if split == "windows" else
+                                   f"msm point shards x{world} + RCCL all-gather of partial points")},
         "consistent_across_steps": consistent,
         "consistent_with_1gpu": consistent_1gpu,
         "roofline": {"bound": "hbm", "achieved": acc_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -302,6 +302,16 @@ TACHYON_C_EXPORT tachyon_bls12_381_g2_jacobian* tachyon_bls12_381_g2_affine_msm_
 /* Affine result written to out_affine (identity = all zero bytes). */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const void* bases, const void* scalars,
                                                     size_t size, void* out_affine);
+/* The windows [w_begin, w_end) of the MSM only (window bits: the context's
+ * set_window_bits, else the size's default; W = ceil((bits + 1) / c)):
+ * sum over them of 2^(c w) * S_w, S_w = window w's bucket sum
+ * (pippenger_base.h:59-77 restricted to the range).  Ranges that tile
+ * [0, W) sum to the full MSM -- the multi-GPU window split, every rank
+ * holding all points.  Affine result as in _msm_gpu_affine. */
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_window_range_affine(int curve, void* ctx, const void* bases,
+                                                                 const void* scalars, size_t size,
+                                                                 unsigned w_begin, unsigned w_end,
+                                                                 void* out_affine);
 /* Contexts for the C++ plugin boundary (include/tachyon_mi355x_msm.h):
  * VariableBaseMSMGpu<Point>(mem_pool, stream) (variable_base_msm_gpu.h:16-18)
  * over any of the four groups, its work on `stream` (hipStream_t; NULL = a
@@ -319,7 +329,7 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ct
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule).
  * Every accepted variant computes the same MSM; returns 0 (nothing changed)
- * for bits outside 0x3BF. */
+ * for bits outside 0xFBF. */
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
  * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total,

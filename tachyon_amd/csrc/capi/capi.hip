@@ -142,6 +142,15 @@ void msm_affine_out(void* ctx, const void* bases, const void* scalars, size_t n,
   memcpy(out, &a, sizeof(a));
 }
 
+template <class Curve>
+void msm_window_range_out(void* ctx, const void* bases, const void* scalars, size_t n, unsigned w_begin,
+                          unsigned w_end, void* out) {
+  using F = typename Curve::F;
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  Affine<F> a = c->impl.run_window_range(bases, scalars, n, w_begin, w_end).to_affine();
+  memcpy(out, &a, sizeof(a));
+}
+
 // The MSM in the point form a C++ caller asks for (include/tachyon_mi355x_msm.h):
 // 0 affine {x, y} ((0, 0) = identity); 1 projective / 2 Jacobian {x, y, z}
 // (identity (1, 1, 0), projective_point.h:34-36, jacobian_point.h; otherwise
@@ -334,6 +343,11 @@ tachyon_bls12_381_g2_jacobian* tachyon_bls12_381_g2_affine_msm_gpu(tachyon_bls12
 void tachyon_mi355x_msm_gpu_affine(int curve, void* ctx, const void* bases, const void* scalars, size_t size,
                                    void* out_affine) {
   GUARD_BEGIN CURVE_DISPATCH(curve, msm_affine_out<C>(ctx, bases, scalars, size, out_affine)) GUARD_END
+}
+void tachyon_mi355x_msm_gpu_window_range_affine(int curve, void* ctx, const void* bases, const void* scalars,
+                                                size_t size, unsigned w_begin, unsigned w_end, void* out_affine) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, msm_window_range_out<C>(ctx, bases, scalars, size, w_begin, w_end, out_affine))
+  GUARD_END
 }
 void* tachyon_mi355x_msm_gpu_create(int curve, void* stream) {
   GUARD_BEGIN CURVE_DISPATCH(curve, return new MsmCtx<C>(static_cast<hipStream_t>(stream))) GUARD_END

@@ -38,7 +38,13 @@ struct MsmPlan {
   unsigned levels = 0;   // number of K2 levels
   unsigned seg = 0;      // buckets per running-sum segment
   unsigned group = 0;    // windows per sort/accumulate pipeline stage
-  static inline MsmPlan make(size_t n, unsigned scalar_bits, unsigned force_c = 0);
+  // the windows this run computes, [w_begin, w_end) of the W (default all):
+  // a window-range MSM is the sum over those windows of 2^(c w) S_w, so the
+  // windows of one MSM can be split across devices (run_window_range)
+  unsigned w_begin = 0, w_end = 0;
+  unsigned active() const { return w_end - w_begin; }
+  static inline MsmPlan make(size_t n, unsigned scalar_bits, unsigned force_c = 0, unsigned w_begin = 0,
+                             unsigned w_end = ~0u);
 };
 
 // Window size: more bits -> fewer windows (fewer madds, fewer sort passes)
@@ -53,7 +59,7 @@ inline unsigned default_window_bits(unsigned lg) {
   return kBest[std::min<unsigned>(lg, 26) - 16];
 }
 
-inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
+inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, unsigned w_begin, unsigned w_end) {
   MsmPlan p;
   unsigned lg = 1;
   while ((size_t(1) << lg) < n) ++lg;
@@ -61,13 +67,15 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
   p.c = c;
   p.windows = (scalar_bits + 1 + c - 1) / c;  // W*c >= bits+1
   p.buckets = 1u << (c - 1);
-  size_t entries = (size_t)n * p.windows;
+  p.w_end = std::min(w_end, p.windows);
+  p.w_begin = std::min(w_begin, p.w_end);
+  size_t entries = (size_t)n * p.active();
   // One sort + one accumulation launch over all windows.  (Pipelining one
   // window at a time -- window w+1 sorting on a second stream while window w
   // accumulates -- measured slower at 2^26: 108 vs 99 ms; the onesweep sort
   // and the accumulation slow each other down by about the time they
   // overlap.  set_variant bits 2-3 keep it for experiments.)
-  p.group = p.windows;
+  p.group = p.active();
   // entries per accumulation thread: ~2^18 threads with K in [16, 64] below
   // 2^26 entries, then 128, and 256 from 2^29 entries.  Longer runs per
   // thread leave fewer bucket pieces for the chain join, which dominates the
@@ -91,7 +99,7 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c) {
   // running-sum segment length: long segments amortise the (jL)*R fix-up, but
   // small MSMs need >= ~64K segment threads to fill the chip (a 2^16 MSM with
   // 64-bucket segments ran 208 threads of ~2000 serial mulmods each)
-  size_t nb = (size_t)p.windows * p.buckets;
+  size_t nb = (size_t)p.active() * p.buckets;
   unsigned seg = 2;
   while (seg < 64 && ((nb / (seg * 2)) >= 65536)) seg *= 2;
   p.seg = std::min<unsigned>(p.buckets, seg);
@@ -122,10 +130,16 @@ class MsmGpu {
   // Returns the MSM as an XYZZ point (host memory).
   Point run(const void* bases, const void* scalars, size_t n);
 
-  // Window sums only (for multi-GPU: each rank ships W points) -- device work
-  // identical to run(); `out` gets plan.windows points.
+  // Window sums only -- device work identical to run(); `out` gets
+  // plan.active() points (the windows of the range set by run_window_range,
+  // all W otherwise).
   void run_windows(const void* bases, const void* scalars, size_t n, std::vector<Point>* out,
                    MsmPlan* plan_out);
+
+  // The windows [w_begin, w_end) of the MSM only: sum_w 2^(c w) S_w over
+  // them (c = the forced window bits or the size's default).  Summing the
+  // results of ranges that tile [0, W) gives run(); multi-GPU window split.
+  Point run_window_range(const void* bases, const void* scalars, size_t n, unsigned w_begin, unsigned w_end);
 
   static Point combine_windows(const std::vector<Point>& window_sums, unsigned c);
 
@@ -182,6 +196,7 @@ class MsmGpu {
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;
   size_t last_divisions_ = 1;
+  unsigned range_begin_ = 0, range_end_ = ~0u;  // window range of the next run_windows
 };
 
 extern template class MsmGpu<Bn254G1>;

@@ -39,8 +39,11 @@ enum : uint32_t { kHead = 1, kTail = 2, kSingle = 4 };
 // on bits [32, 32 + key bits) (keys-only, one array) and the accumulation
 // reads one 8-byte word per entry.
 // Signed c-bit digits of one scalar, window by window: emit(w, key, val).
+// Windows [w0, w0 + wr) of W are emitted, as local windows 0 .. wr-1 (the
+// lower windows still run for their carries).
 template <class Fr, class Emit>
-__device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsigned c, unsigned W, Emit emit) {
+__device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsigned c, unsigned W, unsigned w0,
+                                              unsigned wr, Emit emit) {
   constexpr int N = Fr::N;
   Fr s = scalar.from_mont();
   uint32_t limbs[N];
@@ -49,7 +52,7 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
   const uint32_t mask = (1u << c) - 1;
   const uint32_t half = 1u << (c - 1);
   uint32_t carry = 0;
-  for (unsigned w = 0; w < W; ++w) {
+  for (unsigned w = 0; w < w0 + wr; ++w) {
     uint32_t coeff = (limbs[0] & mask) + carry;
     // shift the scalar right by c (c < 32), constant-indexed limbs only
 #pragma unroll
@@ -65,7 +68,7 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
       key = coeff;  // top digit, carry folded in, non-negative
       sign = 0;
     }
-    emit(w, (w << c) | key, i | sign);
+    if (w >= w0) emit(w - w0, ((w - w0) << c) | key, i | sign);
   }
 }
 
@@ -75,11 +78,11 @@ __device__ __forceinline__ uint32_t entry_val(uint64_t e) { return (uint32_t)e; 
 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
-                                                        unsigned c, unsigned W,
+                                                        unsigned c, unsigned W, unsigned w0, unsigned wr,
                                                         uint64_t* __restrict__ ents) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  recode_scalar(scalars[i], i, c, W, [&](unsigned w, uint32_t key, uint32_t val) {
+  recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned w, uint32_t key, uint32_t val) {
     ents[(size_t)w * n + i] = make_entry(key, val);
   });
 }
@@ -98,7 +101,8 @@ constexpr unsigned kRecodeSpt = 2;  // default scalars per thread of the fused r
 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restrict__ scalars, uint32_t n, unsigned c,
-                                                             unsigned W, uint32_t nblocks, uint32_t spt,
+                                                             unsigned W, unsigned w0, unsigned wr,
+                                                             uint32_t nblocks, uint32_t spt,
                                                              uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[256];
   cnt[threadIdx.x] = 0;
@@ -106,7 +110,8 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
   for (uint32_t k = 0; k < spt; ++k) {
     const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + threadIdx.x;
     if (i < n)
-      recode_scalar(scalars[i], i, c, W, [&](unsigned, uint32_t key, uint32_t) { atomicAdd(&cnt[key & 255], 1u); });
+      recode_scalar(scalars[i], i, c, W, w0, wr,
+                    [&](unsigned, uint32_t key, uint32_t) { atomicAdd(&cnt[key & 255], 1u); });
   }
   __syncthreads();
   hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
@@ -114,14 +119,15 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __restrict__ scalars, uint32_t n,
-                                                                unsigned c, unsigned W, uint32_t nblocks, uint32_t spt,
+                                                                unsigned c, unsigned W, unsigned w0, unsigned wr,
+                                                                uint32_t nblocks, uint32_t spt,
                                                                 const uint32_t* __restrict__ hist,
                                                                 const uint32_t* __restrict__ off,
                                                                 uint64_t* __restrict__ ents) {
   // the block's entries are binned in LDS first, then written out bin run by
   // bin run, so consecutive lanes store to consecutive addresses
   extern __shared__ uint64_t lds_u64[];
-  uint64_t* lents = lds_u64;                      // spt * kBlock * W
+  uint64_t* lents = lds_u64;                      // spt * kBlock * wr
   __shared__ uint32_t base[256], loff[256], cur[256];
   const uint32_t t = threadIdx.x;
   base[t] = off[(size_t)t * nblocks + blockIdx.x];
@@ -143,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
   for (uint32_t k = 0; k < spt; ++k) {
     const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + t;
     if (i < n)
-      recode_scalar(scalars[i], i, c, W, [&](unsigned, uint32_t key, uint32_t val) {
+      recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned, uint32_t key, uint32_t val) {
         const uint32_t bin = key & 255;
         const uint32_t p = loff[bin] + atomicAdd(&cur[bin], 1u);
         lents[p] = make_entry(key, val);
@@ -521,7 +527,9 @@ hipError_t MsmGpu<Curve>::sort_entries(void* tmp, size_t& bytes, const uint64_t*
 template <class Curve>
 void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan,
                             Point* d_windows) {
-  const unsigned W = plan.windows, B = plan.buckets, c = plan.c;
+  // W = the windows this run computes (plan.active()); Wt = all windows of
+  // the scalar (the recode's carry chain), the range starting at window w0
+  const unsigned W = plan.active(), Wt = plan.windows, wr0 = plan.w_begin, B = plan.buckets, c = plan.c;
   const size_t entries = n * W;
   const size_t nb = (size_t)W * B;
   if (n >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM size must be < 2^31 per device");
@@ -580,7 +588,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     uint32_t* hist = static_cast<uint32_t*>(hist_.ensure(2 * hn * 4));
     uint32_t* hoff = hist + hn;
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       W, nblocks, spt, hist);
+                       Wt, wr0, W, nblocks, spt, hist);
     TA_HIP(hipGetLastError());
     size_t hscan_bytes = 0;
     TA_HIP(rocprim::exclusive_scan(nullptr, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
@@ -594,10 +602,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       scatter_lds_set_ = true;
     }
     hipLaunchKernelGGL(recode_scatter_kernel<Fr>, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars,
-                       (uint32_t)n, c, W, nblocks, spt, hist, hoff, dst);
+                       (uint32_t)n, c, Wt, wr0, W, nblocks, spt, hist, hoff, dst);
   } else {
     hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       W, ents);
+                       Wt, wr0, W, ents);
   }
   TA_HIP(hipGetLastError());
   // every bucket without an entry stays the identity
@@ -740,7 +748,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
 template <class Curve>
 void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n, std::vector<Point>* out,
                                 MsmPlan* plan_out) {
-  MsmPlan plan = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_);
+  MsmPlan plan = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_, range_begin_, range_end_);
   switch (variant_ & 3) {  // accumulation chunk experiments
     case 1: plan.K = std::min(2048u, plan.K * 2); break;
     case 2: plan.K = std::min(2048u, plan.K * 4); break;
@@ -750,7 +758,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   switch ((variant_ >> 2) & 3) {  // windows per sort/accumulate group
     case 1: plan.group = 1; break;
     case 2: plan.group = 2; break;
-    case 3: plan.group = plan.windows; break;
+    case 3: plan.group = plan.active(); break;
     default: break;
   }
   idx_mask_ = ~kSignBit;
@@ -759,8 +767,8 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   recode_spt_ = kSpt[(variant_ >> 8) & 3];  // bits 8-9: scalars per thread of the fused recode
   sort_cfg_ = (variant_ >> 4) & 3;  // bits 4-5: onesweep tile shape
   if (plan_out) *plan_out = plan;
-  out->assign(plan.windows, Point::zero());
-  if (n == 0) return;
+  out->assign(plan.active(), Point::zero());
+  if (n == 0 || plan.active() == 0) return;
   if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
   const Aff* d_bases = static_cast<const Aff*>(bases);
   const Fr* d_scalars = static_cast<const Fr*>(scalars);
@@ -774,9 +782,9 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
     TA_HIP(hipMemcpyAsync(p, scalars, n * sizeof(Fr), hipMemcpyHostToDevice, stream_));
     d_scalars = static_cast<const Fr*>(p);
   }
-  Point* d_windows = static_cast<Point*>(windows_.ensure(plan.windows * sizeof(Point)));
+  Point* d_windows = static_cast<Point*>(windows_.ensure(std::max(1u, plan.active()) * sizeof(Point)));
   enqueue(d_bases, d_scalars, n, plan, d_windows);
-  TA_HIP(hipMemcpyAsync(out->data(), d_windows, plan.windows * sizeof(Point), hipMemcpyDeviceToHost, stream_));
+  TA_HIP(hipMemcpyAsync(out->data(), d_windows, plan.active() * sizeof(Point), hipMemcpyDeviceToHost, stream_));
   TA_HIP(hipStreamSynchronize(stream_));
   for (auto& p : *out) p = p.canonical();  // device values live in [0, 2p)
   if (profile_) {
@@ -904,14 +912,14 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_host_pipelined(const void* base
 // pieces and chain tables, bucket and segment sums), plus 10 %.
 template <class Curve>
 size_t MsmGpu<Curve>::work_bytes(size_t n) const {
-  const MsmPlan p = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_);
-  const size_t entries = n * p.windows;
+  const MsmPlan p = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_, range_begin_, range_end_);
+  const size_t entries = n * p.active();
   const size_t T = (entries + p.K - 1) / p.K;
   size_t bytes = entries * 16 + entries / 2;                 // entries (x2) + onesweep scratch
   bytes += (2 * T + 2 * T / p.K2 + T + 2) * sizeof(Point);   // pieces + first join level
   bytes += (T + 2) * 4 * 9;                                  // flags, last bucket, chain tables
-  bytes += (size_t)p.windows * p.buckets * sizeof(Point);    // bucket sums
-  bytes += 2 * (size_t)p.windows * (p.buckets / p.seg) * sizeof(Point);
+  bytes += (size_t)p.active() * p.buckets * sizeof(Point);    // bucket sums
+  bytes += 2 * (size_t)p.active() * (p.buckets / p.seg) * sizeof(Point);
   return bytes + bytes / 10;
 }
 
@@ -985,6 +993,27 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* 
     total = total + combine_windows(ws, plan.c);
   }
   return total;
+}
+
+// The windows [w_begin, w_end) alone (PippengerBase::AccumulateWindowSums
+// restricted to them): Horner over the range, then c * w_begin doublings.
+template <class Curve>
+typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_window_range(const void* bases, const void* scalars, size_t n,
+                                                              unsigned w_begin, unsigned w_end) {
+  struct Reset {
+    MsmGpu* m;
+    ~Reset() { m->range_begin_ = 0; m->range_end_ = ~0u; }
+  } reset{this};
+  range_begin_ = w_begin;
+  range_end_ = w_end;
+  last_divisions_ = 1;
+  std::vector<Point> ws;
+  MsmPlan plan;
+  run_windows(bases, scalars, n, &ws, &plan);
+  if (n == 0 || plan.active() == 0) return Point::zero();
+  Point p = combine_windows(ws, plan.c);
+  for (unsigned k = 0; k < plan.c * plan.w_begin; ++k) p = p.dbl();
+  return p;
 }
 
 }  // namespace tachyon_amd::msm

@@ -82,6 +82,16 @@ class VariableBaseMSMGpu:
         del keep
         return out.raw
 
+    def run_window_range(self, bases, scalars, w_begin: int, w_end: int, n=None) -> bytes:
+        """The windows [w_begin, w_end) of the MSM only: sum_w 2^(c w) S_w
+        (affine).  Ranges tiling [0, W) add up to run(); see
+        dist.window_split_msm."""
+        pb, ps, n, keep = self._args(bases, scalars, n)
+        out = ctypes.create_string_buffer(self.point_bytes)
+        lib().tachyon_mi355x_msm_gpu_window_range_affine(self.curve_id, self._ctx, pb, ps, n, w_begin, w_end, out)
+        del keep
+        return out.raw
+
     def run_jacobian(self, bases, scalars, n=None) -> bytes:
         """Through the reference entry point (*_affine_msm_gpu): returns the
         Jacobian the C-ABI allocates (copied, then freed)."""

@@ -71,6 +71,22 @@ def test_shard_range_covers():
                 pos = s + m if m else pos
 
 
+def test_window_range_tiles():
+    """dist.window_range: contiguous, ordered ranges tiling [0, W), sizes
+    differing by at most one (W = 16 at c = 16 splits 2 per rank at N = 8)."""
+    from tachyon_amd.dist import _windows_for, window_range
+    assert _windows_for("bn254_g1", 16) == 16 and _windows_for("bn254_g1", 20) == 13
+    assert _windows_for("bls12_381_g1", 16) == 16
+    for W in (1, 5, 13, 16, 26):
+        for world in (1, 2, 3, 4, 8, 16):
+            spans = [window_range(W, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == W
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [w1 - w0 for w0, w1 in spans]
+            assert max(sizes) - min(sizes) <= 1
+    assert [window_range(16, r, 8) for r in range(8)] == [(2 * r, 2 * r + 2) for r in range(8)]
+
+
 def _ntt_worker(rank, world, port, log_n, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)

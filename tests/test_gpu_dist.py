@@ -123,3 +123,34 @@ def test_sharded_ntt_cross_stream_world2(log_n):
     for rank, out, oidx, round_trip in got:
         assert round_trip, rank
         assert out == np.ascontiguousarray(want[oidx]).tobytes(), rank
+
+
+def _window_split_worker(rank, world, port, q, n, c):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from tachyon_amd import dist as D
+        from tachyon_amd.msm import VariableBaseMSMGpu
+        bases = O.gen_bases("bn254_g1", 5, n, 64).tobytes()
+        scalars = O.gen_scalars("bn254_fr", 5, n).tobytes()
+        m = VariableBaseMSMGpu("bn254_g1")
+        got = D.window_split_msm("bn254_g1", m, bases, scalars, n, c)
+        m.close()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,c", [(2, 16), (3, 12)])
+def test_window_split_msm_gloo(world, c):
+    """dist.window_split_msm: every rank holds all points and computes its
+    window range (tachyon_mi355x_msm_gpu_window_range_affine); the all-gathered
+    partials sum to the oracle's MSM on every rank."""
+    from oracle import oracle as O
+    n = 3000
+    bases = O.gen_bases("bn254_g1", 5, n, 64).tobytes()
+    scalars = O.gen_scalars("bn254_fr", 5, n).tobytes()
+    want, _ = O.msm("bn254_g1", bases, scalars)
+    for rank, got in _run(_window_split_worker, world, n, c):
+        assert got == want, rank

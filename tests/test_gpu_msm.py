@@ -216,3 +216,33 @@ def test_memory_divisions(monkeypatch):
     assert m.run(d_b.cpu().numpy(), d_s.cpu().numpy()) == whole
     assert m.last_divisions() >= 2
     m.close()
+
+
+@pytest.mark.parametrize("curve", ["bn254_g1", "bn254_g2", "bls12_381_g1"])
+def test_window_ranges_tile_the_msm(curve):
+    """run_window_range: the partials of window ranges that tile [0, W) add up
+    to the MSM (pippenger_base.h:59-77 split by windows); empty and
+    out-of-range ranges are the identity; one range covering everything is
+    the MSM itself."""
+    from tachyon_amd import dist as D
+    from tachyon_amd import msm as M
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    n = 2500
+    pb, sf = O.CURVE_INFO[curve]
+    bases = O.gen_bases(curve, 9, n, 64).tobytes()
+    scalars = O.gen_scalars(sf, 9, n).tobytes()
+    want, _ = O.msm(curve, bases, scalars)
+    m = VariableBaseMSMGpu(curve)
+    for c in (7, 16):
+        m.set_window_bits(c)
+        W = D._windows_for(curve, c)
+        assert m.run_window_range(bases, scalars, 0, W) == want
+        assert m.run_window_range(bases, scalars, 0, 10 ** 6) == want
+        assert m.run_window_range(bases, scalars, 3, 3) == bytes(pb)
+        assert m.run_window_range(bases, scalars, W, W + 4) == bytes(pb)
+        for parts in (2, 3, 8):
+            ranges = [D.window_range(W, r, parts) for r in range(parts)]
+            got = [m.run_window_range(bases, scalars, w0, w1) for w0, w1 in ranges]
+            assert M.affine_sum(curve, b"".join(got)) == want, (c, parts)
+        assert m.run(bases, scalars) == want  # the range is per call
+    m.close()

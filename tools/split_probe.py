@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Per-rank cost of the two multi-GPU MSM partitions, measured on one GPU.
+
+For N ranks over a 2^L MSM: the point split runs an n/N-point MSM (all
+windows, the size's default c); the window split runs all n points over
+W/N windows of c-bit windows (run_window_range).  The slower rank sets the
+N-GPU step time, so these per-rank times are the scaling model the bench's
+--msm-split auto rule follows.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def best_ms(fn, reps):
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2] * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log-n", type=int, default=26)
+    ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--c", type=int, default=16)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    from tachyon_amd import dist as D
+    from tachyon_amd import msm as M
+    n = 1 << args.log_n
+    d_b = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    M.gen_bases("bn254_g1", 1, n, 1024, d_b.data_ptr())
+    M.gen_scalars("bn254_fr", 1, n, d_s.data_ptr())
+    torch.cuda.synchronize()
+    m = M.VariableBaseMSMGpu("bn254_g1")
+    whole = best_ms(lambda: m.run(d_b, d_s, n), args.reps)
+    W = D._windows_for("bn254_g1", args.c)
+    for world in args.worlds:
+        shard = n // world
+        pts = best_ms(lambda: m.run(d_b, d_s, shard), args.reps)
+        m.set_window_bits(args.c)
+        w0, w1 = D.window_range(W, 0, world)
+        win = best_ms(lambda: m.run_window_range(d_b, d_s, w0, w1, n), args.reps)
+        m.set_profile(True)
+        m.run_window_range(d_b, d_s, w0, w1, n)
+        win_phases = {k: round(v, 3) for k, v in m.last_timings().items()}
+        m.set_window_bits(0)
+        m.run(d_b, d_s, shard)
+        pts_phases = {k: round(v, 3) for k, v in m.last_timings().items()}
+        m.set_profile(False)
+        print(json.dumps({"log_n": args.log_n, "world": world, "whole_ms": round(whole, 3),
+                          "point_split_rank_ms": round(pts, 3), "window_split_rank_ms": round(win, 3),
+                          "c": args.c, "windows_per_rank": w1 - w0,
+                          "eff_points": round(whole / (world * pts), 3),
+                          "eff_windows": round(whole / (world * win), 3),
+                          "window_phases": win_phases, "point_phases": pts_phases}), flush=True)
+    m.close()
+
+
+if __name__ == "__main__":
+    main()
