@@ -19,6 +19,7 @@
 #include <cstddef>
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "../common/hip_util.h"
@@ -97,12 +98,16 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, u
     ++p.levels;
   }
   // running-sum segment length: long segments amortise the (jL)*R fix-up, but
-  // small MSMs need >= ~64K segment threads to fill the chip (a 2^16 MSM with
-  // 64-bucket segments ran 208 threads of ~2000 serial mulmods each)
+  // small MSMs need >= ~48K segment threads to fill the chip (a 2^16 MSM with
+  // 64-bucket segments ran 208 threads of ~2000 serial mulmods each).
+  // TACHYON_MSM_SEG sweep (ms): 2^20 L = 8/16/32 2.83/2.97/3.29; 2^22 8/16/32
+  // 7.99/7.84/8.30; 2^24 16/32/64 26.3/26.2/26.3
   size_t nb = (size_t)p.active() * p.buckets;
   unsigned seg = 2;
-  while (seg < 64 && ((nb / (seg * 2)) >= 65536)) seg *= 2;
+  while (seg < 64 && ((nb / (seg * 2)) >= 49152)) seg *= 2;
   p.seg = std::min<unsigned>(p.buckets, seg);
+  if (const char* e = getenv("TACHYON_MSM_SEG"); e && atoi(e) > 0)  // A/B override
+    p.seg = std::clamp<unsigned>(atoi(e), 2, p.buckets);
   return p;
 }
 
