@@ -173,7 +173,14 @@ def lib():
                 "(the MI355X backend has no CPU fallback)")
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                # an A/B build from an older commit (TACHYON_MI355X_LIB) may
+                # predate an entry point; the in-tree library must have all
+                if os.environ.get("TACHYON_MI355X_LIB"):
+                    continue
+                raise
             f.restype = res
             f.argtypes = args
         _lib = L

@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0xFBF;
+constexpr int kMsmVariantMask = 0x3BF;
 
 struct MsmPlan {
   unsigned c = 0;        // window bits
@@ -150,9 +150,9 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-11; see run_windows and enqueue).  Every
-  // variant computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 11 are refused.
+  // A/B tuning knobs (bits 0-5, 7-9; see run_windows).  Every variant
+  // computes the same MSM; bit 6 (once a wrong-result gather-locality
+  // experiment) and anything above bit 9 are refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;

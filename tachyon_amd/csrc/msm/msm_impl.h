@@ -195,8 +195,8 @@ struct AccWaves<Bls381G2> {
   static constexpr int value = 2;
 };
 
-template <class Curve, int kDepth, int kWaves>
-__global__ __launch_bounds__(kBlock, kWaves) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
+template <class Curve>
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
                                                          const uint64_t* __restrict__ ents, uint32_t c,
                                                          uint64_t gbeg, uint64_t gend, uint64_t tbase,
                                                          uint32_t K, uint32_t idx_mask,
@@ -230,31 +230,35 @@ __global__ __launch_bounds__(kBlock, kWaves) void seg_acc_kernel(const Affine<ty
   // its first non-identity base (no madd), identity bases (0, 0) -- canonical
   // input, so a plain limb OR -- add nothing, and madd_nz reports the rare
   // cancellation P = -acc.  Signed digits negate y as p - y by limb selects.
+  // (one-word and BLS12-381 Fq fields; Fq2 keeps the identity-aware madd and
+  // no flag -- its register budget spills more with the extra live state)
+  constexpr bool kFlag = sizeof(F) <= 48;
   bool acc_zero = true;
-  // software pipeline kDepth deep: the entries of g+1 .. g+kDepth and the
-  // bases of g+1 .. g+kDepth-1 are in flight while the madd for g runs
-  uint64_t ew[kDepth + 1];
-  Affine<F> Pw[kDepth];
-#pragma unroll
-  for (int d = 0; d < kDepth; ++d) ew[d] = (g0 + d < g1) ? ents[g0 + d] : 0;
-#pragma unroll
-  for (int d = 0; d + 1 < kDepth; ++d) Pw[d] = hbases[entry_val(ew[d]) & idx_mask];
+  // two-deep software pipeline: the entry of g+2 and the base of g+1 are in
+  // flight while the madd for g runs.  (A 3-deep pipeline and >= 4 waves per
+  // SIMD at 128 VGPRs measured the same for BN254 G1 -- 72.4 / 72.2 vs 72.2
+  // ms at 2^26 -- the kernel is issue-bound; the array-rotated 3-deep form
+  // also cost the BLS12-381 G2 kernel 8 % in scratch traffic.)
+  uint64_t e0 = ents[g0];
+  uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
+  Affine<F> P = hbases[entry_val(e0) & idx_mask];
   for (uint64_t g = g0; g < g1; ++g) {
-    ew[kDepth] = (g + kDepth < g1) ? ents[g + kDepth] : 0;
-    Pw[kDepth - 1] = hbases[entry_val(ew[kDepth - 1]) & idx_mask];
-    const uint32_t k0 = entry_key(ew[0]), v0 = entry_val(ew[0]);
-    Affine<F> P = Pw[0];
+    const uint64_t e2 = (g + 2 < g1) ? ents[g + 2] : 0;
+    Affine<F> Pn = hbases[entry_val(e1) & idx_mask];
+    const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
       if (b != cur) {
         if (cur != kNoBucket) {  // close a run that is not the last one
-          if (acc_zero) acc = XYZZ<F>::zero();
+          if constexpr (kFlag)
+            if (acc_zero) acc = XYZZ<F>::zero();
           if (runs == 1 && cur == prev_b) { hpieces[2 * t] = acc; flags |= kHead; }
           else hsum[cur] = acc;
         }
         cur = b;
         ++runs;
-        acc_zero = true;
+        if constexpr (kFlag) acc_zero = true;
+        else acc = XYZZ<F>::zero();
       }
       if constexpr (sizeof(F) <= 48) {
         if (!P.is_zero_canonical()) {
@@ -267,19 +271,19 @@ __global__ __launch_bounds__(kBlock, kWaves) void seg_acc_kernel(const Affine<ty
           }
         }
       } else {
-        // Fq2 (G2): the generic identity-aware madd measured faster here
-        // (BN254 G2 2^20 accumulation 5.40 vs 5.73 ms with the flag path)
-        if (acc_zero) { acc = XYZZ<F>::zero(); acc_zero = false; }
+        // Fq2 (G2): the generic identity-aware madd and no flag (the flag
+        // path spilled 143 instead of 15 VGPRs at the 2-wave cap: BN254 G2
+        // 2^20 accumulation 6.4 vs 5.5 ms)
         if ((v0 & kSignBit) && !P.is_zero()) P.y = -P.y;
         acc = acc.madd(P);
       }
     }
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d) ew[d] = ew[d + 1];
-#pragma unroll
-    for (int d = 0; d + 1 < kDepth; ++d) Pw[d] = Pw[d + 1];
+    e0 = e1;
+    e1 = e2;
+    P = Pn;
   }
-  if (acc_zero) acc = XYZZ<F>::zero();
+  if constexpr (kFlag)
+    if (acc_zero) acc = XYZZ<F>::zero();
   if (cur != kNoBucket) {  // the last run
     const bool head = runs == 1 && cur == prev_b;
     const bool tail = cur == next_b;
@@ -646,18 +650,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
-    // gather pipeline depth and minimum waves per SIMD (A/B: set_variant
-    // bits 10-11 = 1: depth 3, 2: depth 2 at >= 4 waves, 3: depth 3 at >= 4)
-    constexpr int kW = AccWaves<Curve>::value;
-    constexpr int kW4 = kW > 4 ? kW : 4;
-    auto acc_kernel = seg_acc_kernel<Curve, 2, kW>;
-    switch ((variant_ >> 10) & 3) {
-      case 1: acc_kernel = seg_acc_kernel<Curve, 3, kW>; break;
-      case 2: acc_kernel = seg_acc_kernel<Curve, 2, kW4>; break;
-      case 3: acc_kernel = seg_acc_kernel<Curve, 3, kW4>; break;
-      default: break;
-    }
-    hipLaunchKernelGGL(acc_kernel, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c, (uint64_t)e0,
+    hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c, (uint64_t)e0,
                        (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces, tflags, tlast);
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(gev_acc1_[g], stream_));
