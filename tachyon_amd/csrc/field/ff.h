@@ -19,6 +19,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 #include "constants.h"
 #include "mont_asm.h"
@@ -55,6 +56,8 @@ struct Fp {
   using Config = Cfg;
   // [0, 2p) representation is sound when 4p < 2^(32N)
   static constexpr bool kLazyCapable = Cfg::kModulusBits <= 32 * N - 2;
+  // Fp2 over this field multiplies inline (else through one out-of-line call)
+  static constexpr bool kExtInline = N <= 8;
 #if defined(__HIP_DEVICE_COMPILE__)
   static constexpr bool kLazy = kLazyCapable;
 #else
@@ -418,7 +421,7 @@ struct Fp2 {
   TA_HD Fp2 operator-() const { return {-c0, -c1}; }
   TA_HD Fp2 dbl() const { return {c0.dbl(), c1.dbl()}; }
   TA_HD Fp2 operator*(const Fp2& o) const {
-    if constexpr (F::N <= 8) return mul_inline(o);
+    if constexpr (F::kExtInline) return mul_inline(o);
     else return mul_outline(o);
   }
   TA_HD_NOINLINE Fp2 mul_outline(const Fp2& o) const { return mul_inline(o); }
@@ -462,6 +465,63 @@ struct HotFp : F {
   TA_HD HotFp canonical() const { return F::canonical(); }
 };
 
+// 12-limb products as calls whose operands travel in registers.  An
+// out-of-line Fq2 product takes `this` and its operand by address (48 words
+// exceed the registers clang passes arguments in), so every call went
+// through scratch memory: the caller stores both operands, the callee loads
+// them back with flat loads, and its wide register footprint forces the
+// caller to spill the accumulator around it.  One Fq product takes 24 words
+// in v0..v23 and returns 12 in v0..v11, and its small footprint leaves the
+// caller's live point in registers.
+#define TA_LIMBS12(x) uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, \
+                      uint32_t x##6, uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11
+#define TA_UNPACK12(x) {x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11}
+#define TA_PASS12(f) f.v[0], f.v[1], f.v[2], f.v[3], f.v[4], f.v[5], f.v[6], f.v[7], f.v[8], f.v[9], f.v[10], f.v[11]
+namespace detail {
+template <class F>
+__device__ __noinline__ F mul_in_regs(TA_LIMBS12(a), TA_LIMBS12(b)) {
+  const F x{TA_UNPACK12(a)}, y{TA_UNPACK12(b)};
+  return x.mul_inline(y);
+}
+template <class F>
+__device__ __noinline__ F sqr_in_regs(TA_LIMBS12(a)) {
+  const F x{TA_UNPACK12(a)};
+  return x.mul_inline(x);
+}
+}  // namespace detail
+
+template <class F>
+struct CallFp : F {
+  static_assert(F::N == 12, "register-argument products: 12-limb fields");
+  static constexpr bool kExtInline = true;
+  CallFp() = default;
+  TA_HD CallFp(const F& f) : F(f) {}
+  TA_HD static CallFp zero() { return F::zero(); }
+  TA_HD static CallFp one() { return F::one(); }
+  TA_HD CallFp operator+(const CallFp& o) const { return F::operator+(o); }
+  TA_HD CallFp operator-(const CallFp& o) const { return F::operator-(o); }
+  TA_HD CallFp operator-() const { return F::operator-(); }
+  TA_HD CallFp sub_unreduced(const CallFp& o) const { return F::sub_unreduced(o); }
+  TA_HD CallFp dbl() const { return F::dbl(); }
+  TA_HD CallFp operator*(const CallFp& o) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return detail::mul_in_regs<F>(TA_PASS12((*this)), TA_PASS12(o));
+#else
+    return F::mul_inline(o);
+#endif
+  }
+  TA_HD CallFp sqr() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return detail::sqr_in_regs<F>(TA_PASS12((*this)));
+#else
+    return F::mul_inline(*this);
+#endif
+  }
+  TA_HD CallFp inverse() const { return F::inverse(); }
+  TA_HD CallFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
+  TA_HD CallFp canonical() const { return F::canonical(); }
+};
+
 template <class F>
 struct HotOf {
   using type = F;
@@ -470,9 +530,9 @@ template <class Cfg>
 struct HotOf<Fp<Cfg>> {
   using type = HotFp<Fp<Cfg>>;
 };
-template <class F>
-struct HotOf<Fp2<F>> {
-  using type = Fp2<HotFp<F>>;
+template <class Cfg>
+struct HotOf<Fp2<Fp<Cfg>>> {
+  using type = std::conditional_t<(Fp<Cfg>::N > 8), Fp2<CallFp<Fp<Cfg>>>, Fp2<HotFp<Fp<Cfg>>>>;
 };
 
 using Bn254Fq = Fp<consts::bn254_fq>;
