@@ -99,22 +99,66 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 // 32-byte scalars and one write.
 constexpr unsigned kRecodeSpt = 2;  // default scalars per thread of the fused recode
 
+// Places > 0 (key bits 8..15, 16..23): with `places` > 0 the kernel also
+// counts those digits per block, into later[((p - 1) * nblocks + block) * 256
+// + bin], so the onesweep passes over those places need no histogram pass of
+// their own over the W*n entries (digit_count_kernel + digit_scan_kernel turn
+// the counts into rocPRIM's global digit offsets).
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restrict__ scalars, uint32_t n, unsigned c,
                                                              unsigned W, unsigned w0, unsigned wr,
-                                                             uint32_t nblocks, uint32_t spt,
-                                                             uint32_t* __restrict__ hist) {
-  __shared__ uint32_t cnt[256];
-  cnt[threadIdx.x] = 0;
+                                                             uint32_t nblocks, uint32_t spt, uint32_t places,
+                                                             uint32_t* __restrict__ hist,
+                                                             uint32_t* __restrict__ later) {
+  __shared__ uint32_t cnt[3][256];
+  const uint32_t t = threadIdx.x;
+  cnt[0][t] = 0;
+  cnt[1][t] = 0;
+  cnt[2][t] = 0;
   __syncthreads();
   for (uint32_t k = 0; k < spt; ++k) {
-    const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + threadIdx.x;
+    const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + t;
     if (i < n)
-      recode_scalar(scalars[i], i, c, W, w0, wr,
-                    [&](unsigned, uint32_t key, uint32_t) { atomicAdd(&cnt[key & 255], 1u); });
+      recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned, uint32_t key, uint32_t) {
+        atomicAdd(&cnt[0][key & 255], 1u);
+        if (places > 0) atomicAdd(&cnt[1][(key >> 8) & 255], 1u);
+        if (places > 1) atomicAdd(&cnt[2][(key >> 16) & 255], 1u);
+      });
   }
   __syncthreads();
-  hist[(size_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+  hist[(size_t)t * nblocks + blockIdx.x] = cnt[0][t];
+  for (uint32_t p = 1; p <= places; ++p) later[((size_t)(p - 1) * nblocks + blockIdx.x) * 256 + t] = cnt[p][t];
+}
+
+// counts[q * 256 + bin] += the later-place counts of a chunk of recode blocks
+// (grid: chunks x places; one coalesced 1 KiB row per block)
+__global__ __launch_bounds__(kBlock) void digit_count_kernel(const uint32_t* __restrict__ later, uint32_t nblocks,
+                                                             uint32_t per_chunk, uint32_t* __restrict__ counts) {
+  const uint32_t q = blockIdx.y, t = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * per_chunk, b1 = min(nblocks, b0 + per_chunk);
+  const uint32_t* rows = later + (size_t)q * nblocks * 256;
+  uint32_t acc = 0;
+  for (uint32_t b = b0; b < b1; ++b) acc += rows[(size_t)b * 256 + t];
+  if (acc) atomicAdd(&counts[q * 256 + t], acc);
+}
+
+// exclusive prefix sums of each place's 256 digit counts (one workgroup per
+// place): rocPRIM's global digit offsets, place q at [q * 256, (q + 1) * 256)
+__global__ __launch_bounds__(kBlock) void digit_scan_kernel(const uint32_t* __restrict__ counts,
+                                                            uint32_t* __restrict__ offsets) {
+  const uint32_t q = blockIdx.x, t = threadIdx.x;
+  const uint32_t mine = counts[q * 256 + t];
+  uint32_t v = mine;  // 4 waves x 64 lanes
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(v, d, 64);
+    if ((t & 63) >= (uint32_t)d) v += u;
+  }
+  __shared__ uint32_t wave_tot[kBlock / 64];
+  if ((t & 63) == 63) wave_tot[t >> 6] = v;
+  __syncthreads();
+  uint32_t add = 0;
+  for (uint32_t w = 0; w < (t >> 6); ++w) add += wave_tot[w];
+  offsets[q * 256 + t] = v - mine + add;
 }
 
 template <class Fr>
@@ -511,6 +555,30 @@ using OnesweepCfg = rocprim::radix_sort_config<
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<Threads, Items>, rocprim::kernel_config<Threads, Items>,
                                         8, rocprim::block_radix_rank_algorithm::match>>;
 
+// One rocPRIM onesweep pass (keys only, 1024 x 8 tiles, 8-bit digits) over
+// entry bits [bit, end_bit) from `in` to `out`, with the global digit offsets
+// given: radix_sort_keys would first read all W*n entries once more for its
+// digit histograms (2.4 ms at 2^26); the fused recode counts those digits as
+// it computes them (recode_hist_kernel).  rocPRIM's own iteration entry point
+// (lookback reset, ordered block ids, batching) does the rest.
+namespace {
+using MsmOnesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>,
+                                                        rocprim::kernel_config<1024, 8>, 8,
+                                                        rocprim::block_radix_rank_algorithm::match>;
+using MsmBlockId = rocprim::detail::block_id_wrapper<unsigned int, true>;
+constexpr uint32_t kOnesweepTile = 1024 * 8;
+
+hipError_t onesweep_pass(const uint64_t* in, uint64_t* out, uint32_t size, unsigned bit, unsigned end_bit,
+                         uint32_t* digit_offsets, uint32_t* offsets_tmp, void* lookback, void* block_id,
+                         hipStream_t s) {
+  rocprim::empty_type* none = nullptr;
+  return rocprim::detail::radix_sort_onesweep_iteration<MsmOnesweep, false>(
+      in, static_cast<uint64_t*>(nullptr), out, none, none, none, size, digit_offsets, offsets_tmp,
+      static_cast<rocprim::detail::onesweep_lookback_state*>(lookback), true, true, rocprim::identity_decomposer{},
+      bit, end_bit, MsmBlockId::create(block_id), s, false);
+}
+}  // namespace
+
 template <class Curve>
 hipError_t MsmGpu<Curve>::sort_entries(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, size_t count,
                                        unsigned begin_bit, unsigned end_bit, hipStream_t s) {
@@ -584,22 +652,41 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   const size_t scatter_lds = (size_t)spt * kBlock * W * sizeof(uint64_t);
   const bool fused = fuse_recode_ && G == W && scatter_lds <= 128 * 1024;
   const unsigned sort_begin = fused ? std::min(8u, key_bits) : 0u;
+  // onesweep passes fed with digit counts from the recode (places = the
+  // 8-bit digits after the fused low byte); rocPRIM's radix_sort_keys
+  // otherwise (set_variant bit 10, or other tile shapes, or > 2 places)
+  const unsigned places = (key_bits - sort_begin + 7) / 8;
+  const bool own_sort = fused && sort_cfg_ == 0 && !rocprim_hist_ && places <= 2 && entries < (size_t(1) << 32);
+  uint32_t* digit_off = nullptr;
 
   if (profile_) TA_HIP(hipEventRecord(ev_[1], stream_));
   if (fused) {
     const uint32_t nblocks = (uint32_t)((n + spt * kBlock - 1) / (spt * kBlock));
     const size_t hn = (size_t)256 * nblocks;
-    uint32_t* hist = static_cast<uint32_t*>(hist_.ensure(2 * hn * 4));
+    const unsigned later_places = own_sort ? places : 0;
+    uint32_t* hist = static_cast<uint32_t*>(hist_.ensure((2 + later_places) * hn * 4 + 5 * 256 * 4));
     uint32_t* hoff = hist + hn;
+    uint32_t* later = hist + 2 * hn;
+    uint32_t* digit_cnt = later + later_places * hn;  // 2 x 256 counts, 2 x 256 offsets, 256 spare
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       Wt, wr0, W, nblocks, spt, hist);
+                       Wt, wr0, W, nblocks, spt, later_places, hist, later);
     TA_HIP(hipGetLastError());
+    if (later_places > 0) {
+      digit_off = digit_cnt + 2 * 256;
+      TA_HIP(hipMemsetAsync(digit_cnt, 0, 2 * 256 * 4, stream_));
+      const uint32_t per_chunk = 128, chunks = (nblocks + per_chunk - 1) / per_chunk;
+      hipLaunchKernelGGL(digit_count_kernel, dim3(chunks, later_places), dim3(kBlock), 0, stream_, later, nblocks,
+                         per_chunk, digit_cnt);
+      hipLaunchKernelGGL(digit_scan_kernel, dim3(later_places), dim3(kBlock), 0, stream_, digit_cnt, digit_off);
+      TA_HIP(hipGetLastError());
+    }
     size_t hscan_bytes = 0;
     TA_HIP(rocprim::exclusive_scan(nullptr, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
     void* hscan_tmp = hscan_tmp_.ensure(hscan_bytes);
     TA_HIP(rocprim::exclusive_scan(hscan_tmp, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
-    // the scattered entries are fully sorted when the key has <= 8 bits
-    uint64_t* dst = sort_begin < key_bits ? ents : ents2;
+    // the scattered entries are fully sorted when the key has <= 8 bits; the
+    // own onesweep passes ping-pong from the scatter's output and end in ents2
+    uint64_t* dst = own_sort ? (places % 2 == 0 ? ents2 : ents) : (sort_begin < key_bits ? ents : ents2);
     if (scatter_lds > 64 * 1024 && !scatter_lds_set_) {
       TA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&recode_scatter_kernel<Fr>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
@@ -621,16 +708,35 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // ---- per group: radix sort of its (window, bucket, point) entries, then accumulation ----
   const size_t max_group_entries = (size_t)G * n;
   size_t sort_bytes = 0;
-  TA_HIP(sort_entries(nullptr, sort_bytes, ents, ents2, max_group_entries, sort_begin, key_bits, sort_stream));
-  void* sort_tmp = sort_tmp_.ensure(sort_bytes);
+  void* sort_tmp = nullptr;
+  uint8_t* os_tmp = nullptr;  // own passes: lookback states, block id, spare offsets
+  if (own_sort) {
+    const size_t lookback_bytes = (size_t)256 * ((entries + kOnesweepTile - 1) / kOnesweepTile) * 4;
+    os_tmp = static_cast<uint8_t*>(sort_tmp_.ensure(lookback_bytes + 1024 + 256 * 4));
+  } else {
+    TA_HIP(sort_entries(nullptr, sort_bytes, ents, ents2, max_group_entries, sort_begin, key_bits, sort_stream));
+    sort_tmp = sort_tmp_.ensure(sort_bytes);
+  }
   size_t tbase = 0;
   acc_launches_ = ngroups;
   for (unsigned g = 0; g < ngroups; ++g) {
     const unsigned w0 = g * G, w1 = std::min(W, w0 + G);
     const size_t e0 = (size_t)w0 * n, ecount = (size_t)(w1 - w0) * n;
     size_t bytes = sort_bytes;
-    if (sort_begin < key_bits)
+    if (own_sort) {
+      const size_t lookback_bytes = (size_t)256 * ((entries + kOnesweepTile - 1) / kOnesweepTile) * 4;
+      const uint64_t* src = places % 2 == 0 ? ents2 : ents;
+      uint64_t* out = places % 2 == 0 ? ents : ents2;
+      for (unsigned q = 0; q < places; ++q) {
+        TA_HIP(onesweep_pass(src, out, (uint32_t)entries, 32 + sort_begin + 8 * q, 32 + key_bits, digit_off + q * 256,
+                             reinterpret_cast<uint32_t*>(os_tmp + lookback_bytes + 1024), os_tmp,
+                             os_tmp + lookback_bytes, sort_stream));
+        src = out;
+        out = out == ents ? ents2 : ents;
+      }
+    } else if (sort_begin < key_bits) {
       TA_HIP(sort_entries(sort_tmp, bytes, ents + e0, ents2 + e0, ecount, sort_begin, key_bits, sort_stream));
+    }
     if (profile_ && g + 1 == ngroups) TA_HIP(hipEventRecord(ev_[3], sort_stream));  // last sort done
     if (sort_stream != stream_) {
       TA_HIP(hipEventRecord(gev_sorted_[g], sort_stream));
@@ -759,6 +865,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   static constexpr uint32_t kSpt[] = {kRecodeSpt, 1, 4, 3};
   recode_spt_ = kSpt[(variant_ >> 8) & 3];  // bits 8-9: scalars per thread of the fused recode
   sort_cfg_ = (variant_ >> 4) & 3;  // bits 4-5: onesweep tile shape
+  rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;
