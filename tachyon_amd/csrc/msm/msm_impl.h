@@ -562,20 +562,42 @@ using OnesweepCfg = rocprim::radix_sort_config<
 // it computes them (recode_hist_kernel).  rocPRIM's own iteration entry point
 // (lookback reset, ordered block ids, batching) does the rest.
 namespace {
-using MsmOnesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>,
-                                                        rocprim::kernel_config<1024, 8>, 8,
-                                                        rocprim::block_radix_rank_algorithm::match>;
+template <unsigned Threads, unsigned Items, rocprim::block_radix_rank_algorithm Rank>
+using MsmOnesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<Threads, Items>,
+                                                        rocprim::kernel_config<Threads, Items>, 8, Rank>;
 using MsmBlockId = rocprim::detail::block_id_wrapper<unsigned int, true>;
-constexpr uint32_t kOnesweepTile = 1024 * 8;
+constexpr uint32_t kOnesweepMinTile = 256 * 16;  // smallest tile below (sizes the lookback states)
 
-hipError_t onesweep_pass(const uint64_t* in, uint64_t* out, uint32_t size, unsigned bit, unsigned end_bit,
-                         uint32_t* digit_offsets, uint32_t* offsets_tmp, void* lookback, void* block_id,
-                         hipStream_t s) {
+template <class Cfg>
+hipError_t onesweep_pass_cfg(const uint64_t* in, uint64_t* out, uint32_t size, unsigned bit, unsigned end_bit,
+                             uint32_t* digit_offsets, uint32_t* offsets_tmp, void* lookback, void* block_id,
+                             hipStream_t s) {
   rocprim::empty_type* none = nullptr;
-  return rocprim::detail::radix_sort_onesweep_iteration<MsmOnesweep, false>(
+  return rocprim::detail::radix_sort_onesweep_iteration<Cfg, false>(
       in, static_cast<uint64_t*>(nullptr), out, none, none, none, size, digit_offsets, offsets_tmp,
       static_cast<rocprim::detail::onesweep_lookback_state*>(lookback), true, true, rocprim::identity_decomposer{},
       bit, end_bit, MsmBlockId::create(block_id), s, false);
+}
+
+// tile shapes (set_variant bits 4-5, A/B): 0 = 1024 x 8 warp-match ranking
+hipError_t onesweep_pass(unsigned cfg, const uint64_t* in, uint64_t* out, uint32_t size, unsigned bit,
+                         unsigned end_bit, uint32_t* digit_offsets, uint32_t* offsets_tmp, void* lookback,
+                         void* block_id, hipStream_t s) {
+  using R = rocprim::block_radix_rank_algorithm;
+  switch (cfg) {
+    case 1:
+      return onesweep_pass_cfg<MsmOnesweep<512, 8, R::match>>(in, out, size, bit, end_bit, digit_offsets,
+                                                                offsets_tmp, lookback, block_id, s);
+    case 2:
+      return onesweep_pass_cfg<MsmOnesweep<256, 16, R::match>>(in, out, size, bit, end_bit, digit_offsets,
+                                                                 offsets_tmp, lookback, block_id, s);
+    case 3:
+      return onesweep_pass_cfg<MsmOnesweep<1024, 12, R::match>>(in, out, size, bit, end_bit, digit_offsets,
+                                                                  offsets_tmp, lookback, block_id, s);
+    default:
+      return onesweep_pass_cfg<MsmOnesweep<1024, 8, R::match>>(in, out, size, bit, end_bit, digit_offsets,
+                                                                 offsets_tmp, lookback, block_id, s);
+  }
 }
 }  // namespace
 
@@ -656,7 +678,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // 8-bit digits after the fused low byte); rocPRIM's radix_sort_keys
   // otherwise (set_variant bit 10, or other tile shapes, or > 2 places)
   const unsigned places = (key_bits - sort_begin + 7) / 8;
-  const bool own_sort = fused && sort_cfg_ == 0 && !rocprim_hist_ && places <= 2 && entries < (size_t(1) << 32);
+  const bool own_sort = fused && !rocprim_hist_ && places <= 2 && entries < (size_t(1) << 32);
   uint32_t* digit_off = nullptr;
 
   if (profile_) TA_HIP(hipEventRecord(ev_[1], stream_));
@@ -711,7 +733,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   void* sort_tmp = nullptr;
   uint8_t* os_tmp = nullptr;  // own passes: lookback states, block id, spare offsets
   if (own_sort) {
-    const size_t lookback_bytes = (size_t)256 * ((entries + kOnesweepTile - 1) / kOnesweepTile) * 4;
+    const size_t lookback_bytes = (size_t)256 * ((entries + kOnesweepMinTile - 1) / kOnesweepMinTile) * 4;
     os_tmp = static_cast<uint8_t*>(sort_tmp_.ensure(lookback_bytes + 1024 + 256 * 4));
   } else {
     TA_HIP(sort_entries(nullptr, sort_bytes, ents, ents2, max_group_entries, sort_begin, key_bits, sort_stream));
@@ -724,11 +746,11 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     const size_t e0 = (size_t)w0 * n, ecount = (size_t)(w1 - w0) * n;
     size_t bytes = sort_bytes;
     if (own_sort) {
-      const size_t lookback_bytes = (size_t)256 * ((entries + kOnesweepTile - 1) / kOnesweepTile) * 4;
+      const size_t lookback_bytes = (size_t)256 * ((entries + kOnesweepMinTile - 1) / kOnesweepMinTile) * 4;
       const uint64_t* src = places % 2 == 0 ? ents2 : ents;
       uint64_t* out = places % 2 == 0 ? ents : ents2;
       for (unsigned q = 0; q < places; ++q) {
-        TA_HIP(onesweep_pass(src, out, (uint32_t)entries, 32 + sort_begin + 8 * q, 32 + key_bits, digit_off + q * 256,
+        TA_HIP(onesweep_pass(sort_cfg_, src, out, (uint32_t)entries, 32 + sort_begin + 8 * q, 32 + key_bits, digit_off + q * 256,
                              reinterpret_cast<uint32_t*>(os_tmp + lookback_bytes + 1024), os_tmp,
                              os_tmp + lookback_bytes, sort_stream));
         src = out;
