@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0x7BF;
+constexpr int kMsmVariantMask = 0xFBF;
 
 struct MsmPlan {
   unsigned c = 0;        // window bits
@@ -150,9 +150,9 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-10; see run_windows).  Every variant
+  // A/B tuning knobs (bits 0-5, 7-11; see run_windows).  Every variant
   // computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 10 are refused.
+  // experiment) and anything above bit 11 are refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;
@@ -189,6 +189,7 @@ class MsmGpu {
   unsigned acc_launches_ = 0;
   unsigned sort_cfg_ = 0;  // onesweep tile shape (set_variant bits 4-5)
   bool rocprim_hist_ = false;  // rocPRIM's digit histogram pass instead of the recode's counts (bit 10)
+  bool wide_stage_ = false;    // 8-byte entries in the recode scatter's LDS staging (bit 11)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode

@@ -161,7 +161,10 @@ __global__ __launch_bounds__(kBlock) void digit_scan_kernel(const uint32_t* __re
   offsets[q * 256 + t] = v - mine + add;
 }
 
-template <class Fr>
+// kNarrow: keys of <= 24 bits are staged as 7 bytes (val, key >> 8, bin),
+// 47 KiB instead of 53 KiB per block at 13 windows -- three workgroups per
+// CU instead of two.
+template <class Fr, bool kNarrow>
 __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __restrict__ scalars, uint32_t n,
                                                                 unsigned c, unsigned W, unsigned w0, unsigned wr,
                                                                 uint32_t nblocks, uint32_t spt,
@@ -171,7 +174,10 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
   // the block's entries are binned in LDS first, then written out bin run by
   // bin run, so consecutive lanes store to consecutive addresses
   extern __shared__ uint64_t lds_u64[];
-  uint64_t* lents = lds_u64;                      // spt * kBlock * wr
+  uint64_t* lents = lds_u64;                      // spt * kBlock * wr (wide)
+  uint32_t* lvals = reinterpret_cast<uint32_t*>(lds_u64);  // narrow: vals, then the 16-bit key tops
+  uint16_t* lkeys = reinterpret_cast<uint16_t*>(lvals + (size_t)spt * kBlock * wr);
+  uint8_t* lbins = reinterpret_cast<uint8_t*>(lkeys + (size_t)spt * kBlock * wr);
   __shared__ uint32_t base[256], loff[256], cur[256];
   const uint32_t t = threadIdx.x;
   base[t] = off[(size_t)t * nblocks + blockIdx.x];
@@ -196,15 +202,28 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
       recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned, uint32_t key, uint32_t val) {
         const uint32_t bin = key & 255;
         const uint32_t p = loff[bin] + atomicAdd(&cur[bin], 1u);
-        lents[p] = make_entry(key, val);
+        if constexpr (kNarrow) {
+          lvals[p] = val;
+          lkeys[p] = (uint16_t)(key >> 8);
+          lbins[p] = (uint8_t)bin;
+        } else {
+          lents[p] = make_entry(key, val);
+        }
       });
   }
   __syncthreads();
   const uint32_t total = loff[255] + cur[255];
-  for (uint32_t p = t; p < total; p += kBlock) {
-    const uint64_t e = lents[p];
-    const uint32_t bin = entry_key(e) & 255;
-    ents[base[bin] + (p - loff[bin])] = e;
+  if constexpr (kNarrow) {
+    for (uint32_t p = t; p < total; p += kBlock) {
+      const uint32_t bin = lbins[p];
+      ents[base[bin] + (p - loff[bin])] = make_entry(((uint32_t)lkeys[p] << 8) | bin, lvals[p]);
+    }
+  } else {
+    for (uint32_t p = t; p < total; p += kBlock) {
+      const uint64_t e = lents[p];
+      const uint32_t bin = entry_key(e) & 255;
+      ents[base[bin] + (p - loff[bin])] = e;
+    }
   }
 }
 
@@ -671,7 +690,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // recode fused with the first (low byte) radix pass; one sort group only
   // (the scatter stages a block's spt x 256 x W entries in LDS, <= 128 KiB)
   const uint32_t spt = recode_spt_;
-  const size_t scatter_lds = (size_t)spt * kBlock * W * sizeof(uint64_t);
+  const bool narrow = key_bits <= 24 && !wide_stage_;  // 7-byte LDS staging in the scatter
+  const size_t scatter_lds = (size_t)spt * kBlock * W * (narrow ? 7 : sizeof(uint64_t));
   const bool fused = fuse_recode_ && G == W && scatter_lds <= 128 * 1024;
   const unsigned sort_begin = fused ? std::min(8u, key_bits) : 0u;
   // onesweep passes fed with digit counts from the recode (places = the
@@ -709,13 +729,14 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     // the scattered entries are fully sorted when the key has <= 8 bits; the
     // own onesweep passes ping-pong from the scatter's output and end in ents2
     uint64_t* dst = own_sort ? (places % 2 == 0 ? ents2 : ents) : (sort_begin < key_bits ? ents : ents2);
-    if (scatter_lds > 64 * 1024 && !scatter_lds_set_) {
-      TA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&recode_scatter_kernel<Fr>),
+    if (!narrow && scatter_lds > 64 * 1024 && !scatter_lds_set_) {
+      TA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&recode_scatter_kernel<Fr, false>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
       scatter_lds_set_ = true;
     }
-    hipLaunchKernelGGL(recode_scatter_kernel<Fr>, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars,
-                       (uint32_t)n, c, Wt, wr0, W, nblocks, spt, hist, hoff, dst);
+    auto* scatter = narrow ? &recode_scatter_kernel<Fr, true> : &recode_scatter_kernel<Fr, false>;
+    hipLaunchKernelGGL(scatter, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars, (uint32_t)n, c, Wt, wr0,
+                       W, nblocks, spt, hist, hoff, dst);
   } else {
     hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
                        Wt, wr0, W, ents);
@@ -888,6 +909,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   recode_spt_ = kSpt[(variant_ >> 8) & 3];  // bits 8-9: scalars per thread of the fused recode
   sort_cfg_ = (variant_ >> 4) & 3;  // bits 4-5: onesweep tile shape
   rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
+  wide_stage_ = (variant_ & 2048) != 0;    // bit 11: 8-byte LDS staging in the recode scatter (A/B)
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;

@@ -246,3 +246,26 @@ def test_window_ranges_tile_the_msm(curve):
             assert M.affine_sum(curve, b"".join(got)) == want, (c, parts)
         assert m.run(bases, scalars) == want  # the range is per call
     m.close()
+
+
+@pytest.mark.parametrize("curve", ["bn254_g1", "bls12_381_g2"])
+def test_msm_schedule_variants_agree(curve):
+    """Every accepted set_variant schedule computes the same point: the separate
+    recode + full sort (bit 7), rocPRIM's own digit-histogram pass instead of the
+    recode's counts (bit 10), 8-byte LDS staging in the recode scatter (bit 11),
+    the onesweep tile shapes (bits 4-5) and one window per sort group (bits 2-3);
+    the wrong-result bit 6 and bits above 11 are refused."""
+    n = 1 << 13
+    bases = O.gen_bases(curve, 21, n, 16).tobytes()
+    scalars = O.gen_scalars(O.CURVE_INFO[curve][1], 21, n).tobytes()
+    expect, _ = O.msm(curve, bases, scalars)
+    m = ctx(curve)
+    try:
+        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256):
+            m.set_variant(v)
+            assert m.run(bases, scalars) == expect, hex(v)
+        for bad in (64, 4096):
+            with pytest.raises(ValueError):
+                m.set_variant(bad)
+    finally:
+        m.set_variant(0)
