@@ -298,16 +298,24 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
   constexpr bool kFlag = sizeof(F) <= 48;
   bool acc_zero = true;
   // two-deep software pipeline: the entry of g+2 and the base of g+1 are in
-  // flight while the madd for g runs.  (A 3-deep pipeline and >= 4 waves per
+  // flight while the madd for g runs (one-word and BLS12-381 Fq fields).  (A 3-deep pipeline and >= 4 waves per
   // SIMD at 128 VGPRs measured the same for BN254 G1 -- 72.4 / 72.2 vs 72.2
   // ms at 2^26 -- the kernel is issue-bound; the array-rotated 3-deep form
   // also cost the BLS12-381 G2 kernel 8 % in scratch traffic.)
+  // Fq2 (G2) kernels load each base at its own iteration: the prefetched
+  // next point (64 / 96 words) costs them spills at the 2-wave register cap
+  // (BLS12-381 G2 2^21 accumulation 25.7 -> 23.6 ms, BN254 G2 2^20 5.55 ->
+  // 5.42 without it; the second wave covers the gather latency)
+  constexpr bool kPrefetchBase = sizeof(F) <= 48;
   uint64_t e0 = ents[g0];
   uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
-  Affine<F> P = hbases[entry_val(e0) & idx_mask];
+  Affine<F> P;
+  if constexpr (kPrefetchBase) P = hbases[entry_val(e0) & idx_mask];
   for (uint64_t g = g0; g < g1; ++g) {
     const uint64_t e2 = (g + 2 < g1) ? ents[g + 2] : 0;
-    Affine<F> Pn = hbases[entry_val(e1) & idx_mask];
+    Affine<F> Pn;
+    if constexpr (kPrefetchBase) Pn = hbases[entry_val(e1) & idx_mask];
+    else P = hbases[entry_val(e0) & idx_mask];
     const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
@@ -343,7 +351,7 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
     }
     e0 = e1;
     e1 = e2;
-    P = Pn;
+    if constexpr (kPrefetchBase) P = Pn;
   }
   if constexpr (kFlag)
     if (acc_zero) acc = XYZZ<F>::zero();
