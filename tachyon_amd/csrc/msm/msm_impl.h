@@ -257,6 +257,19 @@ template <>
 struct AccWaves<Bls381G2> {
   static constexpr int value = 2;
 };
+// The identity accumulator as a flag (see seg_acc_kernel): every curve but
+// BN254 G2, whose inline Fq2 products leave no registers for the extra live
+// state (2^20 accumulation 5.30 -> 5.59 ms with it; BLS12-381 G2, whose Fq
+// products are calls, 23.4 -> 21.3 ms at 2^21).  The 2-wave cap above
+// measured best for both G2 kernels against 1 and 3 waves.
+template <class Curve>
+struct AccFlag {
+  static constexpr bool value = true;
+};
+template <>
+struct AccFlag<Bn254G2> {
+  static constexpr bool value = false;
+};
 
 template <class Curve>
 __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel(const Affine<typename Curve::F>* __restrict__ bases,
@@ -293,9 +306,8 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
   // its first non-identity base (no madd), identity bases (0, 0) -- canonical
   // input, so a plain limb OR -- add nothing, and madd_nz reports the rare
   // cancellation P = -acc.  Signed digits negate y as p - y by limb selects.
-  // (one-word and BLS12-381 Fq fields; Fq2 keeps the identity-aware madd and
-  // no flag -- its register budget spills more with the extra live state)
-  constexpr bool kFlag = sizeof(F) <= 48;
+  // (AccFlag: all curves but BN254 G2)
+  constexpr bool kFlag = AccFlag<Curve>::value;
   bool acc_zero = true;
   // two-deep software pipeline: the entry of g+2 and the base of g+1 are in
   // flight while the madd for g runs (one-word and BLS12-381 Fq fields).  (A 3-deep pipeline and >= 4 waves per
@@ -331,7 +343,7 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
         if constexpr (kFlag) acc_zero = true;
         else acc = XYZZ<F>::zero();
       }
-      if constexpr (sizeof(F) <= 48) {
+      if constexpr (kFlag) {
         if (!P.is_zero_canonical()) {
           P.y = P.y.cond_neg_canonical(v0 & kSignBit);
           if (acc_zero) {
@@ -342,9 +354,7 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
           }
         }
       } else {
-        // Fq2 (G2): the generic identity-aware madd and no flag (the flag
-        // path spilled 143 instead of 15 VGPRs at the 2-wave cap: BN254 G2
-        // 2^20 accumulation 6.4 vs 5.5 ms)
+        // BN254 G2: the generic identity-aware madd and no flag (AccFlag)
         if ((v0 & kSignBit) && !P.is_zero()) P.y = -P.y;
         acc = acc.madd(P);
       }
