@@ -112,28 +112,29 @@ def _ntt_worker(rank, world, port, log_n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("log_n", [4, 7])
-def test_sharded_ntt_world2(log_n):
+@pytest.mark.parametrize("world,log_n", [(2, 4), (2, 7), (4, 8), (8, 8)])
+def test_sharded_ntt_gloo(world, log_n):
     """Four-step distributed NTT orchestration (layouts + one all-to-all) over
-    gloo; per-rank stages from the CPU mirror plan, result = the full oracle FFT."""
+    gloo; per-rank stages from the CPU mirror plan, result = the full oracle FFT
+    (world 8 = the driver's 8-GPU layout)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ntt_worker, args=(r, 2, port, log_n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ntt_worker, args=(r, world, port, log_n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=240) for _ in range(2))
+    res = sorted(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res == [(0, True, True), (1, True, True)]
+    assert res == [(r, True, True) for r in range(world)]
 
 
 def test_four_step_layouts_partition():
     import numpy as np
     from tachyon_amd.ntt import FourStepNtt
     for log_n in (2, 5, 12):
-        for world in (1, 2, 4):
+        for world in (1, 2, 4, 8):
             if (1 << (log_n // 2)) < world:
                 continue
             for f in (FourStepNtt.input_indices, FourStepNtt.output_indices):
