@@ -1,4 +1,4 @@
-"""Multi-rank MSM sharding on CPU (gloo, world_size 2): the shard split, the
+"""Multi-rank MSM sharding on CPU (gloo, world_size 2..8): the shard split, the
 all-gather of per-rank partial points and the product's host-side group sum
 (tachyon_mi355x_affine_sum, no GPU needed) reproduce the single-process MSM.
 The per-rank local MSM is the oracle here (the CPU box has no GPU); on the GPU
@@ -43,12 +43,13 @@ def _worker(rank, world, port, curve, n, q):
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libtachyon_mi355x.so not built")
-@pytest.mark.parametrize("curve,n", [("bn254_g1", 301), ("bls12_381_g1", 64)])
-def test_sharded_msm_world2(curve, n):
+@pytest.mark.parametrize("curve,n,world", [("bn254_g1", 301, 2), ("bls12_381_g1", 64, 2), ("bn254_g1", 203, 8),
+                                           ("bn254_g2", 67, 4)])
+def test_sharded_msm_gloo(curve, n, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, curve, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, curve, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     got, expect = q.get(timeout=240)
