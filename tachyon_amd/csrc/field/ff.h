@@ -35,6 +35,11 @@
 #ifndef TA_FIELD_ASM
 #define TA_FIELD_ASM 1
 #endif
+// device squares by the dedicated FIPS square (mont_asm.h mont_sqr_fips_N);
+// 0 = a general product of the value with itself
+#ifndef TA_FIELD_SQR
+#define TA_FIELD_SQR 1
+#endif
 
 namespace tachyon_amd {
 
@@ -365,7 +370,27 @@ struct Fp {
     for (int i = 0; i < N; ++i) r.v[i] = t[i];
     return r;
   }
-  TA_HD Fp sqr() const { return (*this) * (*this); }
+  // Squares count each cross product once (mont_asm.h gen_sqr: 100 instead
+  // of 128 v_mad_u64_u32 for 8 limbs); the device square needs a value below
+  // 2^(32N-1), which every representation here keeps (lazy < 2p of a 254- or
+  // 381-bit field, canonical < p of BLS12-381 Fr)
+  static_assert(Cfg::kModulusBits + (kLazyCapable ? 1 : 0) <= 32 * N - 1, "mont_sqr_fips: top bit must be clear");
+  TA_HD Fp sqr() const {
+    if constexpr (N <= 8) return sqr_inline();
+    else return sqr_outline();
+  }
+  TA_HD_NOINLINE Fp sqr_outline() const { return sqr_inline(); }
+  TA_HD Fp sqr_inline() const {
+#if defined(__HIP_DEVICE_COMPILE__) && TA_FIELD_SQR
+    Fp r;
+    if constexpr (N == 8) detail::mont_sqr_fips_8<Cfg>(r.v, v);
+    else detail::mont_sqr_fips_12<Cfg>(r.v, v);
+    if constexpr (!kLazy) reduce_once(r.v);
+    return r;
+#else
+    return mul_inline(*this);
+#endif
+  }
 
   // Montgomery -> canonical integer (ToBigInt, prime_field_fallback.h:166-169)
   TA_HD Fp from_mont() const {
@@ -458,7 +483,7 @@ struct HotFp : F {
   TA_HD HotFp sub_unreduced(const HotFp& o) const { return F::sub_unreduced(o); }
   TA_HD HotFp operator*(const HotFp& o) const { return F::mul_inline(o); }
   TA_HD HotFp dbl() const { return F::dbl(); }
-  TA_HD HotFp sqr() const { return F::mul_inline(*this); }
+  TA_HD HotFp sqr() const { return F::sqr_inline(); }
   TA_HD HotFp inverse() const { return F::inverse(); }
   TA_HD HotFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
   TA_HD HotFp mul_shoup(const HotFp& w, const HotFp& wq) const { return F::mul_shoup(w, wq); }
@@ -486,7 +511,7 @@ __device__ __noinline__ F mul_in_regs(TA_LIMBS12(a), TA_LIMBS12(b)) {
 template <class F>
 __device__ __noinline__ F sqr_in_regs(TA_LIMBS12(a)) {
   const F x{TA_UNPACK12(a)};
-  return x.mul_inline(x);
+  return x.sqr_inline();
 }
 }  // namespace detail
 
@@ -514,7 +539,7 @@ struct CallFp : F {
 #if defined(__HIP_DEVICE_COMPILE__)
     return detail::sqr_in_regs<F>(TA_PASS12((*this)));
 #else
-    return F::mul_inline(*this);
+    return F::sqr_inline();
 #endif
   }
   TA_HD CallFp inverse() const { return F::inverse(); }

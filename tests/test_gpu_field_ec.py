@@ -128,3 +128,36 @@ def test_twiddle_product_shoup_bn254_fr():
     got = gpu_field_op("bn254_fr", "mul_const", b"".join(map(enc, xs)), b"".join(map(enc, ws)))
     for k, (x, w) in enumerate(zip(xs, ws)):
         assert int.from_bytes(got[32 * k:32 * k + 32], "little") == x * w % p, (k, hex(x), hex(w))
+
+
+@pytest.mark.parametrize("field", ["bn254_fq", "bn254_fr", "bls12_381_fq", "bls12_381_fr"])
+def test_square_every_representative(field):
+    """Field op 3 = Fp::sqr, the dedicated FIPS square (each cross product
+    counted once, through the doubled limbs of x).  The device keeps the
+    254- and 381-bit fields in [0, 2p), so the square must be right for every
+    representative there, not only canonical ones: x^2 R^-1 mod p for x
+    drawn over [0, 2p) (BLS12-381 Fr: [0, p)), limb patterns whose top bits
+    carry into the next doubled limb, and the ends of the range.  Pinned by
+    Python big integers and by the general product of x with itself."""
+    import random
+    from tachyon_amd import params as P
+    p = P.FIELDS[field][0]
+    nb = O.FIELD_BYTES[field]
+    R = 1 << (8 * nb)
+    top = 2 * p if field != "bls12_381_fr" else p
+    rnd = random.Random(11)
+    xs = [rnd.randrange(top) for _ in range(4000)]
+    for _ in range(1000):  # limbs with the top bit set (the bit d_j takes from a_(j-1))
+        v = sum((rnd.randrange(1 << 31) | (1 << 31) if rnd.random() < 0.7 else rnd.randrange(1 << 32)) << (32 * j)
+                for j in range(nb // 4))
+        xs.append(v % top)
+    xs += [0, 1, p - 1, top - 1, (1 << 32) - 1, (1 << 64) - 1, R // 4 - 1 if R // 4 - 1 < top else top - 2]
+    if top == 2 * p:
+        xs += [p, p + 1]
+    enc = lambda v: v.to_bytes(nb, "little")
+    a = b"".join(map(enc, xs))
+    got = gpu_field_op(field, "sqr", a, a)
+    rinv = pow(R, -1, p)
+    for k, x in enumerate(xs):
+        assert int.from_bytes(got[nb * k:nb * k + nb], "little") == x * x * rinv % p, (k, hex(x))
+    assert got == gpu_field_op(field, "mul", a, a)

@@ -65,7 +65,8 @@ def asm_operand(v):
     """asm input for operand name v = kind + limb index: a, b, m, wq limbs in
     VGPRs, modulus limbs p in SGPRs."""
     kind, idx = v[0], int(v[1:])
-    src = {"a": f"a[{idx}]", "b": f"b[{idx}]", "m": f"m[{idx}]", "w": f"wq[{idx}]"}
+    src = {"a": f"a[{idx}]", "b": f"b[{idx}]", "m": f"m[{idx}]", "w": f"wq[{idx}]",
+           "d": f"d[{idx}]", "e": f"e[{idx}]"}
     if kind == "p":
         return f'[{v}] "s"(Cfg::kP32[{idx}])'
     return f'[{v}] "v"({src[kind]})'
@@ -130,6 +131,82 @@ def gen(N):
         lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
         lines.append("  }")
     lines.append(f"  r[{N - 1}] = (uint32_t)acc;  // < 2p < 2^{32 * N}: the top word is the last one")
+    lines.append("}")
+    return "\n".join(lines) + "\n"
+
+
+def gen_sqr(N):
+    """Montgomery square by FIPS with the cross products counted once:
+    a^2 = sum_i a_i^2 2^(64i) + sum_i a_i 2^(32i) * 2 sum_{j>i} a_j 2^(32j), and
+    2 sum_{j>i} a_j 2^(32j) has the limbs of 2a (d_j = a_j << 1 | a_(j-1) >> 31)
+    except at j = i + 1, where the bit shifted in from a_i is not part of the
+    sum (e_j = a_j << 1), and no limb N when a < 2^(32N-1) (the caller's
+    precondition: lazy values < 2p of the 254-bit fields, 381-bit values <
+    2p, canonical 255-bit values).  N(N+1)/2 + N^2 products instead of 2N^2:
+    100 instead of 128 for N = 8, 222 instead of 288 for N = 12."""
+    nprod = N * (N + 1) // 2 + N * N
+    lines = [f"// N = {N}: r = a^2 R^-1 < 2p ({nprod} v_mad_u64_u32); a < 2^{32 * N - 1}; see gen_sqr",
+             "template <class Cfg>",
+             f"__device__ __forceinline__ void mont_sqr_fips_{N}(uint32_t* __restrict__ r, const uint32_t* __restrict__ a) {{",
+             f"  uint32_t m[{N}], d[{N}], e[{N}];",
+             f"  for (int j = 1; j < {N}; ++j) {{",
+             "    d[j] = __builtin_amdgcn_alignbit(a[j], a[j - 1], 31);",
+             "    e[j] = a[j] << 1;",
+             "  }",
+             "  uint64_t acc = 0;",
+             f"  uint64_t sc[{NCARRY}];  // carry-out lane masks (SGPR pairs)",
+             "  uint32_t c2;"]
+
+    def sq_pairs(k):
+        pairs = []
+        for i in range(0, (k + 1) // 2):
+            j = k - i
+            if j >= N or j <= i:
+                continue
+            pairs.append((f"a{i}", f"e{j}" if j == i + 1 else f"d{j}"))
+        if k % 2 == 0 and k // 2 < N:
+            pairs.append((f"a{k // 2}", f"a{k // 2}"))
+        return pairs
+
+    for k in range(N):
+        pairs = []
+        sq = sq_pairs(k)
+        for j in range(k):
+            pairs.append((f"m{j}", f"p{k - j}"))
+        # interleave the square's products with the reduction's
+        mixed = []
+        for t in range(max(len(sq), len(pairs))):
+            if t < len(sq):
+                mixed.append(sq[t])
+            if t < len(pairs):
+                mixed.append(pairs[t])
+        lines.append(f"  {{  // column {k}")
+        if k == 0:  # a0*a0 + 0 cannot carry out
+            lines.append('    asm("v_mad_u64_u32 %[acc], %[s0], %[a0], %[a0], %[acc]"\n'
+                         '                 : [acc] "+&v"(acc), [s0] "=&s"(sc[0])\n'
+                         '                 : [a0] "v"(a[0]));')
+            lines.append("    c2 = 0;")
+        else:
+            lines.append(asm_stmt(mixed, fresh_c2=True).rstrip("\n"))
+        lines.append(f"    m[{k}] = (uint32_t)acc * Cfg::kInv32;")
+        lines.append(asm_stmt([(f"m{k}", "p0")]).rstrip("\n"))
+        lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
+        lines.append("  }")
+    for k in range(N, 2 * N - 1):
+        sq = sq_pairs(k)
+        pairs = [(f"m{j}", f"p{k - j}") for j in range(k - N + 1, N)]
+        mixed = []
+        for t in range(max(len(sq), len(pairs))):
+            if t < len(sq):
+                mixed.append(sq[t])
+            if t < len(pairs):
+                mixed.append(pairs[t])
+        lines.append(f"  {{  // column {k}")
+        lines.append(asm_stmt(mixed, fresh_c2=True).rstrip("\n"))
+        lines.append(f"    r[{k - N}] = (uint32_t)acc;")
+        lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
+        lines.append("  }")
+    lines.append(f"  r[{N - 1}] = (uint32_t)acc;")
     lines.append("}")
     return "\n".join(lines) + "\n"
 
@@ -332,6 +409,7 @@ def main():
                 "  static constexpr uint32_t get(int i) { return k2p ? Cfg::kP232[i] : Cfg::kP32[i]; }\n};\n")
     for N in (8, 12):
         text.append(gen(N))
+        text.append(gen_sqr(N))
         text.append(gen_addsub(N))
     text.append(gen_shoup(8))
     text.append("}  // namespace tachyon_amd::detail")
