@@ -365,8 +365,9 @@ TACHYON_C_EXPORT void tachyon_mi355x_gen_bases_at(int curve, uint64_t seed, size
  * (non_)affine_point_correctness_gpu_test.cc).  field: 0 bn254_fq, 1 bn254_fr,
  * 2 bls12_381_fq, 3 bls12_381_fr; op: 0 add 1 sub 2 mul 3 sqr 4 neg 5 inv
  * 6 to_mont 7 from_mont 8 dbl 9 a times the plain constant b (the NTT's
- * twiddle product: Shoup on BN254 Fr/Fq, a any 256-bit value).  Host buffers
- * in, host buffer out. */
+ * twiddle product: Shoup on BN254 Fr/Fq, a any 256-bit value) 10 a b - b a
+ * and 11 a b - a^2 through the fused one-reduction a b - c d of the XYZZ
+ * y coordinates.  Host buffers in, host buffer out. */
 TACHYON_C_EXPORT void tachyon_mi355x_field_op(int field, int op, const void* a, const void* b, void* out,
                                               size_t count);
 /* point op: 0 add (affine + affine), 1 double, 2 add-mixed into xyzz of a. Affine in/out. */

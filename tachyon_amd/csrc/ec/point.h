@@ -4,7 +4,8 @@
 //   Affine {x, y}, identity = (0, 0), no infinity flag    affine_point.h:39,125
 //   XYZZ   {x, y, zz, zzz}, zero <=> zz == 0               point_xyzz.h:38,193
 //   Jacobian {x, y, z}, zero <=> z == 0                     jacobian_point.h:40,195
-// Formulas (EFD, as in point_xyzz_impl.h):
+// Formulas (EFD, as in point_xyzz_impl.h; the y coordinates' a b - c d as
+// one fused product, Fp::mul_sub):
 //   madd-2008-s (:129-176), add-2008-s (:44-97), dbl-2008-s-1 (:199-236).
 #pragma once
 #include "../field/ff.h"
@@ -65,7 +66,7 @@ struct XYZZ {
     m = m + m.dbl();
     XYZZ r;
     r.x = m.sqr() - s.dbl();
-    r.y = m * (s - r.x) - w * y;
+    r.y = m.mul_sub(s - r.x, w, y);
     r.zz = v * zz;
     r.zzz = w * zzz;
     return r;
@@ -83,7 +84,7 @@ struct XYZZ {
     F q = x * pp;
     XYZZ c;
     c.x = r.sqr() - ppp - q.dbl();
-    c.y = r * (q - c.x) - y * ppp;
+    c.y = r.mul_sub(q - c.x, y, ppp);
     c.zz = zz * pp;
     c.zzz = zzz * ppp;
     return c;
@@ -105,7 +106,7 @@ struct XYZZ {
     F q = x * pp;
     XYZZ c;
     c.x = r.sqr() - ppp - q.dbl();
-    c.y = r * (q - c.x) - y * ppp;
+    c.y = r.mul_sub(q - c.x, y, ppp);
     c.zz = zz * pp;
     c.zzz = zzz * ppp;
     return c;
@@ -125,7 +126,7 @@ struct XYZZ {
     F q = u1 * pp;
     XYZZ c;
     c.x = r.sqr() - ppp - q.dbl();
-    c.y = r * (q - c.x) - s1 * ppp;
+    c.y = r.mul_sub(q - c.x, s1, ppp);
     c.zz = zz * b.zz * pp;
     c.zzz = zzz * b.zzz * ppp;
     return c;

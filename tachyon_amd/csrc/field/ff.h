@@ -40,6 +40,11 @@
 #ifndef TA_FIELD_SQR
 #define TA_FIELD_SQR 1
 #endif
+// a b - c d with one reduction (mont_asm.h mont_mul_sub_fips_N); 0 = two
+// products and a modular subtraction
+#ifndef TA_FIELD_MULSUB
+#define TA_FIELD_MULSUB 1
+#endif
 
 namespace tachyon_amd {
 
@@ -370,6 +375,32 @@ struct Fp {
     for (int i = 0; i < N; ++i) r.v[i] = t[i];
     return r;
   }
+  // (*this) b - c d with one Montgomery reduction (mont_asm.h gen_mulsub):
+  // the y coordinate of the XYZZ additions.  Device, lazy fields: the
+  // columns sum a b + (2p - c) d; the REDC output is < 3p (p < 2^254), one
+  // conditional subtraction of 2p puts it back in [0, 2p)
+  TA_HD Fp mul_sub(const Fp& b, const Fp& c, const Fp& d) const {
+    if constexpr (N <= 8) return mul_sub_inline(b, c, d);
+    else return (*this) * b - c * d;
+  }
+  TA_HD Fp mul_sub_inline(const Fp& b, const Fp& c, const Fp& d) const {
+#if defined(__HIP_DEVICE_COMPILE__) && TA_FIELD_MULSUB
+    if constexpr (N == 8 && kLazy) {
+      static_assert(Cfg::kModulusBits <= 32 * N - 2, "mul_sub: 8p^2/R + p < 3p");
+      Fp r;
+      detail::mont_mul_sub_fips_8<Cfg>(r.v, v, b.v, c.v, d.v);
+      detail::cond_sub_8<Cfg, true>(r.v);
+      return r;
+    } else if constexpr (N == 12 && kLazy) {
+      static_assert(Cfg::kModulusBits <= 32 * N - 3, "mul_sub: 8p^2/R + p < 2p");
+      Fp r;  // BLS12-381 Fq: already below 2p
+      detail::mont_mul_sub_fips_12<Cfg>(r.v, v, b.v, c.v, d.v);
+      return r;
+    }
+#endif
+    return mul_inline(b) - c.mul_inline(d);
+  }
+
   // Squares count each cross product once (mont_asm.h gen_sqr: 100 instead
   // of 128 v_mad_u64_u32 for 8 limbs); the device square needs a value below
   // 2^(32N-1), which every representation here keeps (lazy < 2p of a 254- or
@@ -456,6 +487,7 @@ struct Fp2 {
     F m = (c0 + c1) * (o.c0 + o.c1);
     return {v0 - v1, m - v0 - v1};
   }
+  TA_HD Fp2 mul_sub(const Fp2& b, const Fp2& c, const Fp2& d) const { return (*this) * b - c * d; }
   TA_HD Fp2 sqr() const {
     F ab = c0 * c1;
     return {(c0 + c1) * (c0 - c1), ab.dbl()};
@@ -484,6 +516,7 @@ struct HotFp : F {
   TA_HD HotFp operator*(const HotFp& o) const { return F::mul_inline(o); }
   TA_HD HotFp dbl() const { return F::dbl(); }
   TA_HD HotFp sqr() const { return F::sqr_inline(); }
+  TA_HD HotFp mul_sub(const HotFp& b, const HotFp& c, const HotFp& d) const { return F::mul_sub_inline(b, c, d); }
   TA_HD HotFp inverse() const { return F::inverse(); }
   TA_HD HotFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
   TA_HD HotFp mul_shoup(const HotFp& w, const HotFp& wq) const { return F::mul_shoup(w, wq); }
@@ -542,6 +575,7 @@ struct CallFp : F {
     return F::sqr_inline();
 #endif
   }
+  TA_HD CallFp mul_sub(const CallFp& b, const CallFp& c, const CallFp& d) const { return (*this) * b - c * d; }
   TA_HD CallFp inverse() const { return F::inverse(); }
   TA_HD CallFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
   TA_HD CallFp canonical() const { return F::canonical(); }

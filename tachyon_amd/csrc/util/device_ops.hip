@@ -136,6 +136,8 @@ __global__ __launch_bounds__(kBlock) void field_op_kernel(int op, const F* a, co
       if constexpr (F::N == 8 && F::kLazyCapable) r = x.mul_shoup(y, F::shoup_quotient(y));
       else r = x * y.to_mont();
       break;
+    case 10: r = x.mul_sub(y, y, x); break;  // x y - y x through the fused a b - c d: zero
+    case 11: r = x.mul_sub(y, x, x); break;  // x y - x^2
     default: r = F::zero();
   }
   out[i] = r.canonical();

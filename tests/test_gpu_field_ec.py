@@ -13,7 +13,7 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 OPS = {"add": 0, "sub": 1, "mul": 2, "sqr": 3, "neg": 4, "inv": 5, "to_mont": 6, "from_mont": 7, "dbl": 8,
-       "mul_const": 9}
+       "mul_const": 9, "mul_sub_zero": 10, "mul_sub_x2": 11}
 
 
 def gpu_field_op(field, op, a: bytes, b: bytes) -> bytes:
@@ -161,3 +161,35 @@ def test_square_every_representative(field):
     for k, x in enumerate(xs):
         assert int.from_bytes(got[nb * k:nb * k + nb], "little") == x * x * rinv % p, (k, hex(x))
     assert got == gpu_field_op(field, "mul", a, a)
+
+
+@pytest.mark.parametrize("field", ["bn254_fq", "bn254_fr", "bls12_381_fq", "bls12_381_fr"])
+def test_fused_mul_sub_every_representative(field):
+    """Field ops 10 / 11 = Fp::mul_sub, a b - c d with one Montgomery
+    reduction over the columns of a b + (2p - c) d (the y coordinate of every
+    XYZZ addition).  Its REDC output reaches [2p, 3p) for the 254-bit fields,
+    so the conditional subtraction after it is exercised by inputs drawn over
+    the whole lazy range [0, 2p) and by the ends of the range.  Pinned by
+    Python big integers (x y R^-1 - x^2 R^-1 mod p) and by op 10's zero."""
+    import random
+    from tachyon_amd import params as P
+    p = P.FIELDS[field][0]
+    nb = O.FIELD_BYTES[field]
+    R = 1 << (8 * nb)
+    top = 2 * p if field != "bls12_381_fr" else p
+    rnd = random.Random(13)
+    xs = [rnd.randrange(top) for _ in range(6000)]
+    ys = [rnd.randrange(top) for _ in range(6000)]
+    ends = [0, 1, p - 1, top - 1] + ([p, p + 1] if top == 2 * p else [])
+    for u in ends:
+        for v in ends:
+            xs.append(u)
+            ys.append(v)
+    enc = lambda v: v.to_bytes(nb, "little")
+    a = b"".join(map(enc, xs))
+    b = b"".join(map(enc, ys))
+    got = gpu_field_op(field, "mul_sub_x2", a, b)
+    rinv = pow(R, -1, p)
+    for k, (x, y) in enumerate(zip(xs, ys)):
+        assert int.from_bytes(got[nb * k:nb * k + nb], "little") == (x * y - x * x) * rinv % p, (k, hex(x), hex(y))
+    assert gpu_field_op(field, "mul_sub_zero", a, b) == bytes(len(a))

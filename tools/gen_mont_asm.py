@@ -66,7 +66,7 @@ def asm_operand(v):
     VGPRs, modulus limbs p in SGPRs."""
     kind, idx = v[0], int(v[1:])
     src = {"a": f"a[{idx}]", "b": f"b[{idx}]", "m": f"m[{idx}]", "w": f"wq[{idx}]",
-           "d": f"d[{idx}]", "e": f"e[{idx}]"}
+           "d": f"d[{idx}]", "e": f"e[{idx}]", "x": f"x[{idx}]", "y": f"y[{idx}]"}
     if kind == "p":
         return f'[{v}] "s"(Cfg::kP32[{idx}])'
     return f'[{v}] "v"({src[kind]})'
@@ -203,6 +203,58 @@ def gen_sqr(N):
                 mixed.append(pairs[t])
         lines.append(f"  {{  // column {k}")
         lines.append(asm_stmt(mixed, fresh_c2=True).rstrip("\n"))
+        lines.append(f"    r[{k - N}] = (uint32_t)acc;")
+        lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
+        lines.append("  }")
+    lines.append(f"  r[{N - 1}] = (uint32_t)acc;")
+    lines.append("}")
+    return "\n".join(lines) + "\n"
+
+
+def gen_mulsub(N):
+    """r = (a*b - c*d) R^-1 mod p with ONE Montgomery reduction: the columns
+    accumulate a*b + x*y + m*p where x = 2p - c (c < 2p, so x in (0, 2p], no
+    borrow out) and y = d.  T = a*b + x*y < 8p^2, so the REDC output is
+    < 8p^2/R + p: below 2p when p < 2^(32N-3) (BLS12-381 Fq), below 3p when p <
+    2^(32N-2) (BN254), where one conditional subtraction of 2p follows (the
+    caller's).  2N^2 + N^2 products + N digits instead of two full products
+    and a modular subtraction (the y coordinate of every XYZZ addition)."""
+    lines = [f"// N = {N}: r = (a b - c d) R^-1 < 8p^2/R + p ({3 * N * N} v_mad_u64_u32); see gen_mulsub",
+             "template <class Cfg>",
+             f"__device__ __forceinline__ void mont_mul_sub_fips_{N}(uint32_t* __restrict__ r, const uint32_t* __restrict__ a,",
+             f"    const uint32_t* __restrict__ b, const uint32_t* __restrict__ c, const uint32_t* __restrict__ y) {{",
+             f"  uint32_t m[{N}], x[{N}];"]
+    # (a literal and the VCC carry-in would be two constant-bus reads: the
+    # modulus limbs move into x first)
+    L = [f"v_mov_b32 %[x{i}], %[k{i}]" for i in range(1, N)]
+    L += ["v_sub_co_u32 %[x0], vcc, %[k0], %[q0]"]
+    for i in range(1, N):
+        L += ["s_nop 1", f"v_subb_co_u32 %[x{i}], vcc, %[x{i}], %[q{i}], vcc"]
+    lines.append(asm_block(L, [f'[x{i}] "=&v"(x[{i}])' for i in range(N)],
+                           [f'[k{i}] "i"(Cfg::kP232[{i}])' for i in range(N)] +
+                           [f'[q{i}] "v"(c[{i}])' for i in range(N)]).rstrip("\n"))
+    lines += ["  uint64_t acc = 0;", f"  uint64_t sc[{NCARRY}];", "  uint32_t c2;"]
+    for k in range(N):
+        pairs = []
+        for j in range(k + 1):
+            pairs.append((f"a{j}", f"b{k - j}"))
+            pairs.append((f"x{j}", f"y{k - j}"))
+            if j < k:
+                pairs.append((f"m{j}", f"p{k - j}"))
+        lines.append(f"  {{  // column {k}")
+        lines.append(asm_stmt(pairs, fresh_c2=True).rstrip("\n"))
+        lines.append(f"    m[{k}] = (uint32_t)acc * Cfg::kInv32;")
+        lines.append(asm_stmt([(f"m{k}", "p0")]).rstrip("\n"))
+        lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
+        lines.append("  }")
+    for k in range(N, 2 * N - 1):
+        pairs = []
+        for j in range(k - N + 1, N):
+            pairs.append((f"a{j}", f"b{k - j}"))
+            pairs.append((f"x{j}", f"y{k - j}"))
+            pairs.append((f"m{j}", f"p{k - j}"))
+        lines.append(f"  {{  // column {k}")
+        lines.append(asm_stmt(pairs, fresh_c2=True).rstrip("\n"))
         lines.append(f"    r[{k - N}] = (uint32_t)acc;")
         lines.append("    acc = (acc >> 32) | ((uint64_t)c2 << 32);")
         lines.append("  }")
@@ -411,6 +463,8 @@ def main():
         text.append(gen(N))
         text.append(gen_sqr(N))
         text.append(gen_addsub(N))
+    text.append(gen_mulsub(8))
+    text.append(gen_mulsub(12))
     text.append(gen_shoup(8))
     text.append("}  // namespace tachyon_amd::detail")
     with open(OUT, "w") as f:
