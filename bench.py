@@ -41,7 +41,11 @@ SEED = 0x7AC40001
 # Measured BN254 Montgomery-multiply ceiling of the chip (tools/microbench/mulmod_rates.hip,
 # 8 waves/SIMD, profiles/r01/microbench_int_rates.txt): the VALU roofline of both kernels.
 MULMOD_PEAK_G = 129.0
-MADD_MULMODS = 10  # madd-2008-s: 8 multiplications + 2 squarings (point_xyzz_impl.h:129-176)
+# madd-2008-s (point_xyzz_impl.h:129-176): 8 multiplications + 2 squarings, in
+# 256-bit Montgomery-product equivalents of v_mad_u64_u32 work (128 each): 6
+# products, the y coordinate's fused a*b - c*d (192 = 2 products, one
+# reduction) and 2 FIPS squares (100 each) -> 1160 / 128 = 9.06
+MADD_MULMODS = (6 * 128 + 192 + 2 * 100) / 128
 
 
 def pmc_traffic(kernel):
@@ -497,7 +501,8 @@ def main():
         "msm_phase_ms": phases,
         "valu_roofline": {"bound": "valu", "kernel": "seg_acc_kernel", "achieved": acc_gmulmod,
                           "peak": MULMOD_PEAK_G, "unit": "G mulmod/s", "frac": acc_gmulmod / MULMOD_PEAK_G,
-                          "note": "n x windows mixed additions x 10 Montgomery products per launch / launch time; "
+                          "note": "n x windows mixed additions x 9.06 Montgomery-product equivalents (6 products, "
+                                  "a fused a*b - c*d, 2 squares: 1160 v_mad_u64_u32) per launch / launch time; "
                                   "peak = measured BN254 mulmod ceiling (tools/microbench/mulmod_rates.hip)"},
     }
 
