@@ -49,6 +49,10 @@
 #ifndef TA_FQ2_MULSUB
 #define TA_FQ2_MULSUB 1
 #endif
+// Fq2 products over the inline 8-limb field as two fused products
+#ifndef TA_FQ2_FUSED_MUL
+#define TA_FQ2_FUSED_MUL 1
+#endif
 // the 12-limb fused a b - c d as one register-argument call (48 words in)
 // for BLS12-381 Fq2: off -- measured neutral (2^22 52.2 vs 52.1 ms) with 30
 // more VGPR spills at the G2 kernel's 2-wave cap
@@ -411,6 +415,20 @@ struct Fp {
     return mul_inline(b) - c.mul_inline(d);
   }
 
+  // (*this) b + c d with one Montgomery reduction (mont_mul_add_fips_8; the
+  // Fq2 product's imaginary part), < 3p before one conditional subtraction
+  TA_HD Fp mul_add_inline(const Fp& b, const Fp& c, const Fp& d) const {
+#if defined(__HIP_DEVICE_COMPILE__) && TA_FIELD_MULSUB
+    if constexpr (N == 8 && kLazy) {
+      Fp r;
+      detail::mont_mul_add_fips_8<Cfg>(r.v, v, b.v, c.v, d.v);
+      detail::cond_sub_8<Cfg, true>(r.v);
+      return r;
+    }
+#endif
+    return mul_inline(b) + c.mul_inline(d);
+  }
+
   // Squares count each cross product once (mont_asm.h gen_sqr: 100 instead
   // of 128 v_mad_u64_u32 for 8 limbs); the device square needs a value below
   // 2^(32N-1), which every representation here keeps (lazy < 2p of a 254- or
@@ -492,6 +510,14 @@ struct Fp2 {
   }
   TA_HD_NOINLINE Fp2 mul_outline(const Fp2& o) const { return mul_inline(o); }
   TA_HD Fp2 mul_inline(const Fp2& o) const {
+#if TA_FQ2_FUSED_MUL
+    // inline 8-limb base field (BN254 Fq2): schoolbook as two fused
+    // products -- a0 b0 - a1 b1 and a0 b1 + a1 b0, two reductions instead of
+    // Karatsuba's three and no Karatsuba sums/differences (the same 384
+    // v_mad_u64_u32)
+    if constexpr (F::N == 8 && F::kLazy && F::kExtInline)
+      return {c0.mul_sub(o.c0, c1, o.c1), c0.mul_add_inline(o.c1, c1, o.c0)};
+#endif
     F v0 = c0 * o.c0;
     F v1 = c1 * o.c1;
     F m = (c0 + c1) * (o.c0 + o.c1);
@@ -541,6 +567,7 @@ struct HotFp : F {
   TA_HD HotFp dbl() const { return F::dbl(); }
   TA_HD HotFp sqr() const { return F::sqr_inline(); }
   TA_HD HotFp mul_sub(const HotFp& b, const HotFp& c, const HotFp& d) const { return F::mul_sub_inline(b, c, d); }
+  TA_HD HotFp mul_add_inline(const HotFp& b, const HotFp& c, const HotFp& d) const { return F::mul_add_inline(b, c, d); }
   TA_HD HotFp inverse() const { return F::inverse(); }
   TA_HD HotFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
   TA_HD HotFp mul_shoup(const HotFp& w, const HotFp& wq) const { return F::mul_shoup(w, wq); }

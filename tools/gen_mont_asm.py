@@ -211,6 +211,17 @@ def gen_sqr(N):
     return "\n".join(lines) + "\n"
 
 
+def gen_muladd(N):
+    """r = (a*b + c*d) R^-1 mod p with one Montgomery reduction (the Fq2
+    product's imaginary part a0 b1 + a1 b0): gen_mulsub's columns with x = c."""
+    text = gen_mulsub(N)
+    head, body = text.split("  uint64_t acc = 0;", 1)
+    head = head.replace(f"mont_mul_sub_fips_{N}", f"mont_mul_add_fips_{N}")
+    head = head.replace("r = (a b - c d) R^-1", "r = (a b + c d) R^-1").replace("see gen_mulsub", "see gen_muladd")
+    head = head.split(f"  uint32_t m[{N}], x[{N}];")[0] + f"  uint32_t m[{N}];\n  const uint32_t* __restrict__ x = c;\n"
+    return head + "  uint64_t acc = 0;" + body
+
+
 def gen_mulsub(N):
     """r = (a*b - c*d) R^-1 mod p with ONE Montgomery reduction: the columns
     accumulate a*b + x*y + m*p where x = 2p - c (c < 2p, so x in (0, 2p], no
@@ -465,6 +476,7 @@ def main():
         text.append(gen_addsub(N))
     text.append(gen_mulsub(8))
     text.append(gen_mulsub(12))
+    text.append(gen_muladd(8))
     text.append(gen_shoup(8))
     text.append("}  // namespace tachyon_amd::detail")
     with open(OUT, "w") as f:
