@@ -53,6 +53,10 @@
 #ifndef TA_FQ2_FUSED_MUL
 #define TA_FQ2_FUSED_MUL 1
 #endif
+// BLS12-381 Fq2 products as two fused register-argument calls (48 words in)
+#ifndef TA_CALL_FUSED_MUL
+#define TA_CALL_FUSED_MUL 0
+#endif
 // the 12-limb fused a b - c d as one register-argument call (48 words in)
 // for BLS12-381 Fq2: off -- measured neutral (2^22 52.2 vs 52.1 ms) with 30
 // more VGPR spills at the G2 kernel's 2-wave cap
@@ -424,6 +428,10 @@ struct Fp {
       detail::mont_mul_add_fips_8<Cfg>(r.v, v, b.v, c.v, d.v);
       detail::cond_sub_8<Cfg, true>(r.v);
       return r;
+    } else if constexpr (N == 12 && kLazy) {
+      Fp r;  // BLS12-381 Fq: < 2p already
+      detail::mont_mul_add_fips_12<Cfg>(r.v, v, b.v, c.v, d.v);
+      return r;
     }
 #endif
     return mul_inline(b) + c.mul_inline(d);
@@ -515,7 +523,7 @@ struct Fp2 {
     // products -- a0 b0 - a1 b1 and a0 b1 + a1 b0, two reductions instead of
     // Karatsuba's three and no Karatsuba sums/differences (the same 384
     // v_mad_u64_u32)
-    if constexpr (F::N == 8 && F::kLazy && F::kExtInline)
+    if constexpr (F::kLazy && F::kExtInline && (F::N == 8 || TA_CALL_FUSED_MUL))
       return {c0.mul_sub(o.c0, c1, o.c1), c0.mul_add_inline(o.c1, c1, o.c0)};
 #endif
     F v0 = c0 * o.c0;
@@ -598,6 +606,11 @@ __device__ __noinline__ F mul_sub_in_regs(TA_LIMBS12(a), TA_LIMBS12(b), TA_LIMBS
   return x.mul_sub_inline(y, z, w);
 }
 template <class F>
+__device__ __noinline__ F mul_add_in_regs(TA_LIMBS12(a), TA_LIMBS12(b), TA_LIMBS12(c), TA_LIMBS12(d)) {
+  const F x{TA_UNPACK12(a)}, y{TA_UNPACK12(b)}, z{TA_UNPACK12(c)}, w{TA_UNPACK12(d)};
+  return x.mul_add_inline(y, z, w);
+}
+template <class F>
 __device__ __noinline__ F sqr_in_regs(TA_LIMBS12(a)) {
   const F x{TA_UNPACK12(a)};
   return x.sqr_inline();
@@ -636,6 +649,13 @@ struct CallFp : F {
     return detail::mul_sub_in_regs<F>(TA_PASS12((*this)), TA_PASS12(b), TA_PASS12(c), TA_PASS12(d));
 #else
     return (*this) * b - c * d;
+#endif
+  }
+  TA_HD CallFp mul_add_inline(const CallFp& b, const CallFp& c, const CallFp& d) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return detail::mul_add_in_regs<F>(TA_PASS12((*this)), TA_PASS12(b), TA_PASS12(c), TA_PASS12(d));
+#else
+    return F::mul_add_inline(b, c, d);
 #endif
   }
   TA_HD CallFp inverse() const { return F::inverse(); }

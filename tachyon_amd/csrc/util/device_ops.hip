@@ -136,8 +136,10 @@ __global__ __launch_bounds__(kBlock) void field_op_kernel(int op, const F* a, co
       if constexpr (F::N == 8 && F::kLazyCapable) r = x.mul_shoup(y, F::shoup_quotient(y));
       else r = x * y.to_mont();
       break;
-    case 10: r = x.mul_sub(y, y, x); break;  // x y - y x through the fused a b - c d: zero
-    case 11: r = x.mul_sub(y, x, x); break;  // x y - x^2
+    // x y - y x (zero) and x y - x^2 through the fused a b - c d, in the hot
+    // kernels' inline view (12-limb fields fuse only there)
+    case 10: r = HotFp<F>(x).mul_sub(HotFp<F>(y), HotFp<F>(y), HotFp<F>(x)); break;
+    case 11: r = HotFp<F>(x).mul_sub(HotFp<F>(y), HotFp<F>(x), HotFp<F>(x)); break;
     default: r = F::zero();
   }
   out[i] = r.canonical();

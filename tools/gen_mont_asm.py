@@ -477,6 +477,7 @@ def main():
     text.append(gen_mulsub(8))
     text.append(gen_mulsub(12))
     text.append(gen_muladd(8))
+    text.append(gen_muladd(12))
     text.append(gen_shoup(8))
     text.append("}  // namespace tachyon_amd::detail")
     with open(OUT, "w") as f:
