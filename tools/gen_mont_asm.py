@@ -460,7 +460,9 @@ def gen_addsub(N):
     return "\n".join(out)
 
 
-def main():
+def render():
+    """The text of mont_asm.h (tests/test_generated_asm.py checks the committed
+    header against it)."""
     text = ["// GENERATED by tools/gen_mont_asm.py -- do not edit.",
             "// FIPS Montgomery product for gfx950 (see the generator for the rationale).",
             "// Output is < 2p (the caller applies the final conditional subtraction).",
@@ -480,8 +482,12 @@ def main():
     text.append(gen_muladd(12))
     text.append(gen_shoup(8))
     text.append("}  // namespace tachyon_amd::detail")
+    return "\n".join(text) + "\n"
+
+
+def main():
     with open(OUT, "w") as f:
-        f.write("\n".join(text) + "\n")
+        f.write(render())
     print("wrote", os.path.relpath(OUT, ROOT))
 
 
