@@ -14,13 +14,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def newest_bench_line():
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line*.json")), key=os.path.getmtime)
+    # newest round tag first (file mtimes are the checkout's); the 1-GPU
+    # default-run lines only (multi-rank rehearsals carry no CPU baseline)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line*.json")))
     if not files:
         pytest.skip("no committed bench line")
     for path in reversed(files):
+        if "rehearsal" in os.path.basename(path):
+            continue
         text = open(path).read().strip()
         if text.startswith("{"):
-            return path, json.loads(text.splitlines()[-1])
+            d = json.loads(text.splitlines()[-1])
+            if d.get("n_gpus") == 1:
+                return path, d
     pytest.skip("no parsable bench line")
 
 
