@@ -39,8 +39,11 @@ MSM_BYTES_PER_POINT = 96  # 64 B affine base + 32 B scalar
 NTT_BYTES_PER_ELEM = 64   # 32 B in + 32 B out per transform
 SEED = 0x7AC40001
 # Measured BN254 Montgomery-multiply ceiling of the chip (tools/microbench/mulmod_rates.hip,
-# 8 waves/SIMD, profiles/r01/microbench_int_rates.txt): the VALU roofline of both kernels.
-MULMOD_PEAK_G = 129.0
+# DESIGN.md section 4): 138.6 G/s with >= 2 independent product chains per lane or >= 4
+# waves per SIMD (129.3 G with one chain at one wave): the VALU roofline of both kernels.
+MULMOD_PEAK_G = 138.6
+MULMOD_PEAK_NOTE = ("measured BN254 FIPS Montgomery-product ceiling of the chip, 138.6 G/s with >= 2 "
+                    "independent chains per lane or >= 4 waves/SIMD (tools/microbench/mulmod_rates.hip)")
 # madd-2008-s (point_xyzz_impl.h:129-176): 8 multiplications + 2 squarings, in
 # 256-bit Montgomery-product equivalents of v_mad_u64_u32 work (128 each): 6
 # products, the y coordinate's fused a*b - c*d (192 = 2 products, one
@@ -78,6 +81,8 @@ def parse():
     ap.add_argument("--cpu-log-n", type=int, default=0,
                     help="CPU baseline MSM size (0 = the headline --log-n)")
     ap.add_argument("--no-host-resident", action="store_true")
+    ap.add_argument("--no-non-uniform", action="store_true",
+                    help="skip the NonUniform(n, 1) leg (benchmark/msm --test_set non_uniform)")
     ap.add_argument("--msm-split", choices=("points", "windows"), default="points",
                     help="N > 1 MSM partition: point shards (default), or window ranges with every rank holding "
                          "all points (c = 16: W = 16 windows; measured slower per rank, tools/split_probe.py)")
@@ -237,9 +242,18 @@ def bench_bls(args, rank, world, barrier, dist, backend):
             t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        out[curve.split("_")[-1]] = {"ms_per_msm": dt * 1e3, "scalars_per_s": n_total / dt,
-                                     "consistent": res == ref, "points_per_gpu": n}
+        leg = out[curve.split("_")[-1]] = {"ms_per_msm": dt * 1e3, "scalars_per_s": n_total / dt,
+                                           "consistent": res == ref, "points_per_gpu": n}
         msm.close()
+        if world == 1 and not args.no_cpu_baseline:
+            # the reference's GPU-vs-CPU check (variable_base_msm_gpu_unittest.cc:25-78) at the timed
+            # size: the oracle's kParallelTerm MSM of the same inputs on the host cores
+            from oracle import oracle as O
+            hb, hs = d_b.cpu().numpy(), d_s.cpu().numpy()
+            t0 = time.perf_counter()
+            leg["gpu_equals_cpu"] = O.msm_np(curve, hb, hs, method="parallel_term", threads=cpu_threads()) == res
+            leg["cpu_seconds"] = round(time.perf_counter() - t0, 2)
+            del hb, hs
         del d_b, d_s
         if world > 1:  # the sharded MSM must equal the unsharded one
             out[curve.split("_")[-1]]["consistent_with_1gpu"] = full_msm_equals(curve, n_total, res, rank, dist)
@@ -452,11 +466,15 @@ def main():
     elif args.window_bits:
         c, windows = args.window_bits, D._windows_for("bn254_g1", args.window_bits)
         rank_windows = windows
-    # one launch accumulates every (point, window) digit of the windows it
-    # covers: n x windows / launches point-window units of 96 B each (the
-    # point's base + scalar bytes, consumed once per window)
-    units = n * rank_windows / launches
-    acc_gbs = units * MSM_BYTES_PER_POINT / (acc_ms * 1e-3) / 1e9
+    # the algorithmic bytes of the MSM are its inputs read once,
+    # 96 B per point (64 B affine base + 32 B scalar); one launch covers all n
+    # points of this rank (all windows), so achieved = n x 96 B / launch time.
+    # The (point, window) gathers the kernel actually performs (W x 64 B bases
+    # + 8 B sorted entries per point) are reported beside it as gather_gbs.
+    points_per_launch = n / launches
+    acc_gbs = points_per_launch * MSM_BYTES_PER_POINT / (acc_ms * 1e-3) / 1e9
+    units = n * rank_windows / launches  # mixed additions (point, window) per launch
+    gather_gbs = units * (64 + 8) / (acc_ms * 1e-3) / 1e9
     acc_traffic, acc_traffic_src, acc_traffic_raw = pmc_traffic("seg_acc_kernel")
     acc_gmulmod = units * MADD_MULMODS / (acc_ms * 1e-3) / 1e9
     stream_gbs = stream_copy_gbs()
@@ -493,17 +511,21 @@ def main():
                                            "uncorrected FETCH_SIZE is given as traffic_fetch_raw",
                      "pmc_gbs": (acc_traffic / (acc_ms * 1e-3)) if acc_traffic else None,
                      "kernel": "seg_acc_kernel (bucket accumulation)", "kernel_ms": acc_ms,
-                     "launches_per_msm": launches, "units_per_launch": units,
+                     "launches_per_msm": launches, "points_per_launch": points_per_launch,
+                     "algorithmic_bytes_per_launch": points_per_launch * MSM_BYTES_PER_POINT,
+                     "gather_gbs": gather_gbs, "gathers_per_launch": units,
                      "stream_copy_gbs": stream_gbs, "frac_of_stream_copy": acc_gbs / stream_gbs,
-                     "note": "algorithmic bytes = 96 B per (point, window) unit x n x windows / launches; the "
-                             "kernel is VALU-bound (v_mad_u64_u32), see DESIGN.md; peak = the guide's nominal "
-                             "8 TB/s, stream_copy_gbs = a device-to-device copy measured on this box"},
+                     "note": "algorithmic bytes = SURVEY 8(d)'s 96 B per point (base + scalar read once) x the n "
+                             "points one launch covers / the launch's HIP-event time; gather_gbs = the W x (64 B "
+                             "base + 8 B entry) per point the kernel gathers; the kernel is VALU-bound "
+                             "(v_mad_u64_u32, valu_roofline), see DESIGN.md; peak = the guide's nominal 8 TB/s, "
+                             "stream_copy_gbs = a device-to-device copy measured on this box"},
         "msm_phase_ms": phases,
         "valu_roofline": {"bound": "valu", "kernel": "seg_acc_kernel", "achieved": acc_gmulmod,
                           "peak": MULMOD_PEAK_G, "unit": "G mulmod/s", "frac": acc_gmulmod / MULMOD_PEAK_G,
                           "note": "n x windows mixed additions x 9.06 Montgomery-product equivalents (6 products, "
                                   "a fused a*b - c*d, 2 squares: 1160 v_mad_u64_u32) per launch / launch time; "
-                                  "peak = measured BN254 mulmod ceiling (tools/microbench/mulmod_rates.hip)"},
+                                  "peak = " + MULMOD_PEAK_NOTE},
     }
 
     # ---- configs[1] sweep (2^16, 2^20 .. 2^24: prefixes of the same device-resident input) ----
@@ -521,6 +543,47 @@ def main():
             sweep[str(k)] = {"ms": round(best * 1e3, 3), "scalars_per_s": m / best}
         sweep[str(args.log_n)] = {"ms": round(ms_per_step, 3), "scalars_per_s": value}
         out["msm_sweep"] = sweep
+
+    # ---- NonUniform(n, 1) test set (variable_base_msm_test_set.h:43-53), the set of the reference's
+    # published GPU table (benchmark/msm/README.md:97-111): every scalar equal, so every window puts
+    # all of this rank's points into ONE bucket (the skew path of the load-balanced accumulation) ----
+    if not args.no_non_uniform:
+        one = torch.empty(32, dtype=torch.uint8, device="cuda")
+        M.gen_scalars("bn254_fr", SEED + 3, 1, one.data_ptr())
+        d_nu = one.repeat(max(1, n))
+        torch.cuda.synchronize()
+
+        def nu_step():
+            return D.sharded_msm("bn254_g1", lambda: msm.run(d_bases, d_nu, n), device="cuda")
+
+        nu_ref = nu_step()
+        reps = max(2, min(args.steps, 3))
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            nu_res = nu_step()
+        barrier()
+        dt = (time.perf_counter() - t0) / reps
+        if dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out["non_uniform"] = {"ms_per_msm": dt * 1e3, "scalars_per_s": n_total / dt,
+                              "vs_random_set": dt * 1e3 / ms_per_step, "consistent": nu_res == nu_ref,
+                              "workload": f"BN254 G1 MSM 2^{args.log_n}, NonUniform(n, 1): one seeded scalar "
+                                          f"repeated (benchmark/msm --test_set non_uniform), device-resident"}
+        msm.set_profile(True)
+        msm.run(d_bases, d_nu, n)
+        out["non_uniform"]["phase_ms"] = {k: round(v, 4) for k, v in msm.last_timings().items()}
+        msm.set_profile(False)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            from oracle import oracle as O
+            t0 = time.perf_counter()
+            out["non_uniform"]["gpu_equals_cpu"] = O.msm_np(
+                "bn254_g1", d_bases.cpu().numpy(), d_nu.cpu().numpy(), method="parallel_term",
+                threads=cpu_threads()) == nu_res
+            out["non_uniform"]["cpu_seconds"] = round(time.perf_counter() - t0, 2)
+        del d_nu
 
     # ---- NTT 2^24: one GPU, or the four-step sharded transform (one RCCL all-to-all) ----
     if not args.no_ntt and world > 1:
@@ -583,22 +646,33 @@ def main():
         ntt_in = orig.cpu().numpy()
         ntt_gpu_out = x.cpu().numpy()  # FFT of the input (the round trips left x == orig)
         avg_pass = sum(passes) / len(passes)
+        # 64 B per element per TRANSFORM (read + write the array
+        # once), over the transform's kernel time (all passes)
+        xform_ms = sum(passes)
+        xform_gbs = nn * NTT_BYTES_PER_ELEM / (xform_ms * 1e-3) / 1e9
         pass_gbs = nn * NTT_BYTES_PER_ELEM / (avg_pass * 1e-3) / 1e9
         ntt_traffic, ntt_traffic_src, _ = pmc_traffic("dif_pass_kernel")
         # algorithmic butterflies (one Montgomery product each) per pass: n/2 x log n / passes
         ntt_gmulmod = nn // 2 * args.ntt_log_n / len(passes) / (avg_pass * 1e-3) / 1e9
         out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
                       "round_trip_ok": round_trip_ok, "pass_ms": passes, "mode": "single GPU",
-                      "roofline": {"bound": "hbm", "achieved": pass_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": pass_gbs / HBM_PEAK_GBS, "traffic": ntt_traffic,
-                                   "traffic_unit": "GB per launch", "traffic_source": ntt_traffic_src,
-                                   "kernel": "dif_pass_kernel", "kernel_ms": avg_pass,
-                                   "stream_copy_gbs": stream_gbs, "frac_of_stream_copy": pass_gbs / stream_gbs},
+                      "roofline": {"bound": "hbm", "achieved": xform_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": xform_gbs / HBM_PEAK_GBS, "traffic": ntt_traffic,
+                                   "traffic_unit": "GB per dif_pass_kernel launch",
+                                   "traffic_source": ntt_traffic_src,
+                                   "kernel": "dif_pass_kernel (all passes of one transform)",
+                                   "transform_kernel_ms": xform_ms, "passes": len(passes), "kernel_ms": avg_pass,
+                                   "per_pass_gbs": pass_gbs,
+                                   "note": "algorithmic bytes = SURVEY 8(d)'s 64 B per element per transform / the "
+                                           "summed HIP-event time of the transform's passes; per_pass_gbs prices "
+                                           "one pass's own read + write",
+                                   "stream_copy_gbs": stream_gbs, "frac_of_stream_copy": xform_gbs / stream_gbs},
                       "valu_roofline": {"bound": "valu", "kernel": "dif_pass_kernel", "achieved": ntt_gmulmod,
                                         "peak": MULMOD_PEAK_G, "unit": "G mulmod/s",
                                         "frac": ntt_gmulmod / MULMOD_PEAK_G,
                                         "note": "n/2 x log n butterflies per transform / passes, one product "
-                                                "each (the add/sub of a butterfly are not counted)"}}
+                                                "each (the add/sub of a butterfly are not counted); peak = "
+                                                + MULMOD_PEAK_NOTE}}
         if not args.no_host_resident:
             # reference semantics (fft_runner.h:53-58): host vector in, H2D + transform + D2H
             hv = ntt_in.copy()

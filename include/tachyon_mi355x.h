@@ -356,8 +356,8 @@ TACHYON_C_EXPORT void tachyon_mi355x_gen_scalars(int field, uint64_t seed, size_
                                                  void* stream);
 TACHYON_C_EXPORT void tachyon_mi355x_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, void* d_out,
                                                void* stream);
-/* points [start, start + n) of that same sequence (start a multiple of chunk):
- * a rank's shard of the global input, so N ranks compute the N = 1 MSM. */
+/* points [start, start + n) of that same sequence (any start; the chunk that
+ * holds `start` is advanced by doublings): a rank's shard of the global input, so N ranks compute the N = 1 MSM. */
 TACHYON_C_EXPORT void tachyon_mi355x_gen_bases_at(int curve, uint64_t seed, size_t start, size_t n, size_t chunk,
                                                   void* d_out, void* stream);
 

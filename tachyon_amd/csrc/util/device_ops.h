@@ -10,7 +10,7 @@
 namespace tachyon_amd::util {
 
 void gen_scalars(int field, uint64_t seed, size_t start, size_t n, void* d_out, hipStream_t stream);
-// points [start, start + n) of the seeded sequence (start a multiple of chunk)
+// points [start, start + n) of the seeded sequence (any start)
 void gen_bases(int curve, uint64_t seed, size_t start, size_t n, size_t chunk, void* d_out, hipStream_t stream);
 void field_op(int field, int op, const void* a, const void* b, void* out, size_t count);
 // out[i] = num[i] / den[i] (0 where den[i] == 0) for n BN254 Fr in Montgomery

@@ -93,26 +93,30 @@ struct Gen<Bls381G2> {
 
 // One thread per chunk: k_j * G by double-and-add, then a doubling chain,
 // each point normalised to affine (per-point inversion; a one-off setup cost).
+// The call writes the global points [start, start + n): chunk j of the call is
+// global chunk chunk0 + j, and the first one skips the (start - chunk0 * chunk)
+// points before `start` with doublings, so any start gives the same sequence.
 template <class Curve>
-__global__ __launch_bounds__(kBlock) void gen_bases_kernel(uint64_t seed, uint64_t n, uint64_t chunk,
+__global__ __launch_bounds__(kBlock) void gen_bases_kernel(uint64_t seed, uint64_t start, uint64_t n, uint64_t chunk,
                                                            uint64_t chunk0, Affine<typename Curve::F>* out) {
   using F = typename Curve::F;
   using Fr = typename Curve::Fr;
   uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  uint64_t start = j * chunk;
-  if (start >= n) return;
-  uint64_t len = min(chunk, n - start);
+  const uint64_t gbeg = (chunk0 + j) * chunk;  // global index of this chunk's first point
+  const uint64_t lo = max(gbeg, start), hi = min(gbeg + chunk, start + n);
+  if (lo >= hi) return;
   Affine<F> G{load_generator_coord<F>(Gen<Curve>::x()), load_generator_coord<F>(Gen<Curve>::y())};
   uint64_t k[4];
-  rand_scalar<Fr>(seed ^ kBaseSeedXor, chunk0 + j, k);  // chunk0: global index of this call's first chunk
+  rand_scalar<Fr>(seed ^ kBaseSeedXor, chunk0 + j, k);
   XYZZ<F> r = XYZZ<F>::zero();
   for (int limb = 3; limb >= 0; --limb)
     for (int bit = 63; bit >= 0; --bit) {
       r = r.dbl();
       if ((k[limb] >> bit) & 1) r = r.madd(G);
     }
-  for (uint64_t i = 0; i < len; ++i) {
-    out[start + i] = r.to_affine();
+  for (uint64_t i = gbeg; i < lo; ++i) r = r.dbl();
+  for (uint64_t i = lo; i < hi; ++i) {
+    out[i - start] = r.to_affine();
     r = r.dbl();
   }
 }
@@ -254,18 +258,17 @@ void gen_scalars(int field, uint64_t seed, size_t start, size_t n, void* d_out, 
 void gen_bases(int curve, uint64_t seed, size_t start, size_t n, size_t chunk, void* d_out, hipStream_t stream) {
   if (n == 0) return;
   if (chunk == 0) throw std::runtime_error("tachyon_mi355x_gen_bases: chunk must be > 0");
-  if (start % chunk) throw std::runtime_error("tachyon_mi355x_gen_bases_at: start must be a multiple of chunk");
   const uint64_t chunk0 = start / chunk;
-  size_t chunks = (n + chunk - 1) / chunk;
+  const size_t chunks = (start - chunk0 * chunk + n + chunk - 1) / chunk;
   dim3 g(ceil_div(chunks, kBlock)), b(kBlock);
   switch (curve) {
-    case 0: hipLaunchKernelGGL(gen_bases_kernel<Bn254G1>, g, b, 0, stream, seed, n, chunk, chunk0,
+    case 0: hipLaunchKernelGGL(gen_bases_kernel<Bn254G1>, g, b, 0, stream, seed, start, n, chunk, chunk0,
                                static_cast<Affine<Bn254Fq>*>(d_out)); break;
-    case 1: hipLaunchKernelGGL(gen_bases_kernel<Bn254G2>, g, b, 0, stream, seed, n, chunk, chunk0,
+    case 1: hipLaunchKernelGGL(gen_bases_kernel<Bn254G2>, g, b, 0, stream, seed, start, n, chunk, chunk0,
                                static_cast<Affine<Bn254Fq2>*>(d_out)); break;
-    case 2: hipLaunchKernelGGL(gen_bases_kernel<Bls381G1>, g, b, 0, stream, seed, n, chunk, chunk0,
+    case 2: hipLaunchKernelGGL(gen_bases_kernel<Bls381G1>, g, b, 0, stream, seed, start, n, chunk, chunk0,
                                static_cast<Affine<Bls381Fq>*>(d_out)); break;
-    case 3: hipLaunchKernelGGL(gen_bases_kernel<Bls381G2>, g, b, 0, stream, seed, n, chunk, chunk0,
+    case 3: hipLaunchKernelGGL(gen_bases_kernel<Bls381G2>, g, b, 0, stream, seed, start, n, chunk, chunk0,
                                static_cast<Affine<Bls381Fq2>*>(d_out)); break;
     default: throw std::runtime_error("tachyon_mi355x_gen_bases: unknown curve");
   }

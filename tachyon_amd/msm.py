@@ -152,6 +152,5 @@ def gen_scalars(field: str, seed: int, n: int, d_out_ptr: int, start: int = 0, s
 
 
 def gen_bases(curve: str, seed: int, n: int, chunk: int, d_out_ptr: int, stream=None, start: int = 0):
-    """Points [start, start + n) of the seeded doubling-chain sequence (start a
-    multiple of chunk): every rank can generate its shard of one global input."""
+    """Points [start, start + n) of the seeded doubling-chain sequence (any start): every rank can generate its shard of one global input."""
     lib().tachyon_mi355x_gen_bases_at(CURVES[curve], seed, start, n, chunk, d_out_ptr, stream)

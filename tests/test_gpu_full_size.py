@@ -32,6 +32,86 @@ def test_msm_sweep_vs_oracle(logn):
     assert O.msm_np("bn254_g1", hb, hs) == got
 
 
+def non_uniform_scalars(torch, M, field, n, seed=SEED + 3):
+    """NonUniform(n, 1) (variable_base_msm_test_set.h:43-53; the reference's
+    published GPU table, benchmark/msm --test_set non_uniform): one seeded
+    random scalar repeated n times, on the device."""
+    one = torch.empty(32, dtype=torch.uint8, device="cuda")
+    M.gen_scalars(field, seed, 1, one.data_ptr())
+    torch.cuda.synchronize()
+    return one.repeat(n)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("logn", [23, 26])
+def test_msm_non_uniform_vs_oracle(logn):
+    """Every scalar equal: every window puts all n points into ONE bucket, so
+    at 2^26 one bucket spans ~262 K accumulation threads and the chain join
+    runs at its full depth.  Equals the oracle's kParallelTerm MSM on the same
+    inputs, and s * (sum of the bases) -- the oracle's MSM with unit scalars
+    (one digit per point) scaled by s -- as a second, independent CPU answer."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    n = 1 << logn
+    d_b = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    M.gen_bases("bn254_g1", SEED, n, 1 << 10, d_b.data_ptr())
+    d_s = non_uniform_scalars(torch, M, "bn254_fr", n)
+    m = M.VariableBaseMSMGpu("bn254_g1")
+    got = m.run(d_b, d_s)
+    m.close()
+    hb, hs = d_b.cpu().numpy(), d_s.cpu().numpy()
+    del d_b, d_s
+    assert O.msm_np("bn254_g1", hb, hs) == got
+    from tachyon_amd import params as P
+    ones = np.tile(np.frombuffer(P.mont(1, P.BN254_FR, 4).to_bytes(32, "little"), np.uint8), n)
+    total = O.msm_np("bn254_g1", hb, ones)
+    assert O.msm("bn254_g1", total, hs[:32].tobytes())[0] == got
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("curve,pb", [("bls12_381_g1", 96), ("bls12_381_g2", 192)])
+def test_bls_full_2_24_vs_oracle(curve, pb):
+    """BASELINE configs[3] at the size the bench times: the whole 2^24-point
+    BLS12-381 G1 / G2 MSM on the bench's own input (one GPU, the bench's plan)
+    equals the oracle's kParallelTerm MSM on all host threads
+    (variable_base_msm_gpu_unittest.cc:25-78 compares these groups GPU vs CPU)."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import msm as M
+    n = 1 << 24
+    d_b = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
+    d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    M.gen_bases(curve, SEED, n, 1 << 10, d_b.data_ptr())
+    M.gen_scalars("bls12_381_fr", SEED, n, d_s.data_ptr())
+    torch.cuda.synchronize()
+    m = M.VariableBaseMSMGpu(curve)
+    got = m.run(d_b, d_s)
+    m.close()
+    hb, hs = d_b.cpu().numpy(), d_s.cpu().numpy()
+    del d_b, d_s
+    assert O.msm_np(curve, hb, hs) == got
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("curve,pb", [("bn254_g1", 64), ("bls12_381_g2", 192)])
+def test_gen_bases_any_start(curve, pb):
+    """A rank's slice [start, start + n) of the seeded base sequence equals the
+    same slice of the whole sequence for any start, not only multiples of the
+    chunk (ceil(2^k / N) shards for N = 3, 5, 6, 7 ranks)."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd import dist as D
+    from tachyon_amd import msm as M
+    n_total, chunk = 3 * 4096 + 17, 1 << 10
+    full = torch.empty(n_total * pb, dtype=torch.uint8, device="cuda")
+    M.gen_bases(curve, SEED, n_total, chunk, full.data_ptr())
+    for world in (3, 5, 7):
+        for rank in range(world):
+            start, n = D.shard_range(n_total, rank, world)
+            part = torch.empty(max(1, n) * pb, dtype=torch.uint8, device="cuda")
+            M.gen_bases(curve, SEED, n, chunk, part.data_ptr(), start=start)
+            torch.cuda.synchronize()
+            assert torch.equal(part[:n * pb], full[start * pb:(start + n) * pb]), (world, rank, start)
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("logn", [20, 22, 24])
 def test_ntt_sweep_vs_oracle(logn):
