@@ -340,6 +340,29 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void*
  * icicle_msm_utils.cc:10-68; TACHYON_MSM_MEM_LIMIT caps the free bytes) or when
  * host-resident inputs were uploaded chunk by chunk under the kernels. */
 TACHYON_C_EXPORT size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx);
+/* Schedule of the last run (of its last point chunk): bit 0 the recode fused
+ * with the first radix pass, bit 1 onesweep passes fed by the recode's digit
+ * counts, bit 2 7-byte LDS staging in the recode scatter. */
+TACHYON_C_EXPORT unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx);
+/* One process, several MI355X: every later MSM of this context splits its
+ * points into `count` contiguous shards, shard k on device device_ids[k]
+ * (its own host thread and stream; host inputs are uploaded per shard over
+ * that device's link, device inputs owned by another device are copied
+ * peer-to-peer), and adds the shard results on the host -- the reference's
+ * kParallelTerm chunk-and-sum (pippenger_adapter.h:82-113) and its GPU
+ * divisions loop (icicle_msm_bn254_g1.cc:50-73), across devices.  The
+ * reference pins device 0 (msm_gpu.h:54-56); with this, benchmark/msm and the
+ * scroll_halo2 bridge reach every GPU without torch.  Ids may repeat (several
+ * shards on one GPU).  count <= 1 returns to the context's own device.
+ * Returns 1, or 0 (nothing changed) for an id outside [0, device count).
+ * Environment: TACHYON_MSM_GPU_DEVICES="0,1,2,3" applies it to every new
+ * context (the C-ABI create functions included). */
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_set_devices(int curve, void* ctx, const int* device_ids, size_t count);
+/* The shards of the last multi-device run: for each (up to cap) its wall ms
+ * (upload or peer copy + MSM), point count and device; returns the number of
+ * shards (0 for a single-device context).  Any output pointer may be NULL. */
+TACHYON_C_EXPORT size_t tachyon_mi355x_msm_gpu_last_shards(int curve, const void* ctx, float* shard_ms,
+                                                           size_t* shard_points, int* shard_devices, size_t cap);
 /* window bits / windows the planner picks for `size` points */
 TACHYON_C_EXPORT void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows);
 /* Host-side group arithmetic on affine points (multi-GPU partial sums):

@@ -120,6 +120,10 @@ SIGNATURES = [
     ("tachyon_mi355x_msm_gpu_set_profile", None, [i32, vp, i32]),
     ("tachyon_mi355x_msm_gpu_set_variant", i32, [i32, vp, i32]),
     ("tachyon_mi355x_msm_gpu_last_divisions", sz, [i32, vp]),
+    ("tachyon_mi355x_msm_gpu_last_schedule", ctypes.c_uint, [i32, vp]),
+    ("tachyon_mi355x_msm_gpu_set_devices", i32, [i32, vp, ctypes.POINTER(ctypes.c_int), sz]),
+    ("tachyon_mi355x_msm_gpu_last_shards", sz, [i32, vp, fp, ctypes.POINTER(ctypes.c_size_t),
+                                              ctypes.POINTER(ctypes.c_int), sz]),
     ("tachyon_mi355x_msm_gpu_last_timings", None, [i32, vp, fp]),
     ("tachyon_mi355x_msm_plan", None, [i32, sz, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint)]),
     ("tachyon_mi355x_affine_sum", None, [i32, vp, sz, vp]),

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../msm/msm.h"
+#include "../msm/msm_multi.h"
 #include "../ntt/ntt.h"
 #include "../util/device_ops.h"
 
@@ -41,12 +42,23 @@ namespace {
 template <class Curve>
 struct MsmCtx {
   msm::MsmGpu<Curve> impl;
+  // several devices (tachyon_mi355x_msm_gpu_set_devices or TACHYON_MSM_GPU_DEVICES): one point
+  // shard per device, results added on the host (msm/msm_multi.h); null = impl on the current device
+  std::unique_ptr<msm::MsmMultiDevice<Curve>> multi;
   std::string input_dir;  // TACHYON_MSM_GPU_INPUT_DIR
   bool log = false;       // TACHYON_LOG_MSM=1
   size_t idx = 0;
   explicit MsmCtx(hipStream_t stream = nullptr) : impl(stream) {
     if (const char* d = getenv("TACHYON_MSM_GPU_INPUT_DIR")) input_dir = d;
     if (const char* l = getenv("TACHYON_LOG_MSM")) log = (std::string(l) == "1");
+    if (const char* e = getenv("TACHYON_MSM_GPU_DEVICES")) {
+      const std::vector<int> ids = msm::parse_device_list(e);
+      if (ids.empty()) throw std::runtime_error(std::string("TACHYON_MSM_GPU_DEVICES: malformed device list '") + e + "'");
+      if (ids.size() > 1) multi = std::make_unique<msm::MsmMultiDevice<Curve>>(ids);
+    }
+  }
+  XYZZ<typename Curve::F> run(const void* bases, const void* scalars, size_t n) {
+    return multi ? multi->run(bases, scalars, n) : impl.run(bases, scalars, n);
   }
 };
 
@@ -116,7 +128,7 @@ void print_hex(const Fp2<B>& x) {
 template <class Curve, class CJac>
 CJac* do_msm(MsmCtx<Curve>* ctx, const void* bases, const void* scalars, size_t n) {
   using F = typename Curve::F;
-  XYZZ<F> r = ctx->impl.run(bases, scalars, n);
+  XYZZ<F> r = ctx->run(bases, scalars, n);
   Affine<F> a = r.to_affine();
   Jacobian<F> j = a.is_zero() ? Jacobian<F>::zero() : Jacobian<F>{a.x, a.y, F::one()};
   static_assert(sizeof(CJac) == sizeof(Jacobian<F>), "layout");
@@ -138,7 +150,7 @@ template <class Curve>
 void msm_affine_out(void* ctx, const void* bases, const void* scalars, size_t n, void* out) {
   using F = typename Curve::F;
   auto* c = static_cast<MsmCtx<Curve>*>(ctx);
-  Affine<F> a = c->impl.run(bases, scalars, n).to_affine();
+  Affine<F> a = c->run(bases, scalars, n).to_affine();
   memcpy(out, &a, sizeof(a));
 }
 
@@ -160,7 +172,7 @@ template <class Curve>
 void msm_form_out(void* ctx, const void* bases, const void* scalars, size_t n, int form, void* out) {
   using F = typename Curve::F;
   auto* c = static_cast<MsmCtx<Curve>*>(ctx);
-  const Affine<F> a = c->impl.run(bases, scalars, n).to_affine();
+  const Affine<F> a = c->run(bases, scalars, n).to_affine();
   switch (form) {
     case 0:
       memcpy(out, &a, sizeof(a));
@@ -364,7 +376,41 @@ int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void* bases, size_t b
   return 1;
 }
 void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c) {
-  GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_force_window_bits(c)) GUARD_END
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    auto* m = static_cast<MsmCtx<C>*>(ctx);
+    m->impl.set_force_window_bits(c);
+    if (m->multi) m->multi->set_force_window_bits(c);
+  }) GUARD_END
+}
+int tachyon_mi355x_msm_gpu_set_devices(int curve, void* ctx, const int* device_ids, size_t count) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  for (size_t i = 0; i < count; ++i)
+    if (device_ids[i] < 0 || device_ids[i] >= n) return 0;  // refused, nothing changed
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    auto* m = static_cast<MsmCtx<C>*>(ctx);
+    m->multi.reset();
+    if (count > 1)
+      m->multi = std::make_unique<msm::MsmMultiDevice<C>>(std::vector<int>(device_ids, device_ids + count));
+  }) GUARD_END
+  return 1;
+}
+size_t tachyon_mi355x_msm_gpu_last_shards(int curve, const void* ctx, float* shard_ms, size_t* shard_points,
+                                          int* shard_devices, size_t cap) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    auto* m = static_cast<const MsmCtx<C>*>(ctx);
+    if (!m->multi) return 0;
+    const auto& ms = m->multi->last_shard_ms();
+    const auto& np = m->multi->last_shard_points();
+    const auto ids = m->multi->device_ids();
+    for (size_t i = 0; i < ids.size() && i < cap; ++i) {
+      if (shard_ms) shard_ms[i] = i < ms.size() ? ms[i] : 0.f;
+      if (shard_points) shard_points[i] = i < np.size() ? np[i] : 0;
+      if (shard_devices) shard_devices[i] = ids[i];
+    }
+    return ids.size();
+  }) GUARD_END
+  return 0;
 }
 void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on) {
   GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_profile(on != 0)) GUARD_END
@@ -380,6 +426,10 @@ void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8
     out8[0] = t.h2d; out8[1] = t.recode; out8[2] = t.sort; out8[3] = t.prep; out8[4] = t.acc; out8[5] = t.reduce;
     out8[6] = t.total; out8[7] = t.acc_launches;
   }) GUARD_END
+}
+unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.last_schedule()) GUARD_END
+  return 0;
 }
 size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx) {
   GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.last_divisions()) GUARD_END

@@ -53,16 +53,6 @@
 #ifndef TA_FQ2_FUSED_MUL
 #define TA_FQ2_FUSED_MUL 1
 #endif
-// BLS12-381 Fq2 products as two fused register-argument calls (48 words in)
-#ifndef TA_CALL_FUSED_MUL
-#define TA_CALL_FUSED_MUL 0
-#endif
-// the 12-limb fused a b - c d as one register-argument call (48 words in)
-// for BLS12-381 Fq2: off -- measured neutral (2^22 52.2 vs 52.1 ms) with 30
-// more VGPR spills at the G2 kernel's 2-wave cap
-#ifndef TA_CALL_MULSUB
-#define TA_CALL_MULSUB 0
-#endif
 
 namespace tachyon_amd {
 
@@ -523,7 +513,10 @@ struct Fp2 {
     // products -- a0 b0 - a1 b1 and a0 b1 + a1 b0, two reductions instead of
     // Karatsuba's three and no Karatsuba sums/differences (the same 384
     // v_mad_u64_u32)
-    if constexpr (F::kLazy && F::kExtInline && (F::N == 8 || TA_CALL_FUSED_MUL))
+    // (BLS12-381 Fq2 keeps Karatsuba: the same pair as two register-argument
+    // calls with 48 words in each spilled at the G2 kernel's 2-wave cap, 2^22
+    // 52.2 -> 54.8 ms)
+    if constexpr (F::kLazy && F::kExtInline && F::N == 8)
       return {c0.mul_sub(o.c0, c1, o.c1), c0.mul_add_inline(o.c1, c1, o.c0)};
 #endif
     F v0 = c0 * o.c0;
@@ -531,13 +524,15 @@ struct Fp2 {
     F m = (c0 + c1) * (o.c0 + o.c1);
     return {v0 - v1, m - v0 - v1};
   }
-  // a b - c d: over the inline 8-limb base field (BN254 Fq2; BLS12-381 Fq2
-  // with TA_CALL_MULSUB) each Karatsuba term pairs with its counterpart in
-  // one fused base product (three reductions instead of six; BN254 G2 2^22
-  // 22.1 -> 21.5 ms); otherwise two products and a subtraction
+  // a b - c d: over the inline 8-limb base field (BN254 Fq2) each Karatsuba
+  // term pairs with its counterpart in one fused base product (three
+  // reductions instead of six; BN254 G2 2^22 22.1 -> 21.5 ms); otherwise two
+  // products and a subtraction (BLS12-381 Fq2: the 12-limb fused product as
+  // a register-argument call measured neutral, 2^22 52.2 vs 52.1 ms, with 30
+  // more VGPR spills at the 2-wave cap)
   TA_HD Fp2 mul_sub(const Fp2& b, const Fp2& c, const Fp2& d) const {
 #if TA_FQ2_MULSUB
-    if constexpr (F::kLazy && F::kExtInline && (F::N == 8 || TA_CALL_MULSUB)) {
+    if constexpr (F::kLazy && F::kExtInline && F::N == 8) {
       const F u0 = c0.mul_sub(b.c0, c.c0, d.c0);
       const F u1 = c1.mul_sub(b.c1, c.c1, d.c1);
       const F um = (c0 + c1).mul_sub(b.c0 + b.c1, c.c0 + c.c1, d.c0 + d.c1);
@@ -601,16 +596,6 @@ __device__ __noinline__ F mul_in_regs(TA_LIMBS12(a), TA_LIMBS12(b)) {
   return x.mul_inline(y);
 }
 template <class F>
-__device__ __noinline__ F mul_sub_in_regs(TA_LIMBS12(a), TA_LIMBS12(b), TA_LIMBS12(c), TA_LIMBS12(d)) {
-  const F x{TA_UNPACK12(a)}, y{TA_UNPACK12(b)}, z{TA_UNPACK12(c)}, w{TA_UNPACK12(d)};
-  return x.mul_sub_inline(y, z, w);
-}
-template <class F>
-__device__ __noinline__ F mul_add_in_regs(TA_LIMBS12(a), TA_LIMBS12(b), TA_LIMBS12(c), TA_LIMBS12(d)) {
-  const F x{TA_UNPACK12(a)}, y{TA_UNPACK12(b)}, z{TA_UNPACK12(c)}, w{TA_UNPACK12(d)};
-  return x.mul_add_inline(y, z, w);
-}
-template <class F>
 __device__ __noinline__ F sqr_in_regs(TA_LIMBS12(a)) {
   const F x{TA_UNPACK12(a)};
   return x.sqr_inline();
@@ -644,20 +629,7 @@ struct CallFp : F {
     return F::sqr_inline();
 #endif
   }
-  TA_HD CallFp mul_sub(const CallFp& b, const CallFp& c, const CallFp& d) const {
-#if defined(__HIP_DEVICE_COMPILE__) && TA_CALL_MULSUB
-    return detail::mul_sub_in_regs<F>(TA_PASS12((*this)), TA_PASS12(b), TA_PASS12(c), TA_PASS12(d));
-#else
-    return (*this) * b - c * d;
-#endif
-  }
-  TA_HD CallFp mul_add_inline(const CallFp& b, const CallFp& c, const CallFp& d) const {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return detail::mul_add_in_regs<F>(TA_PASS12((*this)), TA_PASS12(b), TA_PASS12(c), TA_PASS12(d));
-#else
-    return F::mul_add_inline(b, c, d);
-#endif
-  }
+  TA_HD CallFp mul_sub(const CallFp& b, const CallFp& c, const CallFp& d) const { return (*this) * b - c * d; }
   TA_HD CallFp inverse() const { return F::inverse(); }
   TA_HD CallFp cond_neg_canonical(bool neg) const { return F::cond_neg_canonical(neg); }
   TA_HD CallFp canonical() const { return F::canonical(); }

@@ -29,6 +29,10 @@ namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
 constexpr int kMsmVariantMask = 0xFBF;
+// schedule of the last run (last_schedule()): the recode fused with the first
+// radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
+// staging in the recode scatter
+constexpr unsigned kSchedFusedRecode = 1, kSchedRecodeFedSort = 2, kSchedNarrowStaging = 4;
 
 struct MsmPlan {
   unsigned c = 0;        // window bits
@@ -106,8 +110,10 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, u
   unsigned seg = 2;
   while (seg < 64 && ((nb / (seg * 2)) >= 49152)) seg *= 2;
   p.seg = std::min<unsigned>(p.buckets, seg);
-  if (const char* e = getenv("TACHYON_MSM_SEG"); e && atoi(e) > 0)  // A/B override
+#ifdef TACHYON_TUNING_KNOBS
+  if (const char* e = getenv("TACHYON_MSM_SEG"); e && atoi(e) > 0)  // A/B override (tuning builds only)
     p.seg = std::clamp<unsigned>(atoi(e), 2, p.buckets);
+#endif
   return p;
 }
 
@@ -164,6 +170,7 @@ class MsmGpu {
   // number of point chunks the last run() was split into for device memory
   // (DetermineMsmDivisionsForMemory) or for the host-upload pipeline
   size_t last_divisions() const { return last_divisions_; }
+  unsigned last_schedule() const { return last_schedule_; }  // kSched* bits of the last run
 
  private:
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
@@ -193,7 +200,7 @@ class MsmGpu {
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode
-  bool scatter_lds_set_ = false;
+  bool scatter_lds_set_[2] = {false, false};  // 128 KiB dynamic LDS allowed: wide / narrow scatter
   const void* pending_host_bases_ = nullptr;  // host bases still to upload (see enqueue)
   hipStream_t copy_stream_ = nullptr;
   hipEvent_t copy_done_ = nullptr;
@@ -203,6 +210,7 @@ class MsmGpu {
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;
   size_t last_divisions_ = 1;
+  unsigned last_schedule_ = 0;
   unsigned range_begin_ = 0, range_end_ = ~0u;  // window range of the next run_windows
 };
 

@@ -717,6 +717,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // otherwise (set_variant bit 10, or other tile shapes, or > 2 places)
   const unsigned places = (key_bits - sort_begin + 7) / 8;
   const bool own_sort = fused && !rocprim_hist_ && places <= 2 && entries < (size_t(1) << 32);
+  last_schedule_ = (fused ? kSchedFusedRecode : 0u) | (own_sort ? kSchedRecodeFedSort : 0u) |
+                   (fused && narrow ? kSchedNarrowStaging : 0u);
   uint32_t* digit_off = nullptr;
 
   if (profile_) TA_HIP(hipEventRecord(ev_[1], stream_));
@@ -747,12 +749,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     // the scattered entries are fully sorted when the key has <= 8 bits; the
     // own onesweep passes ping-pong from the scatter's output and end in ents2
     uint64_t* dst = own_sort ? (places % 2 == 0 ? ents2 : ents) : (sort_begin < key_bits ? ents : ents2);
-    if (!narrow && scatter_lds > 64 * 1024 && !scatter_lds_set_) {
-      TA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&recode_scatter_kernel<Fr, false>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
-      scatter_lds_set_ = true;
-    }
     auto* scatter = narrow ? &recode_scatter_kernel<Fr, true> : &recode_scatter_kernel<Fr, false>;
+    // dynamic LDS above 64 KiB: raise the launched instance's limit once (per instantiation)
+    if (scatter_lds > 64 * 1024 && !scatter_lds_set_[narrow ? 1 : 0]) {
+      TA_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(scatter), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 128 * 1024));
+      scatter_lds_set_[narrow ? 1 : 0] = true;
+    }
     hipLaunchKernelGGL(scatter, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars, (uint32_t)n, c, Wt, wr0,
                        W, nblocks, spt, hist, hoff, dst);
   } else {
@@ -1171,11 +1174,36 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_window_range(const void* bases,
   last_divisions_ = 1;
   std::vector<Point> ws;
   MsmPlan plan;
-  run_windows(bases, scalars, n, &ws, &plan);
-  if (n == 0 || plan.active() == 0) return Point::zero();
-  Point p = combine_windows(ws, plan.c);
-  for (unsigned k = 0; k < plan.c * plan.w_begin; ++k) p = p.dbl();
-  return p;
+  // the window range of every point chunk run() would use for memory
+  // (DetermineMsmDivisionsForMemory), partials added; host inputs stay on the
+  // host and each chunk uploads its own slice (counted as resident: a
+  // conservative bound).  The window bits must not depend on the chunk size,
+  // so the whole input's plan is forced on the chunks.
+  if (n == 0) {
+    run_windows(bases, scalars, 0, &ws, &plan);
+    return Point::zero();
+  }
+  const size_t resident = (is_device_pointer(bases) ? 0 : n * sizeof(Aff)) +
+                          (is_device_pointer(scalars) ? 0 : n * sizeof(Fr));
+  const size_t divisions = memory_divisions(n, resident);
+  struct RestoreC {
+    MsmGpu* m;
+    unsigned c;
+    ~RestoreC() { m->force_c_ = c; }
+  } restore_c{this, force_c_};
+  if (divisions > 1 && !force_c_) force_c_ = MsmPlan::make(n, Fr::Config::kModulusBits).c;
+  last_divisions_ = divisions;
+  const size_t step = (n + divisions - 1) / divisions;
+  Point total = Point::zero();
+  for (size_t lo = 0; lo < n; lo += step) {
+    const size_t len = std::min(step, n - lo);
+    run_windows(static_cast<const Aff*>(bases) + lo, static_cast<const Fr*>(scalars) + lo, len, &ws, &plan);
+    if (plan.active() == 0) return Point::zero();
+    Point p = combine_windows(ws, plan.c);
+    for (unsigned k = 0; k < plan.c * plan.w_begin; ++k) p = p.dbl();
+    total = total + p;
+  }
+  return total;
 }
 
 }  // namespace tachyon_amd::msm

@@ -353,9 +353,12 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
   offset_ = Fr::one();
   offset_inv_ = Fr::one();
 
-  // elements per workgroup (LDS footprint); TACHYON_NTT_LDS_ELEMS overrides for A/B runs
+  // elements per workgroup (LDS footprint); TACHYON_NTT_LDS_ELEMS overrides it
+  // in tuning builds only (-DTACHYON_TUNING_KNOBS, tools/tune_ntt.py)
   uint32_t lds_elems = kMaxLdsElems;
+#ifdef TACHYON_TUNING_KNOBS
   if (const char* e = getenv("TACHYON_NTT_LDS_ELEMS")) lds_elems = std::clamp<uint32_t>(atoi(e), 256, 2048);
+#endif
   // pass plan: ceil(L / 8) passes, stages split evenly
   if (log_n_ > 0) {
     uint32_t P = (log_n_ + kMaxPassStages - 1) / kMaxPassStages;
@@ -375,11 +378,13 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
     }
   }
   pow_bits_ = (log_n_ + 1) / 2;
-  // stages per register step (1 = radix-2 through LDS every stage); the
-  // TACHYON_NTT_RADIX_LOG override is for A/B measurements
+  // stages per register step (1 = radix-2 through LDS every stage) and the
+  // other schedule overrides: A/B measurements in tuning builds only
+#ifdef TACHYON_TUNING_KNOBS
   if (const char* e = getenv("TACHYON_NTT_RADIX_LOG")) radix_ = std::clamp(atoi(e), 1, 3);
   if (const char* e = getenv("TACHYON_NTT_SHOUP")) shoup_mode_ = std::clamp(atoi(e), 0, 2);
-  if (const char* e = getenv("TACHYON_NTT_VARIANT")) ntt_variant_ = atoi(e);
+  if (const char* e = getenv("TACHYON_NTT_VARIANT")) ntt_variant_ = std::clamp(atoi(e), 0, 3);
+#endif
   ev_.resize(plan_.size() + 1);
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
   build_twiddles();
@@ -517,6 +522,7 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
     // (A/B, TACHYON_NTT_VARIANT: bit 0 = the Montgomery radix-4 pass at >= 5
     // waves/SIMD, bit 1 = the Shoup radix-4 passes without the twiddle
     // prefetch at >= 5 waves/SIMD)
+#ifdef TACHYON_TUNING_KNOBS
     if (shoup) {
       auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Tw, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Tw, 2>
                                                                          : dif_pass_kernel<Fr, Tw, 3>;
@@ -528,6 +534,15 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
       if (radix_ == 2 && (ntt_variant_ & 1)) kern = dif_pass_kernel<Fr, Fr, 2, true, 5>;
       hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, twm, a);
     }
+#else
+    // release schedule: radix-4 register steps (2 DIF stages per LDS round trip)
+    if (shoup)
+      hipLaunchKernelGGL((dif_pass_kernel<Fr, Tw, 2>), dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src,
+                         dst, tw, a);
+    else
+      hipLaunchKernelGGL((dif_pass_kernel<Fr, Fr, 2>), dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src,
+                         dst, twm, a);
+#endif
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(ev_[p + 1], stream_));
   }

@@ -92,10 +92,14 @@ def window_split_msm(curve: str, msm, bases, scalars, n: int, c: int, group=None
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if world > 1 else 0
-    msm.set_window_bits(c)
     windows = _windows_for(curve, c)
     w0, w1 = window_range(windows, rank, world)
-    part = msm.run_window_range(bases, scalars, w0, w1, n)
+    prev = getattr(msm, "window_bits", 0)
+    msm.set_window_bits(c)
+    try:
+        part = msm.run_window_range(bases, scalars, w0, w1, n)
+    finally:  # the caller's context keeps its own window choice
+        msm.set_window_bits(prev)
     if world == 1:
         return part
     return combine_partials(curve, all_gather_partials(curve, part, group, device))

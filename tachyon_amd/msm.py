@@ -47,6 +47,7 @@ class VariableBaseMSMGpu:
             raise ValueError(f"unknown curve {curve}")
         self.curve = curve
         self.curve_id = CURVES[curve]
+        self.window_bits = 0  # forced window bits (set_window_bits), 0 = the size's default
         self.point_bytes, self.scalar_field = CURVE_INFO[curve]
         self.scalar_bytes = FIELD_BYTES[self.scalar_field]
         create, self._destroy, self._affine_msm = _CREATE[curve]
@@ -104,7 +105,9 @@ class VariableBaseMSMGpu:
         return data
 
     def set_window_bits(self, c: int):
+        """Force the window bits of later runs (0 = the size's default)."""
         lib().tachyon_mi355x_msm_gpu_set_window_bits(self.curve_id, self._ctx, c)
+        self.window_bits = c
 
     def set_profile(self, on: bool):
         lib().tachyon_mi355x_msm_gpu_set_profile(self.curve_id, self._ctx, 1 if on else 0)
@@ -112,6 +115,28 @@ class VariableBaseMSMGpu:
     def set_variant(self, variant: int):
         if not lib().tachyon_mi355x_msm_gpu_set_variant(self.curve_id, self._ctx, variant):
             raise ValueError(f"unknown MSM variant bits in {variant:#x}")
+
+    def set_devices(self, device_ids):
+        """Shard every later MSM over these devices (one point chunk per entry,
+        ids may repeat; [] or one id = single device), results added on the
+        host -- tachyon_mi355x_msm_gpu_set_devices."""
+        ids = list(device_ids)
+        arr = (ctypes.c_int * max(1, len(ids)))(*ids)
+        if not lib().tachyon_mi355x_msm_gpu_set_devices(self.curve_id, self._ctx, arr, len(ids)):
+            raise ValueError(f"device ids out of range: {ids}")
+
+    def last_shards(self) -> list:
+        """[(device, points, wall ms)] of the last multi-device run ([] if single device)."""
+        cap = 64
+        ms, pts, dev = (ctypes.c_float * cap)(), (ctypes.c_size_t * cap)(), (ctypes.c_int * cap)()
+        k = lib().tachyon_mi355x_msm_gpu_last_shards(self.curve_id, self._ctx, ms, pts, dev, cap)
+        return [(dev[i], pts[i], ms[i]) for i in range(min(k, cap))]
+
+    def last_schedule(self) -> dict:
+        """Schedule of the last run: fused recode + first radix pass, recode-fed
+        onesweep passes, 7-byte LDS staging (tachyon_mi355x_msm_gpu_last_schedule)."""
+        b = lib().tachyon_mi355x_msm_gpu_last_schedule(self.curve_id, self._ctx)
+        return {"fused_recode": bool(b & 1), "recode_fed_sort": bool(b & 2), "narrow_staging": bool(b & 4)}
 
     def last_divisions(self) -> int:
         """Point chunks the last run was split into (device memory or host-upload pipeline)."""

@@ -215,6 +215,18 @@ def test_memory_divisions(monkeypatch):
     monkeypatch.setenv("TACHYON_MSM_MEM_LIMIT", str(200 << 20))
     assert m.run(d_b.cpu().numpy(), d_s.cpu().numpy()) == whole
     assert m.last_divisions() >= 2
+    # a window-range MSM divides the same way (its chunks keep the whole input's
+    # window bits): the ranges of a 2-way window split still add up to the MSM
+    from tachyon_amd import dist as D
+    c, W = M.plan("bn254_g1", n)
+    parts = []
+    for w0, w1 in (D.window_range(W, 0, 2), D.window_range(W, 1, 2)):
+        parts.append(m.run_window_range(d_b, d_s, w0, w1))
+        assert m.last_divisions() >= 2
+    assert M.affine_sum("bn254_g1", b"".join(parts)) == whole
+    parts = [m.run_window_range(d_b.cpu().numpy(), d_s.cpu().numpy(), w0, w1)
+             for w0, w1 in (D.window_range(W, 0, 2), D.window_range(W, 1, 2))]
+    assert M.affine_sum("bn254_g1", b"".join(parts)) == whole
     m.close()
 
 
@@ -248,22 +260,30 @@ def test_window_ranges_tile_the_msm(curve):
     m.close()
 
 
-@pytest.mark.parametrize("curve", ["bn254_g1", "bls12_381_g2"])
-def test_msm_schedule_variants_agree(curve):
+@pytest.mark.parametrize("curve,logn", [("bn254_g1", 16), ("bn254_g1", 18), ("bls12_381_g2", 16)])
+def test_msm_schedule_variants_agree(curve, logn):
     """Every accepted set_variant schedule computes the same point: the separate
     recode + full sort (bit 7), rocPRIM's own digit-histogram pass instead of the
     recode's counts (bit 10), 8-byte LDS staging in the recode scatter (bit 11),
     the onesweep tile shapes (bits 4-5) and one window per sort group (bits 2-3);
-    the wrong-result bit 6 and bits above 11 are refused."""
-    n = 1 << 13
+    the wrong-result bit 6 and bits above 11 are refused.  At 2^16 (one onesweep
+    place after the fused low byte) and 2^18 (two places) the default schedule is
+    the fused recode feeding the onesweep passes its digit counts, so bits 10
+    and 11 really switch schedules -- asserted through last_schedule()."""
+    n = 1 << logn
     bases = O.gen_bases(curve, 21, n, 16).tobytes()
     scalars = O.gen_scalars(O.CURVE_INFO[curve][1], 21, n).tobytes()
     expect, _ = O.msm(curve, bases, scalars)
     m = ctx(curve)
+    want = {0: (True, True, True), 128: (False, False, False), 1024: (True, False, True),
+            2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
         for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
+            if v in want:
+                s = m.last_schedule()
+                assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
         for bad in (64, 4096):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
