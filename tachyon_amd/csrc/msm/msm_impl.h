@@ -99,6 +99,34 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 // 32-byte scalars and one write.
 constexpr unsigned kRecodeSpt = 2;  // default scalars per thread of the fused recode
 
+// LDS bin counters with one atomic per wave when every active lane hits the
+// same bin -- NonUniform(n, 1) scalars (variable_base_msm_test_set.h:43-53),
+// small scalars' empty high windows -- instead of 64 serialised atomics on
+// one address (2^26 NonUniform recode 12.8 -> see DESIGN.md); otherwise one
+// atomic per lane.  The test is wave-uniform (ballots), so no divergence.
+__device__ __forceinline__ void lds_count(uint32_t* cnt, uint32_t bin) {
+  const uint32_t b0 = __builtin_amdgcn_readfirstlane(bin);
+  const uint64_t active = __ballot(1);
+  if (__ballot(bin == b0) == active) {
+    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)active) - 1)) atomicAdd(&cnt[b0], (uint32_t)__popcll(active));
+  } else {
+    atomicAdd(&cnt[bin], 1u);
+  }
+}
+// the same for a returning add of 1: this lane's slot in bin's run
+__device__ __forceinline__ uint32_t lds_rank(uint32_t* cur, uint32_t bin) {
+  const uint32_t b0 = __builtin_amdgcn_readfirstlane(bin);
+  const uint64_t active = __ballot(1);
+  if (__ballot(bin == b0) == active) {
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)active) - 1);
+    const uint32_t below = (uint32_t)__popcll(active & ((1ull << __lane_id()) - 1));
+    uint32_t base = 0;
+    if (__lane_id() == leader) base = atomicAdd(&cur[b0], (uint32_t)__popcll(active));
+    return __shfl(base, leader, 64) + below;
+  }
+  return atomicAdd(&cur[bin], 1u);
+}
+
 // Places > 0 (key bits 8..15, 16..23): with `places` > 0 the kernel also
 // counts those digits per block, into later[((p - 1) * nblocks + block) * 256
 // + bin], so the onesweep passes over those places need no histogram pass of
@@ -120,9 +148,9 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
     const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + t;
     if (i < n)
       recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned, uint32_t key, uint32_t) {
-        atomicAdd(&cnt[0][key & 255], 1u);
-        if (places > 0) atomicAdd(&cnt[1][(key >> 8) & 255], 1u);
-        if (places > 1) atomicAdd(&cnt[2][(key >> 16) & 255], 1u);
+        lds_count(cnt[0], key & 255);
+        if (places > 0) lds_count(cnt[1], (key >> 8) & 255);
+        if (places > 1) lds_count(cnt[2], (key >> 16) & 255);
       });
   }
   __syncthreads();
@@ -201,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
     if (i < n)
       recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned, uint32_t key, uint32_t val) {
         const uint32_t bin = key & 255;
-        const uint32_t p = loff[bin] + atomicAdd(&cur[bin], 1u);
+        const uint32_t p = loff[bin] + lds_rank(cur, bin);
         if constexpr (kNarrow) {
           lvals[p] = val;
           lkeys[p] = (uint16_t)(key >> 8);

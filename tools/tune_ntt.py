@@ -2,6 +2,8 @@
 """NTT pass timing (device-resident, HIP events per pass) for A/B runs.
 
   TACHYON_NTT_RADIX_LOG=3 python tools/tune_ntt.py --log-n 20 24
+(the TACHYON_NTT_* overrides exist only in a tuning build of the library:
+ make -C tachyon_amd/csrc EXTRA_CXXFLAGS=-DTACHYON_TUNING_KNOBS)
 Prints per-pass device ms and the per-transform wall time; checks the round trip.
 """
 import argparse
