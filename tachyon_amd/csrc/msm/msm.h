@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0xFBF;
+constexpr int kMsmVariantMask = 0x1FBF;
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter
@@ -42,6 +42,7 @@ struct MsmPlan {
   unsigned K2 = 16;      // fan-in of the partial-reduction levels
   unsigned levels = 0;   // number of K2 levels
   unsigned seg = 0;      // buckets per running-sum segment
+  unsigned seg_tree = 0; // the same for the workgroup-tree window reduction (no fix-up: shorter)
   unsigned group = 0;    // windows per sort/accumulate pipeline stage
   // the windows this run computes, [w_begin, w_end) of the W (default all):
   // a window-range MSM is the sum over those windows of 2^(c w) S_w, so the
@@ -110,6 +111,11 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, u
   unsigned seg = 2;
   while (seg < 64 && ((nb / (seg * 2)) >= 49152)) seg *= 2;
   p.seg = std::min<unsigned>(p.buckets, seg);
+  // workgroup-tree reduction: no per-segment fix-up, so shorter segments (more
+  // threads, shorter serial chains) until ~128 K segment threads
+  unsigned st = 2;
+  while (st < 64 && (nb / (st * 2)) >= 131072) st *= 2;
+  p.seg_tree = std::min<unsigned>(p.buckets, st);
 #ifdef TACHYON_TUNING_KNOBS
   if (const char* e = getenv("TACHYON_MSM_SEG"); e && atoi(e) > 0)  // A/B override (tuning builds only)
     p.seg = std::clamp<unsigned>(atoi(e), 2, p.buckets);
@@ -197,6 +203,7 @@ class MsmGpu {
   unsigned sort_cfg_ = 0;  // onesweep tile shape (set_variant bits 4-5)
   bool rocprim_hist_ = false;  // rocPRIM's digit histogram pass instead of the recode's counts (bit 10)
   bool wide_stage_ = false;    // 8-byte entries in the recode scatter's LDS staging (bit 11)
+  bool tree_reduce_ = false;   // window sums by workgroup trees (bit 12)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode

@@ -564,6 +564,68 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void reduce_uniform
   reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
 }
 
+// Window reduction by workgroup trees (no per-segment (jL)*R fix-up, two
+// launches instead of one per binary-tree level).  Units of a window are
+// segments of L buckets; a node over the units [a, a + s) is
+//   V  = sum_j [A_j + (j - a) L R_j],   Rs = s L sum_j R_j
+// (A_j = sum_k (k + 1) B_{jL+k}, R_j = sum_k B_{jL+k}: the segment's running
+// sums), so the root over all units is the window sum sum_b (b + 1) B_b
+// (PippengerBase::AccumulateBuckets, pippenger_base.h:36-57).  Two adjacent
+// nodes of equal size merge as V = V_l + V_r + Rs_r, Rs = 2 (Rs_l + Rs_r):
+// three point operations per merge, none depending on the position.
+// kLeafBuckets: leaves are segments read from bucket_sum (grid (groups, W));
+// otherwise leaves are the nodes of the previous launch (`nodes_in`, `units`
+// per window).  Each workgroup writes the node over its kWinBlock leaves
+// (padding leaves are (0, 0): units past the end hold no buckets).
+constexpr unsigned kWinBlock = 256;
+template <class Curve, bool kLeafBuckets>
+__global__ __launch_bounds__(kWinBlock, AccWaves<Curve>::value) void window_tree_kernel(
+    const XYZZ<typename Curve::F>* __restrict__ bucket_sum, unsigned B, unsigned L, unsigned log_l,
+    const XYZZ<typename Curve::F>* __restrict__ nodes_in, unsigned units, XYZZ<typename Curve::F>* __restrict__ nodes_out) {
+  using F = typename HotOf<typename Curve::F>::type;
+  using P = XYZZ<F>;
+  extern __shared__ uint64_t win_lds[];
+  P* lv = reinterpret_cast<P*>(win_lds);           // kWinBlock / 2 right-node V
+  P* lr = lv + kWinBlock / 2;                      // and Rs
+  const unsigned t = threadIdx.x, w = blockIdx.y;
+  const unsigned u = blockIdx.x * kWinBlock + t;   // this thread's leaf unit
+  P V = P::zero(), Rs = P::zero();
+  if (u < units) {
+    if constexpr (kLeafBuckets) {
+      const P* bs = reinterpret_cast<const P*>(bucket_sum) + (size_t)w * B + (size_t)u * L;
+      for (int k = (int)L - 1; k >= 0; --k) {
+        Rs = Rs + bs[k];
+        V = V + Rs;
+      }
+      for (unsigned k = 0; k < log_l; ++k) Rs = Rs.dbl();  // L R
+    } else {
+      const P* in = reinterpret_cast<const P*>(nodes_in) + 2 * ((size_t)w * units + u);
+      V = in[0];
+      Rs = in[1];
+    }
+  }
+  for (unsigned k = 0; (1u << k) < kWinBlock; ++k) {
+    const unsigned span = 1u << k;
+    if ((t & (2 * span - 1)) == span) {  // a right node: hand it to its left neighbour
+      lv[t >> (k + 1)] = V;
+      lr[t >> (k + 1)] = Rs;
+    }
+    __syncthreads();
+    if ((t & (2 * span - 1)) == 0) {
+      const P rv = lv[t >> (k + 1)], rr = lr[t >> (k + 1)];
+      V = V + rv + rr;
+      Rs = (Rs + rr).dbl();
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const unsigned groups = gridDim.x;
+    P* o = reinterpret_cast<P*>(nodes_out) + 2 * ((size_t)w * groups + blockIdx.x);
+    o[0] = V;
+    o[1] = Rs;
+  }
+}
+
 inline unsigned grid_for(size_t threads) { return (unsigned)std::max<size_t>(1, (threads + kBlock - 1) / kBlock); }
 
 }  // namespace
@@ -909,6 +971,34 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   }
 
   // ---- window sums ----
+  if (tree_reduce_) {
+    // segments of L buckets, workgroup trees of kWinBlock nodes, launches until one node per window
+    unsigned L = plan.seg_tree, log_l = 0;
+    while ((1u << log_l) < L) ++log_l;
+    unsigned units = B / L;
+    unsigned groups = (units + kWinBlock - 1) / kWinBlock;
+    const size_t lds = (size_t)kWinBlock * sizeof(Point);  // kWinBlock / 2 (V, Rs) pairs
+    Point* na = static_cast<Point*>(seg_a_.ensure((size_t)W * groups * 2 * sizeof(Point)));
+    Point* nb_ = static_cast<Point*>(seg_b_.ensure((size_t)W * ((groups + kWinBlock - 1) / kWinBlock) * 2 * sizeof(Point)));
+    hipLaunchKernelGGL((window_tree_kernel<Curve, true>), dim3(groups, W), dim3(kWinBlock), lds, stream_, bucket_sum, B,
+                       L, log_l, nullptr, units, na);
+    TA_HIP(hipGetLastError());
+    Point* cur_n = na;
+    Point* nxt_n = nb_;
+    while (groups > 1) {
+      units = groups;
+      groups = (units + kWinBlock - 1) / kWinBlock;
+      hipLaunchKernelGGL((window_tree_kernel<Curve, false>), dim3(groups, W), dim3(kWinBlock), lds, stream_, nullptr,
+                         B, L, log_l, cur_n, units, nxt_n);
+      TA_HIP(hipGetLastError());
+      std::swap(cur_n, nxt_n);
+    }
+    // the root V of every window: node pairs (V, Rs), stride 2
+    TA_HIP(hipMemcpy2DAsync(d_windows, sizeof(Point), cur_n, 2 * sizeof(Point), sizeof(Point), W,
+                            hipMemcpyDeviceToDevice, stream_));
+    if (profile_) TA_HIP(hipEventRecord(ev_[5], stream_));
+    return;
+  }
   unsigned S = B / plan.seg;
   Point* seg_a = static_cast<Point*>(seg_a_.ensure((size_t)W * S * sizeof(Point)));
   Point* seg_b = static_cast<Point*>(seg_b_.ensure((size_t)W * S * sizeof(Point)));
@@ -959,6 +1049,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   sort_cfg_ = (variant_ >> 4) & 3;  // bits 4-5: onesweep tile shape
   rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
   wide_stage_ = (variant_ & 2048) != 0;    // bit 11: 8-byte LDS staging in the recode scatter (A/B)
+  tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;

@@ -102,11 +102,14 @@ def test_msm_window_sizes_agree():
     expect, _ = O.msm("bn254_g1", bases, scalars)
     m = ctx("bn254_g1")
     try:
-        for c in (4, 7, 11, 16, 21):
-            m.set_window_bits(c)
-            assert m.run(bases, scalars) == expect, c
+        for var in (0, 4096):  # per-segment fix-up / workgroup-tree window reduction
+            m.set_variant(var)
+            for c in (4, 7, 11, 16, 21):
+                m.set_window_bits(c)
+                assert m.run(bases, scalars) == expect, (c, var)
     finally:
         m.set_window_bits(0)
+        m.set_variant(0)
 
 
 def test_msm_empty_and_single():
@@ -278,13 +281,13 @@ def test_msm_schedule_variants_agree(curve, logn):
     want = {0: (True, True, True), 128: (False, False, False), 1024: (True, False, True),
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
-        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256):
+        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
                 s = m.last_schedule()
                 assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
-        for bad in (64, 4096):
+        for bad in (64, 8192):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
