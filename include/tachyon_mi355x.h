@@ -471,6 +471,14 @@ TACHYON_C_EXPORT int tachyon_mi355x_kzg_downsize(tachyon_mi355x_kzg* kzg, size_t
 TACHYON_C_EXPORT void tachyon_mi355x_kzg_get_srs(const tachyon_mi355x_kzg* kzg, int lagrange, void* out);
 TACHYON_C_EXPORT int tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* kzg, int lagrange, const void* scalars,
                                                size_t len, void* out_affine);
+/* Batch commitments (ResizeBatchCommitments / Commit(v, state, index) /
+ * GetBatchCommitments, kzg.h:116-165,296-307): `count` polynomials,
+ * scalars[i] of lens[i] elements (host or device), their commitments written
+ * affine to out_affine[i], normalised together with one field inversion
+ * (BatchNormalize).  Returns 1, or 0 (nothing written) when any lens[i] > N. */
+TACHYON_C_EXPORT int tachyon_mi355x_kzg_commit_batch(tachyon_mi355x_kzg* kzg, int lagrange,
+                                                     const void* const* scalars, const size_t* lens, size_t count,
+                                                     void* out_affine);
 
 /* delete a Jacobian returned by an *_msm / *_msm_gpu entry point (for callers
  * that cannot use C++ delete, e.g. ctypes). */

@@ -152,6 +152,8 @@ SIGNATURES = [
     ("tachyon_mi355x_kzg_downsize", i32, [vp, sz]),
     ("tachyon_mi355x_kzg_get_srs", None, [vp, i32, vp]),
     ("tachyon_mi355x_kzg_commit", i32, [vp, i32, vp, sz, vp]),
+    ("tachyon_mi355x_kzg_commit_batch", i32, [vp, i32, ctypes.POINTER(ctypes.c_void_p),
+                                              ctypes.POINTER(ctypes.c_size_t), sz, vp]),
     ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
     ("tachyon_mi355x_version", ctypes.c_char_p, []),
     ("tachyon_mi355x_device_count", i32, []),

@@ -95,4 +95,17 @@ int tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* p, int lagrange, const void* s
   GUARD_END
 }
 
+int tachyon_mi355x_kzg_commit_batch(tachyon_mi355x_kzg* p, int lagrange, const void* const* scalars,
+                                    const size_t* lens, size_t count, void* out_affine) {
+  GUARD_BEGIN
+  KZG_DISPATCH(p, {
+    using K = std::remove_pointer_t<decltype(impl)>;
+    return impl->commit_batch(reinterpret_cast<const typename K::Fr* const*>(scalars), lens, count, lagrange != 0,
+                              static_cast<typename K::Aff*>(out_affine))
+               ? 1
+               : 0;
+  });
+  GUARD_END
+}
+
 }  // extern "C"

@@ -43,6 +43,12 @@ class Kzg {
   // to min(|bases|, |scalars|) and PippengerAdapter then refuses unequal
   // sizes, so Commit / CommitLagrange return false, kzg.h:217-258,267-290).
   bool commit(const Fr* scalars, size_t len, bool lagrange, Aff* out);
+  // Batch mode (ResizeBatchCommitments / Commit(v, state, index) /
+  // GetBatchCommitments, kzg.h:116-165,296-307): one MSM per polynomial, the
+  // results kept projective (XYZZ) and normalised together with ONE field
+  // inversion (BatchNormalize's Montgomery trick, projective_point.h).  False,
+  // with out untouched, when any len > N.
+  bool commit_batch(const Fr* const* scalars, const size_t* lens, size_t count, bool lagrange, Aff* out);
 
   const Aff* d_srs(bool lagrange) const { return lagrange ? lagrange_.as<Aff>() : powers_.as<Aff>(); }
   void copy_srs(bool lagrange, Aff* host_out) const;

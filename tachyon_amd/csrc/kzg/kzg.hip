@@ -142,6 +142,42 @@ bool Kzg<Curve>::commit(const Fr* scalars, size_t len, bool lagrange, Aff* out) 
   return true;
 }
 
+// XYZZ -> affine for a whole batch with one inversion: x = X / ZZ = X (ZZZ^-1 ZZ)^2,
+// y = Y / ZZZ (point_xyzz.h:199-212), the ZZZ inverted together by
+// Montgomery's trick (prefix products, one inverse, backward pass); identity
+// points (zz = 0) stay (0, 0).
+template <class F>
+void batch_to_affine(const std::vector<XYZZ<F>>& pts, Affine<F>* out) {
+  const size_t m = pts.size();
+  std::vector<F> prefix(m);
+  F acc = F::one();
+  for (size_t i = 0; i < m; ++i) {
+    if (!pts[i].is_zero()) acc = acc * pts[i].zzz;
+    prefix[i] = acc;
+  }
+  F inv = acc.inverse();  // product of the non-identity ZZZ: invertible
+  for (size_t i = m; i-- > 0;) {
+    if (pts[i].is_zero()) {
+      out[i] = Affine<F>::zero();
+      continue;
+    }
+    const F zinv3 = i > 0 ? inv * prefix[i - 1] : inv;  // 1 / ZZZ_i
+    inv = inv * pts[i].zzz;
+    const F zinv2 = (zinv3 * pts[i].zz).sqr();
+    out[i] = Affine<F>{pts[i].x * zinv2, pts[i].y * zinv3}.canonical();
+  }
+}
+
+template <class Curve>
+bool Kzg<Curve>::commit_batch(const Fr* const* scalars, const size_t* lens, size_t count, bool lagrange, Aff* out) {
+  for (size_t i = 0; i < count; ++i)
+    if (lens[i] > n_) return false;
+  std::vector<XYZZ<F>> pts(count);
+  for (size_t i = 0; i < count; ++i) pts[i] = msm_->run(d_srs(lagrange), scalars[i], lens[i]);
+  batch_to_affine(pts, out);
+  return true;
+}
+
 template <class Curve>
 void Kzg<Curve>::copy_srs(bool lagrange, Aff* host_out) const {
   TA_HIP(hipMemcpy(host_out, d_srs(lagrange), n_ * sizeof(Aff), hipMemcpyDeviceToHost));

@@ -77,7 +77,19 @@ class KZG:
         or None when |evals| > N (kzg.h:239-248)."""
         return self._commit(evals, True)
 
-    def commit_batch(self, polys, lagrange: bool = False) -> list:
-        """Batch mode: one commitment per polynomial, returned together
-        (BatchCommitmentState + GetBatchCommitments)."""
-        return [self._commit(p, lagrange) for p in polys]
+    def commit_batch(self, polys, lagrange: bool = False):
+        """Batch mode (ResizeBatchCommitments + Commit(v, state, i) +
+        GetBatchCommitments, kzg.h:116-165): one MSM per polynomial, the
+        commitments normalised together with one inversion
+        (tachyon_mi355x_kzg_commit_batch).  A list of affine bytes, or None
+        when any polynomial has more than N elements."""
+        if not polys:
+            return []
+        ptrs = [_ptr(p) for p in polys]
+        arr = (ctypes.c_void_p * len(ptrs))(*[p for p, _, _ in ptrs])
+        lens = (ctypes.c_size_t * len(ptrs))(*[nb // 32 for _, nb, _ in ptrs])
+        out = ctypes.create_string_buffer(len(ptrs) * self.point_bytes)
+        if not lib().tachyon_mi355x_kzg_commit_batch(self._h, 1 if lagrange else 0, arr, lens, len(ptrs), out):
+            return None
+        pb = self.point_bytes
+        return [out.raw[i * pb:(i + 1) * pb] for i in range(len(ptrs))]

@@ -64,6 +64,13 @@ def test_batch_and_downsize():
     batch = kzg.commit_batch(polys)
     lag = kzg.commit_batch([O.fft(p, n) for p in polys], lagrange=True)
     assert batch == lag == [kzg.commit(p) for p in polys]
+    # ragged batch incl. an empty polynomial and a zero polynomial (identity
+    # commitments stay (0, 0) through the one-inversion normalisation)
+    ragged = [polys[0][:32 * 3], b"", bytes(32 * n), polys[1]]
+    assert kzg.commit_batch(ragged) == [kzg.commit(p) if p else bytes(64) for p in ragged]
+    assert kzg.commit_batch(ragged)[1] == bytes(64) and kzg.commit_batch(ragged)[2] == bytes(64)
+    assert kzg.commit_batch([polys[0] + polys[0][:32]]) is None  # more than N: nothing written
+    assert kzg.commit_batch([]) == []
     assert not kzg.downsize(n)
     assert kzg.downsize(n // 2) and kzg.N() == n // 2
     assert len(kzg.g1_powers_of_tau()) == (n // 2) * 64
