@@ -6,6 +6,7 @@
 // tests compare affine coordinates bytewise).
 #pragma once
 #include "msm.h"
+#include "../field/f29.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -406,6 +407,146 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
   if (!(flags & kHead)) hpieces[2 * t] = XYZZ<F>::zero();
   const bool through = (flags & kHead) && (flags & kTail) && (flags & kSingle);
   if (!(flags & kTail) || through) hpieces[2 * t + 1] = XYZZ<F>::zero();
+  tflags[t] = flags;
+  tlast[t] = cur;
+}
+
+// ---------------------------------------------------------------------------
+// BN254 G1 accumulation over the carry-free 29-bit-limb field (field/f29.h).
+// The same load-balanced run logic as seg_acc_kernel; the accumulator lives
+// in R' = 2^261 form and is converted back to the library's R-form XYZZ
+// (lazy < 2p) when a run is stored.  madd-2008-s (point_xyzz_impl.h:129-176)
+// with every subtraction folded into a product's output columns (limb-wise
+// K - x, K a raised multiple of p) and Y3 = R (Q - X3) - Y1 PPP as one
+// reduction of R T + (4p - Y1) PPP.  Value bounds (in units of p; a product
+// of A and B leaves < A B / 128 + 1 + addend), invariant acc X < 10,
+// Y, ZZ, ZZZ < 2; base coordinates x~ << 5 < 32:
+//   P   = x2 ZZ1 + (16p - X1)  < 17.5     R  = y2 ZZZ1 + (4p - Y1) < 5.5
+//   PP  = P^2 < 3.4   PPP = P PP < 1.47   Q  = X1 PP < 1.27
+//   X3  = R^2 + (8p - PPP - 2Q) < 9.24    T  = Q + (16p - X3) < 17.3
+//   Y3  = R T + (4p - Y1) PPP < 1.8       ZZ3, ZZZ3 < 1.05
+// Column sums stay below 2^64: the widest, R T + (4p - Y1) PPP + m p, is
+// < 13.5 2^60 (T's limbs < 1.41 2^30, 4p - Y1's < 2^30).
+namespace acc29 {
+using namespace ::tachyon_amd::f29;
+struct Acc {
+  F29 x, y, zz, zzz;
+};
+
+__device__ __forceinline__ Acc from_affine(const Affine<Bn254Fq>& a) {
+  return {from32(a.x.v), from32(a.y.v), konst(kOne29), konst(kOne29)};
+}
+__device__ __forceinline__ XYZZ<Bn254Fq> to_xyzz(const Acc& a) {
+  XYZZ<Bn254Fq> r;
+  to32(a.x, r.x.v);
+  to32(a.y, r.y.v);
+  to32(a.zz, r.zz.v);
+  to32(a.zzz, r.zzz.v);
+  return r;
+}
+__device__ __noinline__ Acc dbl_slow(const Acc& a) {  // P == acc: through the R-form doubling (rare)
+  using HF = HotFp<Bn254Fq>;
+  XYZZ<Bn254Fq> s = to_xyzz(a);
+  XYZZ<HF> h{s.x, s.y, s.zz, s.zzz};
+  h = h.dbl();
+  return {from32(h.x.v), from32(h.y.v), from32(h.zz.v), from32(h.zzz.v)};
+}
+
+// acc + (x2, y2); *special = 1: the sum is the identity (P = -acc), 2: P = acc
+// (the caller doubles); acc is returned unchanged then.
+__device__ __forceinline__ Acc madd(const Acc& A, const F29& x2, const F29& y2, int* special) {
+  const F29 P = mul_add(x2, A.zz, ksub(kK16, A.x));
+  const F29 R = mul_add(y2, A.zzz, ksub(kK4, A.y));
+  if (is_zero_mod_p(P)) {
+    *special = is_zero_mod_p(R) ? 2 : 1;
+    return A;
+  }
+  const F29 PP = sqr(P);
+  const F29 PPP = mul(P, PP);
+  const F29 Q = mul(A.x, PP);
+  Acc C;
+  C.x = sqr_add(R, ksub2(kK8, PPP, Q));
+  const F29 T = add_ksub(Q, kK16, C.x);
+  C.y = mul2_add(R, T, ksub(kK4, A.y), PPP);
+  C.zz = mul(A.zz, PP);
+  C.zzz = mul(A.zzz, PPP);
+  return C;
+}
+}  // namespace acc29
+
+__global__ __launch_bounds__(kBlock) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
+                                                           const uint64_t* __restrict__ ents, uint32_t c,
+                                                           uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
+                                                           uint32_t idx_mask, XYZZ<Bn254Fq>* __restrict__ bucket_sum,
+                                                           XYZZ<Bn254Fq>* __restrict__ pieces,
+                                                           uint32_t* __restrict__ tflags, uint32_t* __restrict__ tlast) {
+  using namespace acc29;
+  const uint64_t tl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t g0 = gbeg + tl * K;
+  if (g0 >= gend) return;
+  const uint64_t g1 = min(g0 + K, gend);
+  const uint64_t t = tbase + tl;
+  const uint32_t dmask = (1u << c) - 1;
+  auto bucket_of_key = [&](uint32_t key) -> uint32_t {
+    uint32_t d = key & dmask;
+    return d ? ((key >> c) << (c - 1)) + (d - 1) : kNoBucket;
+  };
+  const uint32_t prev_b = g0 > gbeg ? bucket_of_key(entry_key(ents[g0 - 1])) : kNoBucket;
+  const uint32_t next_b = (g1 < gend) ? bucket_of_key(entry_key(ents[g1])) : kNoBucket;
+  uint32_t flags = 0, runs = 0, cur = kNoBucket;
+  Acc acc;
+  bool acc_zero = true;
+  auto stored = [&]() { return acc_zero ? XYZZ<Bn254Fq>::zero() : to_xyzz(acc); };
+  uint64_t e0 = ents[g0];
+  uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
+  Affine<Bn254Fq> P = bases[entry_val(e0) & idx_mask];
+  for (uint64_t g = g0; g < g1; ++g) {
+    const uint64_t e2 = (g + 2 < g1) ? ents[g + 2] : 0;
+    const Affine<Bn254Fq> Pn = bases[entry_val(e1) & idx_mask];
+    const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
+    const uint32_t b = bucket_of_key(k0);
+    if (b != kNoBucket) {
+      if (b != cur) {
+        if (cur != kNoBucket) {
+          const XYZZ<Bn254Fq> s = stored();
+          if (runs == 1 && cur == prev_b) { pieces[2 * t] = s; flags |= kHead; }
+          else bucket_sum[cur] = s;
+        }
+        cur = b;
+        ++runs;
+        acc_zero = true;
+      }
+      if (!P.is_zero_canonical()) {
+        P.y = P.y.cond_neg_canonical(v0 & kSignBit);
+        if (acc_zero) {
+          acc = from_affine(P);
+          acc_zero = false;
+        } else {
+          int special = 0;
+          const Acc nxt = madd(acc, shl5_repack(P.x.v), shl5_repack(P.y.v), &special);
+          if (special == 0) acc = nxt;
+          else if (special == 1) acc_zero = true;
+          else acc = dbl_slow(acc);
+        }
+      }
+    }
+    e0 = e1;
+    e1 = e2;
+    P = Pn;
+  }
+  if (cur != kNoBucket) {
+    const XYZZ<Bn254Fq> s = stored();
+    const bool head = runs == 1 && cur == prev_b;
+    const bool tail = cur == next_b;
+    if (head) { pieces[2 * t] = s; flags |= kHead; }
+    if (tail) flags |= kTail;
+    if (tail && !head) pieces[2 * t + 1] = s;
+    if (!head && !tail) bucket_sum[cur] = s;
+  }
+  if (runs <= 1) flags |= kSingle;
+  if (!(flags & kHead)) pieces[2 * t] = XYZZ<Bn254Fq>::zero();
+  const bool through = (flags & kHead) && (flags & kTail) && (flags & kSingle);
+  if (!(flags & kTail) || through) pieces[2 * t + 1] = XYZZ<Bn254Fq>::zero();
   tflags[t] = flags;
   tlast[t] = cur;
 }
@@ -910,8 +1051,20 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
-    hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c, (uint64_t)e0,
-                       (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces, tflags, tlast);
+    if constexpr (std::is_same_v<Curve, Bn254G1>) {
+      if (acc29_)  // 29-bit-limb accumulation (set_variant bit 13, A/B)
+        hipLaunchKernelGGL(seg_acc29_kernel, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+                           (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
+                           tflags, tlast);
+      else
+        hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+                           (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
+                           tflags, tlast);
+    } else {
+      hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+                         (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
+                         tflags, tlast);
+    }
     TA_HIP(hipGetLastError());
     if (profile_) TA_HIP(hipEventRecord(gev_acc1_[g], stream_));
     tbase += Tg;
@@ -1050,6 +1203,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
   wide_stage_ = (variant_ & 2048) != 0;    // bit 11: 8-byte LDS staging in the recode scatter (A/B)
   tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
+  acc29_ = (variant_ & 8192) != 0;         // bit 13: BN254 G1 accumulation over 29-bit limbs (A/B)
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;

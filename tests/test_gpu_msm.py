@@ -33,6 +33,32 @@ def test_msm_golden(curve):
         assert ctx(curve).run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
 
 
+@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096])
+def test_msm_golden_bn254_g1_variants(variant):
+    """The golden edge cases (zero scalars, identity bases, P + (-P), doubling
+    inside a bucket, r - 1, Easy KAT) through the workgroup-tree window
+    reduction (bit 12) and the 29-bit-limb accumulation (bit 13), plus a
+    NonUniform set whose every bucket takes the doubling / cancellation paths."""
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    g = json.load(open(os.path.join(GOLDEN, "msm.json")))["bn254_g1"]
+    m = VariableBaseMSMGpu("bn254_g1")
+    m.set_variant(variant)
+    for c in g["cases"]:
+        bases = b"".join(bytes.fromhex(x) for x in c["bases"])
+        scalars = b"".join(bytes.fromhex(x) for x in c["scalars"])
+        assert m.run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
+    # the same base repeated with equal scalars: every madd after the first is a doubling
+    n = 600
+    g1 = O.gen_bases("bn254_g1", 3, 1, 1).tobytes()
+    s1 = O.gen_scalars("bn254_fr", 3, 1).tobytes()
+    assert m.run(g1 * n, s1 * n) == O.msm("bn254_g1", g1 * n, s1 * n)[0]
+    # P and -P alternating in one bucket: every other madd cancels to the identity
+    neg = O.field_op("bn254_fq", "neg", g1[32:64])
+    pm = (g1 + g1[:32] + neg) * (n // 2)
+    assert m.run(pm, s1 * n) == bytes(64)
+    m.close()
+
+
 def test_msm_zkey_points():
     z = json.load(open(os.path.join(GOLDEN, "zkey_multiplier_3.json")))
     for key, curve in (("g1", "bn254_g1"), ("g2", "bn254_g2")):
@@ -102,7 +128,7 @@ def test_msm_window_sizes_agree():
     expect, _ = O.msm("bn254_g1", bases, scalars)
     m = ctx("bn254_g1")
     try:
-        for var in (0, 4096):  # per-segment fix-up / workgroup-tree window reduction
+        for var in (0, 4096, 8192):  # per-segment fix-up / workgroup-tree window reduction / 29-bit accumulation
             m.set_variant(var)
             for c in (4, 7, 11, 16, 21):
                 m.set_window_bits(c)
@@ -281,13 +307,13 @@ def test_msm_schedule_variants_agree(curve, logn):
     want = {0: (True, True, True), 128: (False, False, False), 1024: (True, False, True),
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
-        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128):
+        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
                 s = m.last_schedule()
                 assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
-        for bad in (64, 8192):
+        for bad in (64, 16384):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
