@@ -444,7 +444,10 @@ __device__ __forceinline__ XYZZ<Bn254Fq> to_xyzz(const Acc& a) {
   to32(a.zzz, r.zzz.v);
   return r;
 }
-__device__ __noinline__ Acc dbl_slow(const Acc& a) {  // P == acc: through the R-form doubling (rare)
+// P == acc: through the R-form doubling (rare).  Inline: an out-of-line call
+// takes the accumulator's address and the compiler then keeps it in scratch
+// for the whole loop (a 288-byte scratch round trip per madd: 2^26 82.7 ms)
+__device__ __forceinline__ Acc dbl_slow(const Acc& a) {
   using HF = HotFp<Bn254Fq>;
   XYZZ<Bn254Fq> s = to_xyzz(a);
   XYZZ<HF> h{s.x, s.y, s.zz, s.zzz};
@@ -474,7 +477,8 @@ __device__ __forceinline__ Acc madd(const Acc& A, const F29& x2, const F29& y2, 
 }
 }  // namespace acc29
 
-__global__ __launch_bounds__(kBlock) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
+template <bool kPrefetch>
+__global__ __launch_bounds__(kBlock, kPrefetch ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
                                                            const uint64_t* __restrict__ ents, uint32_t c,
                                                            uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
                                                            uint32_t idx_mask, XYZZ<Bn254Fq>* __restrict__ bucket_sum,
@@ -499,10 +503,13 @@ __global__ __launch_bounds__(kBlock) void seg_acc29_kernel(const Affine<Bn254Fq>
   auto stored = [&]() { return acc_zero ? XYZZ<Bn254Fq>::zero() : to_xyzz(acc); };
   uint64_t e0 = ents[g0];
   uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
-  Affine<Bn254Fq> P = bases[entry_val(e0) & idx_mask];
+  Affine<Bn254Fq> P;
+  if constexpr (kPrefetch) P = bases[entry_val(e0) & idx_mask];
   for (uint64_t g = g0; g < g1; ++g) {
     const uint64_t e2 = (g + 2 < g1) ? ents[g + 2] : 0;
-    const Affine<Bn254Fq> Pn = bases[entry_val(e1) & idx_mask];
+    Affine<Bn254Fq> Pn;
+    if constexpr (kPrefetch) Pn = bases[entry_val(e1) & idx_mask];
+    else P = bases[entry_val(e0) & idx_mask];
     const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
@@ -532,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void seg_acc29_kernel(const Affine<Bn254Fq>
     }
     e0 = e1;
     e1 = e2;
-    P = Pn;
+    if constexpr (kPrefetch) P = Pn;
   }
   if (cur != kNoBucket) {
     const XYZZ<Bn254Fq> s = stored();
@@ -1052,8 +1059,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
-      if (acc29_)  // 29-bit-limb accumulation (set_variant bit 13, A/B)
-        hipLaunchKernelGGL(seg_acc29_kernel, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+      if (acc29_)  // 29-bit-limb accumulation (set_variant bit 13, A/B; bit 14: without the base prefetch)
+        hipLaunchKernelGGL(acc29_prefetch_ ? seg_acc29_kernel<true> : seg_acc29_kernel<false>, dim3(grid_for(Tg)),
+                           dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                            tflags, tlast);
       else
@@ -1203,7 +1211,8 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
   wide_stage_ = (variant_ & 2048) != 0;    // bit 11: 8-byte LDS staging in the recode scatter (A/B)
   tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
-  acc29_ = (variant_ & 8192) != 0;         // bit 13: BN254 G1 accumulation over 29-bit limbs (A/B)
+  acc29_ = (variant_ & (8192 | 16384)) != 0;  // bits 13/14: BN254 G1 accumulation over 29-bit limbs (A/B)
+  acc29_prefetch_ = (variant_ & 16384) == 0;  // bit 14: ... without the next-base prefetch
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;

@@ -33,7 +33,7 @@ def test_msm_golden(curve):
         assert ctx(curve).run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
 
 
-@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096])
+@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096, 16384])
 def test_msm_golden_bn254_g1_variants(variant):
     """The golden edge cases (zero scalars, identity bases, P + (-P), doubling
     inside a bucket, r - 1, Easy KAT) through the workgroup-tree window
@@ -307,13 +307,13 @@ def test_msm_schedule_variants_agree(curve, logn):
     want = {0: (True, True, True), 128: (False, False, False), 1024: (True, False, True),
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
-        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096):
+        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
                 s = m.last_schedule()
                 assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
-        for bad in (64, 16384):
+        for bad in (64, 32768):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:

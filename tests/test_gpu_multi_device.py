@@ -67,7 +67,7 @@ def test_logical_devices_device_inputs_and_reference_entry():
         m2 = M.VariableBaseMSMGpu("bn254_g1")  # tachyon_bn254_g1_create_msm_gpu reads the list
     finally:
         del os.environ["TACHYON_MSM_GPU_DEVICES"]
-    assert len(m2.last_shards()) == 0  # nothing run yet
+    assert [p for _, p, _ in m2.last_shards()] == [0, 0]  # two shards, nothing run yet
     jac = m2.run_jacobian(hb, hs)
     assert M.jacobian_to_affine("bn254_g1", jac) == want
     assert [d for d, _, _ in m2.last_shards()] == [0, 0]
