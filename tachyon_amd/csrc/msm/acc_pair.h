@@ -1,0 +1,156 @@
+// G2 bucket accumulation with a LANE PAIR per point: lane 2v holds the c0
+// and lane 2v + 1 the c1 component of every Fq2 value of virtual thread v.
+//
+// Why: an Fq2 XYZZ accumulator, the gathered point and the madd's temporaries
+// are ~10 Fq2 values -- 240 VGPRs for BLS12-381 (12-limb Fq), 160 for BN254 --
+// so the one-lane-per-point kernels run at a 2-wave cap, and BLS12-381's Fq
+// products are out-of-line calls whose argument marshalling and register
+// saves cost ~1,250 moves and ~550 B of scratch writes per addition
+// (profiles/r03a: 36.8 GB of WRITE_SIZE per 2^22 accumulation).  Split by
+// component, a lane holds one Fq per value; additions and subtractions are
+// component-wise, and a product needs the partner's components, fetched with
+// one DPP quad_perm per word:
+//   (a0 + a1 u)(b0 + b1 u) = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u   (u^2 = -1)
+//   lane h: a0 * b_h + a1 * s_h,  s_0 = -b1, s_1 = b0
+// -- one fused two-product Montgomery reduction per lane (mul_add_inline),
+// the same multiply count as the Karatsuba product on one lane (3 N^2 per
+// lane pair... 2 x 3N^2 / 2), with no calls and every value in registers.
+//   a^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u: lane h multiplies X_h Y_h with
+// X_0 = a0 + a1, Y_0 = a0 - a1, X_1 = a0, Y_1 = 2 a1 (one plain product).
+// Both lanes of a pair follow the same entries, so every branch is
+// pair-uniform; zero tests AND the two lanes' results.
+#pragma once
+#include "msm.h"
+
+namespace tachyon_amd::msm::pair {
+
+// DPP quad_perm controls: [1,0,3,2] swap partners, [0,0,2,2] even lane's
+// value to both, [1,1,3,3] odd lane's value to both
+constexpr int kSwap = 0xB1, kEven = 0xA0, kOdd = 0xF5;
+
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, kCtrl, 0xF, 0xF, false);
+}
+
+// The lane's component of a b (a0 b_h + a1 s_h) and of a^2, given its own
+// components; the partner's come in by DPP.  Inline for 8-limb fields; for
+// 12-limb fields an out-of-line call with the operands as 24 register
+// arguments (the ~900-instruction fused product inlined ~10 times per madd
+// would overflow the instruction cache), result in 12 registers.
+template <class F>
+__device__ __forceinline__ F perm_even(const F& a) {
+  F r;
+#pragma unroll
+  for (int i = 0; i < F::N; ++i) r.v[i] = dpp<kEven>(a.v[i]);
+  return r;
+}
+template <class F>
+__device__ __forceinline__ F perm_odd(const F& a) {
+  F r;
+#pragma unroll
+  for (int i = 0; i < F::N; ++i) r.v[i] = dpp<kOdd>(a.v[i]);
+  return r;
+}
+template <class F>
+__device__ __forceinline__ F pair_mul(const F& a, const F& b, bool h) {
+  const F a0 = perm_even(a), a1 = perm_odd(a);
+  // the partner's b with the sign this lane needs: lane 1 offers -b1 to
+  // lane 0 (a lazy 2p - b1), lane 0 offers b0 to lane 1
+  const F nb = -b;
+  F s;
+#pragma unroll
+  for (int i = 0; i < F::N; ++i) s.v[i] = dpp<kSwap>(h ? nb.v[i] : b.v[i]);
+  return a0.mul_add_inline(b, a1, s);
+}
+template <class F>
+__device__ __forceinline__ F pair_sqr(const F& a, bool h) {
+  const F a0 = perm_even(a), a1 = perm_odd(a);
+  const F s = a0 + a1, d = a0 - a1, t = a1.dbl();
+  F x, y;
+#pragma unroll
+  for (int i = 0; i < F::N; ++i) {
+    x.v[i] = h ? a0.v[i] : s.v[i];
+    y.v[i] = h ? t.v[i] : d.v[i];
+  }
+  return x.mul_inline(y);
+}
+template <class F>
+__device__ __noinline__ F pair_mul_regs(TA_LIMBS12(a), TA_LIMBS12(b), uint32_t h) {
+  const F x{TA_UNPACK12(a)}, y{TA_UNPACK12(b)};
+  return pair_mul(x, y, h != 0);
+}
+template <class F>
+__device__ __noinline__ F pair_sqr_regs(TA_LIMBS12(a), uint32_t h) {
+  const F x{TA_UNPACK12(a)};
+  return pair_sqr(x, h != 0);
+}
+
+template <class F>
+struct Half {  // this lane's component of an Fq2 value
+  F v;
+  __device__ __forceinline__ Half operator+(const Half& o) const { return {v + o.v}; }
+  __device__ __forceinline__ Half operator-(const Half& o) const { return {v - o.v}; }
+  __device__ __forceinline__ Half dbl() const { return {v.dbl()}; }
+  __device__ __forceinline__ Half mul(const Half& b, bool h) const {
+    if constexpr (F::N == 12) return {pair_mul_regs<F>(TA_PASS12(v), TA_PASS12(b.v), h ? 1u : 0u)};
+    else return {pair_mul(v, b.v, h)};
+  }
+  __device__ __forceinline__ Half sqr(bool h) const {
+    if constexpr (F::N == 12) return {pair_sqr_regs<F>(TA_PASS12(v), h ? 1u : 0u)};
+    else return {pair_sqr(v, h)};
+  }
+  // zero of the whole Fq2 value (both lanes agree)
+  __device__ __forceinline__ bool is_zero() const {
+    const uint32_t z = v.is_zero() ? 1u : 0u;
+    return (z & dpp<kSwap>(z)) != 0;
+  }
+};
+
+template <class F>
+struct Acc {
+  Half<F> x, y, zz, zzz;
+};
+
+// madd-2008-s (point_xyzz_impl.h:129-176) on lane-pair Fq2 values, with the
+// identity accumulator kept as a flag by the caller.  *special: 1 = the sum is
+// the identity (P = -acc), 2 = P = acc (the caller doubles); acc unchanged then.
+template <class F>
+__device__ __forceinline__ Acc<F> madd(const Acc<F>& A, const Half<F>& x2, const Half<F>& y2, bool h, int* special) {
+  const Half<F> p = x2.mul(A.zz, h) - A.x;
+  const Half<F> r = y2.mul(A.zzz, h) - A.y;
+  if (p.is_zero()) {
+    *special = r.is_zero() ? 2 : 1;
+    return A;
+  }
+  const Half<F> pp = p.sqr(h);
+  const Half<F> ppp = p.mul(pp, h);
+  const Half<F> q = A.x.mul(pp, h);
+  Acc<F> c;
+  c.x = r.sqr(h) - ppp - q.dbl();
+  c.y = r.mul(q - c.x, h) - A.y.mul(ppp, h);
+  c.zz = A.zz.mul(pp, h);
+  c.zzz = A.zzz.mul(ppp, h);
+  return c;
+}
+
+// dbl-2008-s-1 (a = 0; point_xyzz_impl.h:199-236): the P = acc case.  Inline
+// (an out-of-line call taking the accumulator's address would keep it in
+// scratch for the whole loop); its 12-limb products are calls anyway.
+template <class F>
+__device__ __forceinline__ Acc<F> dbl(const Acc<F>& A, bool h) {
+  const Half<F> u = A.y.dbl();
+  const Half<F> v = u.sqr(h);
+  const Half<F> w = u.mul(v, h);
+  const Half<F> s = A.x.mul(v, h);
+  Half<F> m = A.x.sqr(h);
+  m = m + m.dbl();
+  Acc<F> c;
+  c.x = m.sqr(h) - s.dbl();
+  c.y = m.mul(s - c.x, h) - w.mul(A.y, h);
+  c.zz = v.mul(A.zz, h);
+  c.zzz = w.mul(A.zzz, h);
+  return c;
+}
+
+}  // namespace tachyon_amd::msm::pair

@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0x7FBF;
+constexpr int kMsmVariantMask = 0xFFBF;
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter
@@ -206,6 +206,7 @@ class MsmGpu {
   bool tree_reduce_ = false;   // window sums by workgroup trees (bit 12)
   bool acc29_ = false;         // BN254 G1 accumulation over 29-bit limbs (bit 13)
   bool acc29_prefetch_ = true; // ... with the next base prefetched (bit 14 clears it)
+  bool pair_acc_ = false;      // G2 accumulation with a lane pair per point (bit 15)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode

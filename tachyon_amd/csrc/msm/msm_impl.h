@@ -7,6 +7,7 @@
 #pragma once
 #include "msm.h"
 #include "../field/f29.h"
+#include "acc_pair.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -558,6 +559,110 @@ __global__ __launch_bounds__(kBlock, kPrefetch ? 1 : 3) void seg_acc29_kernel(co
   tlast[t] = cur;
 }
 
+// ---------------------------------------------------------------------------
+// G2 (Fq2) accumulation with a lane pair per virtual thread (acc_pair.h): the
+// run logic of seg_acc_kernel, lane h holding component h of every Fq2 value.
+// Both lanes of a pair read the same entries and take the same branches.
+template <class Curve>
+__global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typename Curve::F>* __restrict__ bases,
+                                                              const uint64_t* __restrict__ ents, uint32_t c,
+                                                              uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
+                                                              uint32_t idx_mask,
+                                                              XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+                                                              XYZZ<typename Curve::F>* __restrict__ pieces,
+                                                              uint32_t* __restrict__ tflags,
+                                                              uint32_t* __restrict__ tlast) {
+  using Fb = typename Curve::F::Base;  // Fq
+  using F = HotFp<Fb>;
+  using namespace pair;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint64_t tl = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 1;
+  const uint64_t g0 = gbeg + tl * K;
+  if (g0 >= gend) return;  // both lanes of the pair
+  const uint64_t g1 = min(g0 + K, gend);
+  const uint64_t t = tbase + tl;
+  const uint32_t dmask = (1u << c) - 1;
+  auto bucket_of_key = [&](uint32_t key) -> uint32_t {
+    uint32_t d = key & dmask;
+    return d ? ((key >> c) << (c - 1)) + (d - 1) : kNoBucket;
+  };
+  const uint32_t prev_b = g0 > gbeg ? bucket_of_key(entry_key(ents[g0 - 1])) : kNoBucket;
+  const uint32_t next_b = (g1 < gend) ? bucket_of_key(entry_key(ents[g1])) : kNoBucket;
+  // component views: a point is {x.c0, x.c1, y.c0, y.c1}, an XYZZ {x.c0, x.c1, ..., zzz.c1}
+  const Fb* comp = reinterpret_cast<const Fb*>(bases);
+  Fb* bsum = reinterpret_cast<Fb*>(bucket_sum);
+  Fb* pcs = reinterpret_cast<Fb*>(pieces);
+  const F one_h = h ? F::zero() : F::one();
+  Acc<F> acc;
+  bool acc_zero = true;
+  auto store = [&](Fb* dst, uint64_t idx) {  // this lane's components of the run sum (identity if none)
+    Fb* o = dst + 8 * idx;
+    if (acc_zero) {
+      o[h] = one_h;
+      o[2 + h] = one_h;
+      o[4 + h] = Fb::zero();
+      o[6 + h] = Fb::zero();
+    } else {
+      o[h] = acc.x.v;
+      o[2 + h] = acc.y.v;
+      o[4 + h] = acc.zz.v;
+      o[6 + h] = acc.zzz.v;
+    }
+  };
+  uint32_t flags = 0, runs = 0, cur = kNoBucket;
+  uint64_t e0 = ents[g0];
+  for (uint64_t g = g0; g < g1; ++g) {
+    const uint64_t e1 = (g + 1 < g1) ? ents[g + 1] : 0;
+    const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
+    const uint32_t b = bucket_of_key(k0);
+    if (b != kNoBucket) {
+      const Fb* pt = comp + 4 * (size_t)(v0 & idx_mask);
+      Half<F> px{pt[h]}, py{pt[2 + h]};
+      if (b != cur) {
+        if (cur != kNoBucket) {
+          if (runs == 1 && cur == prev_b) { store(pcs, 2 * t); flags |= kHead; }
+          else store(bsum, cur);
+        }
+        cur = b;
+        ++runs;
+        acc_zero = true;
+      }
+      const uint32_t pz = (px.v.is_zero_canonical() && py.v.is_zero_canonical()) ? 1u : 0u;
+      if (!(pz & dpp<kSwap>(pz))) {  // not the identity base (both components zero)
+        py.v = py.v.cond_neg_canonical(v0 & kSignBit);
+        if (acc_zero) {
+          acc = Acc<F>{px, py, Half<F>{one_h}, Half<F>{one_h}};
+          acc_zero = false;
+        } else {
+          int special = 0;
+          const Acc<F> nxt = madd(acc, px, py, h != 0, &special);
+          if (special == 0) acc = nxt;
+          else if (special == 1) acc_zero = true;
+          else acc = pair::dbl(acc, h != 0);
+        }
+      }
+    }
+    e0 = e1;
+  }
+  if (cur != kNoBucket) {
+    const bool head = runs == 1 && cur == prev_b;
+    const bool tail = cur == next_b;
+    if (head) { store(pcs, 2 * t); flags |= kHead; }
+    if (tail) flags |= kTail;
+    if (tail && !head) store(pcs, 2 * t + 1);
+    if (!head && !tail) store(bsum, cur);
+  }
+  if (runs <= 1) flags |= kSingle;
+  acc_zero = true;  // absent pieces are the identity
+  if (!(flags & kHead)) store(pcs, 2 * t);
+  const bool through = (flags & kHead) && (flags & kTail) && (flags & kSingle);
+  if (!(flags & kTail) || through) store(pcs, 2 * t + 1);
+  if (h == 0) {
+    tflags[t] = flags;
+    tlast[t] = cur;
+  }
+}
+
 // A bucket that crosses thread boundaries forms a chain t0 < ... < t1: the
 // tail of t0, the whole-range heads of the "through" threads in between and
 // the head of t1 -- i.e. pieces[2*t0+1 .. 2*t1] (absent tails are identity).
@@ -1068,6 +1173,15 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
         hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                            tflags, tlast);
+    } else if constexpr (std::is_same_v<Curve, Bn254G2> || std::is_same_v<Curve, Bls381G2>) {
+      if (pair_acc_)  // a lane pair per virtual thread (set_variant bit 15, A/B)
+        hipLaunchKernelGGL(seg_acc_pair_kernel<Curve>, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
+                           ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum,
+                           pieces, tflags, tlast);
+      else
+        hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+                           (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
+                           tflags, tlast);
     } else {
       hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
                          (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
@@ -1213,6 +1327,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
   acc29_ = (variant_ & (8192 | 16384)) != 0;  // bits 13/14: BN254 G1 accumulation over 29-bit limbs (A/B)
   acc29_prefetch_ = (variant_ & 16384) == 0;  // bit 14: ... without the next-base prefetch
+  pair_acc_ = (variant_ & 32768) != 0;        // bit 15: G2 accumulation with a lane pair per point (A/B)
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;

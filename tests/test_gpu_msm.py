@@ -59,6 +59,34 @@ def test_msm_golden_bn254_g1_variants(variant):
     m.close()
 
 
+@pytest.mark.parametrize("curve", ["bn254_g2", "bls12_381_g2"])
+def test_msm_golden_g2_lane_pair(curve):
+    """The G2 accumulation with a lane pair per point (set_variant bit 15):
+    golden edge cases, a random set, a repeated base (doublings inside one
+    bucket) and P, -P alternating (cancellations)."""
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    g = json.load(open(os.path.join(GOLDEN, "msm.json")))[curve]
+    m = VariableBaseMSMGpu(curve)
+    m.set_variant(32768)
+    for c in g["cases"]:
+        bases = b"".join(bytes.fromhex(x) for x in c["bases"])
+        scalars = b"".join(bytes.fromhex(x) for x in c["scalars"])
+        assert m.run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
+    pb, sf = O.CURVE_INFO[curve]
+    n = 3001
+    bases = O.gen_bases(curve, 17, n, 40).tobytes()
+    scalars = O.gen_scalars(sf, 17, n).tobytes()
+    assert m.run(bases, scalars) == O.msm(curve, bases, scalars)[0]
+    g1, s1 = bases[:pb], scalars[:32]
+    assert m.run(g1 * 300, s1 * 300) == O.msm(curve, g1 * 300, s1 * 300)[0]
+    fq = "bn254_fq" if curve.startswith("bn254") else "bls12_381_fq"
+    half = pb // 4  # one Fq
+    ny = O.field_op(fq, "neg", g1[2 * half:])  # -y, component-wise
+    pm = (g1 + g1[:2 * half] + ny) * 150
+    assert m.run(pm, s1 * 300) == bytes(pb)
+    m.close()
+
+
 def test_msm_zkey_points():
     z = json.load(open(os.path.join(GOLDEN, "zkey_multiplier_3.json")))
     for key, curve in (("g1", "bn254_g1"), ("g2", "bn254_g2")):
@@ -307,13 +335,14 @@ def test_msm_schedule_variants_agree(curve, logn):
     want = {0: (True, True, True), 128: (False, False, False), 1024: (True, False, True),
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
-        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384):
+        for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384,
+                  32768):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
                 s = m.last_schedule()
                 assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
-        for bad in (64, 32768):
+        for bad in (64, 65536):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
