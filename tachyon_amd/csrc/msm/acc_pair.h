@@ -86,18 +86,18 @@ __device__ __noinline__ F pair_sqr_regs(TA_LIMBS12(a), uint32_t h) {
   return pair_sqr(x, h != 0);
 }
 
-template <class F>
-struct Half {  // this lane's component of an Fq2 value
+template <class F, bool kCall = (F::N == 12)>
+struct Half {  // this lane's component of an Fq2 value (kCall: 12-limb products out of line)
   F v;
   __device__ __forceinline__ Half operator+(const Half& o) const { return {v + o.v}; }
   __device__ __forceinline__ Half operator-(const Half& o) const { return {v - o.v}; }
   __device__ __forceinline__ Half dbl() const { return {v.dbl()}; }
   __device__ __forceinline__ Half mul(const Half& b, bool h) const {
-    if constexpr (F::N == 12) return {pair_mul_regs<F>(TA_PASS12(v), TA_PASS12(b.v), h ? 1u : 0u)};
+    if constexpr (kCall) return {pair_mul_regs<F>(TA_PASS12(v), TA_PASS12(b.v), h ? 1u : 0u)};
     else return {pair_mul(v, b.v, h)};
   }
   __device__ __forceinline__ Half sqr(bool h) const {
-    if constexpr (F::N == 12) return {pair_sqr_regs<F>(TA_PASS12(v), h ? 1u : 0u)};
+    if constexpr (kCall) return {pair_sqr_regs<F>(TA_PASS12(v), h ? 1u : 0u)};
     else return {pair_sqr(v, h)};
   }
   // zero of the whole Fq2 value (both lanes agree)
@@ -107,26 +107,26 @@ struct Half {  // this lane's component of an Fq2 value
   }
 };
 
-template <class F>
+template <class H>
 struct Acc {
-  Half<F> x, y, zz, zzz;
+  H x, y, zz, zzz;
 };
 
 // madd-2008-s (point_xyzz_impl.h:129-176) on lane-pair Fq2 values, with the
 // identity accumulator kept as a flag by the caller.  *special: 1 = the sum is
 // the identity (P = -acc), 2 = P = acc (the caller doubles); acc unchanged then.
-template <class F>
-__device__ __forceinline__ Acc<F> madd(const Acc<F>& A, const Half<F>& x2, const Half<F>& y2, bool h, int* special) {
-  const Half<F> p = x2.mul(A.zz, h) - A.x;
-  const Half<F> r = y2.mul(A.zzz, h) - A.y;
+template <class H>
+__device__ __forceinline__ Acc<H> madd(const Acc<H>& A, const H& x2, const H& y2, bool h, int* special) {
+  const H p = x2.mul(A.zz, h) - A.x;
+  const H r = y2.mul(A.zzz, h) - A.y;
   if (p.is_zero()) {
     *special = r.is_zero() ? 2 : 1;
     return A;
   }
-  const Half<F> pp = p.sqr(h);
-  const Half<F> ppp = p.mul(pp, h);
-  const Half<F> q = A.x.mul(pp, h);
-  Acc<F> c;
+  const H pp = p.sqr(h);
+  const H ppp = p.mul(pp, h);
+  const H q = A.x.mul(pp, h);
+  Acc<H> c;
   c.x = r.sqr(h) - ppp - q.dbl();
   c.y = r.mul(q - c.x, h) - A.y.mul(ppp, h);
   c.zz = A.zz.mul(pp, h);
@@ -137,15 +137,15 @@ __device__ __forceinline__ Acc<F> madd(const Acc<F>& A, const Half<F>& x2, const
 // dbl-2008-s-1 (a = 0; point_xyzz_impl.h:199-236): the P = acc case.  Inline
 // (an out-of-line call taking the accumulator's address would keep it in
 // scratch for the whole loop); its 12-limb products are calls anyway.
-template <class F>
-__device__ __forceinline__ Acc<F> dbl(const Acc<F>& A, bool h) {
-  const Half<F> u = A.y.dbl();
-  const Half<F> v = u.sqr(h);
-  const Half<F> w = u.mul(v, h);
-  const Half<F> s = A.x.mul(v, h);
-  Half<F> m = A.x.sqr(h);
+template <class H>
+__device__ __forceinline__ Acc<H> dbl(const Acc<H>& A, bool h) {
+  const H u = A.y.dbl();
+  const H v = u.sqr(h);
+  const H w = u.mul(v, h);
+  const H s = A.x.mul(v, h);
+  H m = A.x.sqr(h);
   m = m + m.dbl();
-  Acc<F> c;
+  Acc<H> c;
   c.x = m.sqr(h) - s.dbl();
   c.y = m.mul(s - c.x, h) - w.mul(A.y, h);
   c.zz = v.mul(A.zz, h);

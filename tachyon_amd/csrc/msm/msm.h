@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0xFFBF;
+constexpr int kMsmVariantMask = 0x3FFBF;
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter
@@ -205,8 +205,9 @@ class MsmGpu {
   bool wide_stage_ = false;    // 8-byte entries in the recode scatter's LDS staging (bit 11)
   bool tree_reduce_ = false;   // window sums by workgroup trees (bit 12)
   bool acc29_ = false;         // BN254 G1 accumulation over 29-bit limbs (bit 13)
-  bool acc29_prefetch_ = true; // ... with the next base prefetched (bit 14 clears it)
+  int acc29_mode_ = 1;         // ... next base: 1 in registers, 0 not prefetched (bit 14), 2 via LDS-DMA (bit 17)
   bool pair_acc_ = false;      // G2 accumulation with a lane pair per point (bit 15)
+  bool pair_inline_ = false;   // ... its 12-limb products inline (bit 16)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass
   uint32_t recode_spt_ = 2;          // scalars per thread of the fused recode

@@ -478,8 +478,13 @@ __device__ __forceinline__ Acc madd(const Acc& A, const F29& x2, const F29& y2, 
 }
 }  // namespace acc29
 
-template <bool kPrefetch>
-__global__ __launch_bounds__(kBlock, kPrefetch ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
+// kPrefetch: 0 = gather each base at its own iteration; 1 = the next base in
+// registers (16 VGPRs: 186, two waves per SIMD); 2 = the next base through
+// LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR destination, so the
+// kernel keeps its 3-wave register budget with the gather one iteration ahead)
+typedef __attribute__((address_space(3))) void lds_void_t;
+template <int kPrefetch>
+__global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
                                                            const uint64_t* __restrict__ ents, uint32_t c,
                                                            uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
                                                            uint32_t idx_mask, XYZZ<Bn254Fq>* __restrict__ bucket_sum,
@@ -505,12 +510,35 @@ __global__ __launch_bounds__(kBlock, kPrefetch ? 1 : 3) void seg_acc29_kernel(co
   uint64_t e0 = ents[g0];
   uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
   Affine<Bn254Fq> P;
-  if constexpr (kPrefetch) P = bases[entry_val(e0) & idx_mask];
-  for (uint64_t g = g0; g < g1; ++g) {
+  // LDS-DMA staging: [slot][wave][16-byte chunk][lane], 32 KiB per workgroup; a
+  // wave-instruction writes its 64 lanes' chunks contiguously (base + 16 lane)
+  __shared__ uint4 stage[kPrefetch == 2 ? 2 : 1][kPrefetch == 2 ? kBlock / 64 : 1][4][64];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  auto issue = [&](uint64_t e, uint32_t slot) {  // the base of entry e into stage[slot]
+    const uint4* src = reinterpret_cast<const uint4*>(bases + (entry_val(e) & idx_mask));
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch)
+      __builtin_amdgcn_global_load_lds(src + ch, (lds_void_t*)&stage[slot][wave][ch][0], 16, 0, 0);
+  };
+  if constexpr (kPrefetch == 1) P = bases[entry_val(e0) & idx_mask];
+  if constexpr (kPrefetch == 2) issue(e0, 0);
+  uint32_t it = 0;  // iteration count: the same for every lane of the wave (K entries each)
+  for (uint64_t g = g0; g < g1; ++g, ++it) {
     const uint64_t e2 = (g + 2 < g1) ? ents[g + 2] : 0;
     Affine<Bn254Fq> Pn;
-    if constexpr (kPrefetch) Pn = bases[entry_val(e1) & idx_mask];
-    else P = bases[entry_val(e0) & idx_mask];
+    if constexpr (kPrefetch == 1) {
+      Pn = bases[entry_val(e1) & idx_mask];
+    } else if constexpr (kPrefetch == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this iteration's base has landed
+      const uint32_t slot = it & 1;
+      uint4 ch[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ch[q] = stage[slot][wave][q][lane];
+      memcpy(&P, ch, sizeof(P));
+      if (g + 1 < g1) issue(e1, slot ^ 1);  // the next base, under this iteration's madd
+    } else {
+      P = bases[entry_val(e0) & idx_mask];
+    }
     const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
@@ -540,7 +568,7 @@ __global__ __launch_bounds__(kBlock, kPrefetch ? 1 : 3) void seg_acc29_kernel(co
     }
     e0 = e1;
     e1 = e2;
-    if constexpr (kPrefetch) P = Pn;
+    if constexpr (kPrefetch == 1) P = Pn;
   }
   if (cur != kNoBucket) {
     const XYZZ<Bn254Fq> s = stored();
@@ -563,7 +591,7 @@ __global__ __launch_bounds__(kBlock, kPrefetch ? 1 : 3) void seg_acc29_kernel(co
 // G2 (Fq2) accumulation with a lane pair per virtual thread (acc_pair.h): the
 // run logic of seg_acc_kernel, lane h holding component h of every Fq2 value.
 // Both lanes of a pair read the same entries and take the same branches.
-template <class Curve>
+template <class Curve, bool kCall>
 __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typename Curve::F>* __restrict__ bases,
                                                               const uint64_t* __restrict__ ents, uint32_t c,
                                                               uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
@@ -575,6 +603,7 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typen
   using Fb = typename Curve::F::Base;  // Fq
   using F = HotFp<Fb>;
   using namespace pair;
+  using H = Half<F, kCall>;
   const uint32_t h = threadIdx.x & 1u;
   const uint64_t tl = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 1;
   const uint64_t g0 = gbeg + tl * K;
@@ -593,7 +622,7 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typen
   Fb* bsum = reinterpret_cast<Fb*>(bucket_sum);
   Fb* pcs = reinterpret_cast<Fb*>(pieces);
   const F one_h = h ? F::zero() : F::one();
-  Acc<F> acc;
+  Acc<H> acc;
   bool acc_zero = true;
   auto store = [&](Fb* dst, uint64_t idx) {  // this lane's components of the run sum (identity if none)
     Fb* o = dst + 8 * idx;
@@ -617,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typen
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
       const Fb* pt = comp + 4 * (size_t)(v0 & idx_mask);
-      Half<F> px{pt[h]}, py{pt[2 + h]};
+      H px{pt[h]}, py{pt[2 + h]};
       if (b != cur) {
         if (cur != kNoBucket) {
           if (runs == 1 && cur == prev_b) { store(pcs, 2 * t); flags |= kHead; }
@@ -631,11 +660,11 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typen
       if (!(pz & dpp<kSwap>(pz))) {  // not the identity base (both components zero)
         py.v = py.v.cond_neg_canonical(v0 & kSignBit);
         if (acc_zero) {
-          acc = Acc<F>{px, py, Half<F>{one_h}, Half<F>{one_h}};
+          acc = Acc<H>{px, py, H{one_h}, H{one_h}};
           acc_zero = false;
         } else {
           int special = 0;
-          const Acc<F> nxt = madd(acc, px, py, h != 0, &special);
+          const Acc<H> nxt = madd(acc, px, py, h != 0, &special);
           if (special == 0) acc = nxt;
           else if (special == 1) acc_zero = true;
           else acc = pair::dbl(acc, h != 0);
@@ -1165,7 +1194,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     const size_t Tg = (ecount + K - 1) / K;
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
       if (acc29_)  // 29-bit-limb accumulation (set_variant bit 13, A/B; bit 14: without the base prefetch)
-        hipLaunchKernelGGL(acc29_prefetch_ ? seg_acc29_kernel<true> : seg_acc29_kernel<false>, dim3(grid_for(Tg)),
+        hipLaunchKernelGGL(acc29_mode_ == 2 ? seg_acc29_kernel<2> : acc29_mode_ == 1 ? seg_acc29_kernel<1>
+                                                                            : seg_acc29_kernel<0>,
+                           dim3(grid_for(Tg)),
                            dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                            tflags, tlast);
@@ -1174,8 +1205,11 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                            tflags, tlast);
     } else if constexpr (std::is_same_v<Curve, Bn254G2> || std::is_same_v<Curve, Bls381G2>) {
-      if (pair_acc_)  // a lane pair per virtual thread (set_variant bit 15, A/B)
-        hipLaunchKernelGGL(seg_acc_pair_kernel<Curve>, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
+      // a lane pair per virtual thread (set_variant bit 15, A/B; bit 16: inline 12-limb products)
+      constexpr bool kCallDefault = Curve::F::Base::N == 12;
+      auto* pair_kernel = pair_inline_ ? &seg_acc_pair_kernel<Curve, false> : &seg_acc_pair_kernel<Curve, kCallDefault>;
+      if (pair_acc_)
+        hipLaunchKernelGGL(pair_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
                            ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum,
                            pieces, tflags, tlast);
       else
@@ -1325,9 +1359,12 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
   wide_stage_ = (variant_ & 2048) != 0;    // bit 11: 8-byte LDS staging in the recode scatter (A/B)
   tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
-  acc29_ = (variant_ & (8192 | 16384)) != 0;  // bits 13/14: BN254 G1 accumulation over 29-bit limbs (A/B)
-  acc29_prefetch_ = (variant_ & 16384) == 0;  // bit 14: ... without the next-base prefetch
-  pair_acc_ = (variant_ & 32768) != 0;        // bit 15: G2 accumulation with a lane pair per point (A/B)
+  // bits 13 / 14 / 17: BN254 G1 accumulation over 29-bit limbs with the next
+  // base prefetched in registers / not prefetched / prefetched through LDS (A/B)
+  acc29_ = (variant_ & (8192 | 16384 | 131072)) != 0;
+  acc29_mode_ = (variant_ & 131072) ? 2 : (variant_ & 16384) ? 0 : 1;
+  pair_acc_ = (variant_ & (32768 | 65536)) != 0;  // bits 15/16: G2 accumulation with a lane pair per point (A/B)
+  pair_inline_ = (variant_ & 65536) != 0;         // bit 16: ... with the 12-limb products inline
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;

@@ -33,7 +33,7 @@ def test_msm_golden(curve):
         assert ctx(curve).run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
 
 
-@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096, 16384])
+@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096, 16384, 131072])
 def test_msm_golden_bn254_g1_variants(variant):
     """The golden edge cases (zero scalars, identity bases, P + (-P), doubling
     inside a bucket, r - 1, Easy KAT) through the workgroup-tree window
@@ -67,7 +67,7 @@ def test_msm_golden_g2_lane_pair(curve):
     from tachyon_amd.msm import VariableBaseMSMGpu
     g = json.load(open(os.path.join(GOLDEN, "msm.json")))[curve]
     m = VariableBaseMSMGpu(curve)
-    m.set_variant(32768)
+    m.set_variant(32768 if curve == "bn254_g2" else 65536)
     for c in g["cases"]:
         bases = b"".join(bytes.fromhex(x) for x in c["bases"])
         scalars = b"".join(bytes.fromhex(x) for x in c["scalars"])
@@ -156,7 +156,7 @@ def test_msm_window_sizes_agree():
     expect, _ = O.msm("bn254_g1", bases, scalars)
     m = ctx("bn254_g1")
     try:
-        for var in (0, 4096, 8192):  # per-segment fix-up / workgroup-tree window reduction / 29-bit accumulation
+        for var in (0, 4096, 8192, 131072):  # fix-up / workgroup-tree reduction / 29-bit accumulation (+ LDS-DMA)
             m.set_variant(var)
             for c in (4, 7, 11, 16, 21):
                 m.set_window_bits(c)
@@ -336,13 +336,13 @@ def test_msm_schedule_variants_agree(curve, logn):
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
         for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384,
-                  32768):
+                  32768, 65536, 131072):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
                 s = m.last_schedule()
                 assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
-        for bad in (64, 65536):
+        for bad in (64, 1 << 18):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
