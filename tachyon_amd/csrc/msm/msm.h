@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0x3FFBF;
+constexpr int kMsmVariantMask = 0x7FFBF;
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter

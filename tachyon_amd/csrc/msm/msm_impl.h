@@ -1208,6 +1208,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       // a lane pair per virtual thread (set_variant bit 15, A/B; bit 16: inline 12-limb products)
       constexpr bool kCallDefault = Curve::F::Base::N == 12;
       auto* pair_kernel = pair_inline_ ? &seg_acc_pair_kernel<Curve, false> : &seg_acc_pair_kernel<Curve, kCallDefault>;
+      // (kCallDefault is false for 8-limb fields: both entries are the inline kernel there)
       if (pair_acc_)
         hipLaunchKernelGGL(pair_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
                            ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum,
@@ -1361,10 +1362,18 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
   // bits 13 / 14 / 17: BN254 G1 accumulation over 29-bit limbs with the next
   // base prefetched in registers / not prefetched / prefetched through LDS (A/B)
-  acc29_ = (variant_ & (8192 | 16384 | 131072)) != 0;
+  // Default: the 29-bit field for BN254 G1 at >= 2^29 (point, window) entries
+  // (the 2^26 headline: accumulation 67.7 -> 65.5 ms; at 2^24 it measured
+  // 2 % slower and stays off -- profiles/r03a/ab_acc29_fips32.log); bit 18
+  // forces the 32-bit FIPS field at every size
+  const bool acc29_default = std::is_same_v<Curve, Bn254G1> && (size_t)n * plan.active() >= (size_t(1) << 29);
+  acc29_ = !(variant_ & 262144) && ((variant_ & (8192 | 16384 | 131072)) != 0 || acc29_default);
   acc29_mode_ = (variant_ & 131072) ? 2 : (variant_ & 16384) ? 0 : 1;
-  pair_acc_ = (variant_ & (32768 | 65536)) != 0;  // bits 15/16: G2 accumulation with a lane pair per point (A/B)
-  pair_inline_ = (variant_ & 65536) != 0;         // bit 16: ... with the 12-limb products inline
+  // G2: a lane pair per point with inline products by default (BLS12-381 G2
+  // 2^24 accumulation 129 -> 113 ms, BN254 G2 2^22 16.3 -> 15.7 ms); bit 15
+  // restores the one-lane kernel, bit 16 the pair with out-of-line 12-limb products
+  pair_acc_ = !(variant_ & 32768);
+  pair_inline_ = !(variant_ & 65536);
   if (plan_out) *plan_out = plan;
   out->assign(plan.active(), Point::zero());
   if (n == 0 || plan.active() == 0) return;

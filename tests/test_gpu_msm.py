@@ -33,7 +33,7 @@ def test_msm_golden(curve):
         assert ctx(curve).run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
 
 
-@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096, 16384, 131072])
+@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096, 16384, 131072, 262144])
 def test_msm_golden_bn254_g1_variants(variant):
     """The golden edge cases (zero scalars, identity bases, P + (-P), doubling
     inside a bucket, r - 1, Easy KAT) through the workgroup-tree window
@@ -59,15 +59,18 @@ def test_msm_golden_bn254_g1_variants(variant):
     m.close()
 
 
-@pytest.mark.parametrize("curve", ["bn254_g2", "bls12_381_g2"])
-def test_msm_golden_g2_lane_pair(curve):
-    """The G2 accumulation with a lane pair per point (set_variant bit 15):
-    golden edge cases, a random set, a repeated base (doublings inside one
-    bucket) and P, -P alternating (cancellations)."""
+@pytest.mark.parametrize("curve,variant", [("bn254_g2", 0), ("bn254_g2", 32768), ("bls12_381_g2", 0),
+                                           ("bls12_381_g2", 32768), ("bls12_381_g2", 65536)])
+def test_msm_golden_g2_lane_pair(curve, variant):
+    """The G2 accumulations: a lane pair per point with inline products (the
+    default), the one-lane kernel (set_variant bit 15) and, for BLS12-381, the
+    pair with out-of-line 12-limb products (bit 16) -- golden edge cases, a
+    random set, a repeated base (doublings inside one bucket) and P, -P
+    alternating (cancellations)."""
     from tachyon_amd.msm import VariableBaseMSMGpu
     g = json.load(open(os.path.join(GOLDEN, "msm.json")))[curve]
     m = VariableBaseMSMGpu(curve)
-    m.set_variant(32768 if curve == "bn254_g2" else 65536)
+    m.set_variant(variant)
     for c in g["cases"]:
         bases = b"".join(bytes.fromhex(x) for x in c["bases"])
         scalars = b"".join(bytes.fromhex(x) for x in c["scalars"])
@@ -336,13 +339,13 @@ def test_msm_schedule_variants_agree(curve, logn):
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
         for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384,
-                  32768, 65536, 131072):
+                  32768, 65536, 131072, 262144):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
                 s = m.last_schedule()
                 assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
-        for bad in (64, 1 << 18):
+        for bad in (64, 1 << 19):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
