@@ -342,7 +342,8 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void*
 TACHYON_C_EXPORT size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx);
 /* Schedule of the last run (of its last point chunk): bit 0 the recode fused
  * with the first radix pass, bit 1 onesweep passes fed by the recode's digit
- * counts, bit 2 7-byte LDS staging in the recode scatter. */
+ * counts, bit 2 7-byte LDS staging in the recode scatter, bit 3 the BN254 G1
+ * accumulation over the 29-bit-limb field, bit 4 the lane-pair G2 accumulation. */
 TACHYON_C_EXPORT unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx);
 /* One process, several MI355X: every later MSM of this context splits its
  * points into `count` contiguous shards, shard k on device device_ids[k]

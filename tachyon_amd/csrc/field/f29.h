@@ -133,11 +133,24 @@ TA_HD F29 sqr_redc(const F29& a, const F29& e) {
   return r;
 }
 
+}  // namespace tachyon_amd::f29
+#include "f29_asm.h"  // device: the same columns as hand-chained v_mad_u64_u32 (tools/gen_f29_asm.py)
+namespace tachyon_amd::f29 {
+
+// mul2_add(a, b, c, d) = REDC(a b + c d); mul_add / sqr_add add e to the output
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TA_F29_CXX)
+TA_HD F29 mul(const F29& a, const F29& b) { return asm29::mul(a, b); }
+TA_HD F29 mul_add(const F29& a, const F29& b, const F29& e) { return asm29::mul_add(a, b, e); }
+TA_HD F29 mul2_add(const F29& a, const F29& b, const F29& c, const F29& d) { return asm29::mul2(a, b, c, d); }
+TA_HD F29 sqr(const F29& a) { return asm29::sqr(a); }
+TA_HD F29 sqr_add(const F29& a, const F29& e) { return asm29::sqr_add(a, e); }
+#else
 TA_HD F29 mul(const F29& a, const F29& b) { return redc<false, false>(a, b, a, b, a); }
 TA_HD F29 mul_add(const F29& a, const F29& b, const F29& e) { return redc<false, true>(a, b, a, b, e); }
 TA_HD F29 mul2_add(const F29& a, const F29& b, const F29& c, const F29& d) { return redc<true, false>(a, b, c, d, a); }
 TA_HD F29 sqr(const F29& a) { return sqr_redc<false>(a, a); }
 TA_HD F29 sqr_add(const F29& a, const F29& e) { return sqr_redc<true>(a, e); }
+#endif
 
 // limb-wise (no carries): K - x, K + a - x, K - a - b (K a raised multiple of p
 // whose limbs are at least the subtrahends' limbs)
@@ -177,11 +190,12 @@ TA_HD F29 shl5_repack(const uint32_t* w) {
   return r;
 }
 
-// N-form value < 2^256 -> 8 x 32-bit words
+// bits kOff .. kOff + 255 of a limb-exact value (limbs 0..7 < 2^29) -> 8 x 32-bit words
+template <int kOff = 0>
 TA_HD void repack32(const F29& x, uint32_t* w) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int bit = 32 * j;
+    const int bit = 32 * j + kOff;
     const int i = bit / 29, sh = bit % 29;
     uint64_t v = (uint64_t)(x.l[i] >> sh);
     int got = 29 - sh;
@@ -192,15 +206,41 @@ TA_HD void repack32(const F29& x, uint32_t* w) {
   }
 }
 
-// R-form words (lazy < 2p) -> R' form, value < 2p: x' = (x~ << 5) 1' / 2^261
-TA_HD F29 from32(const uint32_t* w) { return mul(shl5_repack(w), konst(kOne29)); }
-// R' form (value < 16p) -> R-form words, value < 2p: x' 2^256 / 2^261 = x 2^256
-TA_HD void to32(const F29& x, uint32_t* w) {
-  F29 c;
+// R-form words (x~ < 2^255) -> R' form x' = x~ 2^5 - q p, value < 3p: no
+// product, the quotient estimated from the top two limbs.  With v = x~ << 5
+// and v_hi = v >> 203, v_hi / (p_hi + 1) <= v / p < v_hi / (p_hi + 1) + 2^-40,
+// so the float estimate (relative error < 2^-21, times q < 64) minus one is
+// q* - 2 .. q*, q* = floor(v / p): 0 <= v - q p < 3p.
+constexpr float kInvPhi = 1.0f / 1702635872462389.0f;  // 1 / (p >> 203 + 1)
+TA_HD F29 from32(const uint32_t* w) {
+  const F29 v = shl5_repack(w);
+  const float vf = (float)v.l[8] * 536870912.0f + (float)v.l[7];
+  int q = (int)(vf * kInvPhi) - 1;
+  q = q < 0 ? 0 : q;
+  F29 r;
+  int64_t carry = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) c.l[i] = 0;
-  c.l[8] = 1u << 24;  // 2^256
-  repack32(mul(x, c), w);
+  for (int i = 0; i < 9; ++i) {
+    const int64_t t = (int64_t)v.l[i] - (int64_t)q * kP29[i] + carry;
+    r.l[i] = i < 8 ? (uint32_t)t & kM29 : (uint32_t)t;
+    carry = t >> 29;  // arithmetic: the borrow
+  }
+  return r;
+}
+// R' form (N-form, value < 16p) -> R-form words, value < 2p: x' 2^-5 =
+// (x' + k p) / 32 with k = -x' p^-1 mod 32 (p = 7 mod 32, -7^-1 = 9 mod 32):
+// < (16 + 31) p / 32.  One digit of a Montgomery reduction by 2^5.
+TA_HD void to32(const F29& x, uint32_t* w) {
+  const uint32_t k = (x.l[0] * 9u) & 31u;
+  F29 v;
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint64_t t = (uint64_t)x.l[i] + (uint64_t)k * kP29[i] + carry;
+    v.l[i] = i < 8 ? (uint32_t)t & kM29 : (uint32_t)t;
+    carry = t >> 29;
+  }
+  repack32<5>(v, w);
 }
 
 // x = 0 (mod p) for an N-form x < 32p: x = k p exactly for some k < 32, so

@@ -31,8 +31,10 @@ namespace tachyon_amd::msm {
 constexpr int kMsmVariantMask = 0x7FFBF;
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
-// staging in the recode scatter
-constexpr unsigned kSchedFusedRecode = 1, kSchedRecodeFedSort = 2, kSchedNarrowStaging = 4;
+// staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
+// G2 accumulation
+constexpr unsigned kSchedFusedRecode = 1, kSchedRecodeFedSort = 2, kSchedNarrowStaging = 4, kSchedAcc29 = 8,
+                   kSchedLanePair = 16;
 
 struct MsmPlan {
   unsigned c = 0;        // window bits
@@ -204,8 +206,8 @@ class MsmGpu {
   bool rocprim_hist_ = false;  // rocPRIM's digit histogram pass instead of the recode's counts (bit 10)
   bool wide_stage_ = false;    // 8-byte entries in the recode scatter's LDS staging (bit 11)
   bool tree_reduce_ = false;   // window sums by workgroup trees (bit 12)
-  bool acc29_ = false;         // BN254 G1 accumulation over 29-bit limbs (bit 13)
-  int acc29_mode_ = 1;         // ... next base: 1 in registers, 0 not prefetched (bit 14), 2 via LDS-DMA (bit 17)
+  bool acc29_ = false;         // BN254 G1 accumulation over 29-bit limbs (default; bit 18: FIPS 32-bit)
+  int acc29_mode_ = 0;         // ... next base: 0 not prefetched, 1 in registers (bit 13), 2 via LDS-DMA (bit 17)
   bool pair_acc_ = false;      // G2 accumulation with a lane pair per point (bit 15)
   bool pair_inline_ = false;   // ... its 12-limb products inline (bit 16)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)

@@ -1193,7 +1193,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
-      if (acc29_)  // 29-bit-limb accumulation (set_variant bit 13, A/B; bit 14: without the base prefetch)
+      if (acc29_) last_schedule_ |= kSchedAcc29;
+      if (acc29_)  // 29-bit-limb accumulation (BN254 G1 default; set_variant bits 13 / 17: base prefetch A/B)
         hipLaunchKernelGGL(acc29_mode_ == 2 ? seg_acc29_kernel<2> : acc29_mode_ == 1 ? seg_acc29_kernel<1>
                                                                             : seg_acc29_kernel<0>,
                            dim3(grid_for(Tg)),
@@ -1209,6 +1210,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       constexpr bool kCallDefault = Curve::F::Base::N == 12;
       auto* pair_kernel = pair_inline_ ? &seg_acc_pair_kernel<Curve, false> : &seg_acc_pair_kernel<Curve, kCallDefault>;
       // (kCallDefault is false for 8-limb fields: both entries are the inline kernel there)
+      if (pair_acc_) last_schedule_ |= kSchedLanePair;
       if (pair_acc_)
         hipLaunchKernelGGL(pair_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
                            ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum,
@@ -1360,15 +1362,15 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
   wide_stage_ = (variant_ & 2048) != 0;    // bit 11: 8-byte LDS staging in the recode scatter (A/B)
   tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
-  // bits 13 / 14 / 17: BN254 G1 accumulation over 29-bit limbs with the next
-  // base prefetched in registers / not prefetched / prefetched through LDS (A/B)
-  // Default: the 29-bit field for BN254 G1 at >= 2^29 (point, window) entries
-  // (the 2^26 headline: accumulation 67.7 -> 65.5 ms; at 2^24 it measured
-  // 2 % slower and stays off -- profiles/r03a/ab_acc29_fips32.log); bit 18
-  // forces the 32-bit FIPS field at every size
-  const bool acc29_default = std::is_same_v<Curve, Bn254G1> && (size_t)n * plan.active() >= (size_t(1) << 29);
+  // BN254 G1 accumulates over the 29-bit-limb field with hand-chained products
+  // (field/f29_asm.h) and product-free conversions, the next base not
+  // prefetched (3 waves per SIMD): 2^26 accumulation 67.3 -> 61.0 ms, faster
+  // at every size from 2^16 (profiles/r03b/ab_acc29_conv.log).  Bit 18 forces
+  // the 32-bit FIPS field; bits 13 / 17 prefetch the next base in registers
+  // (2 waves) / through LDS by LDS-DMA (A/B); bit 14 is the default
+  const bool acc29_default = std::is_same_v<Curve, Bn254G1>;
   acc29_ = !(variant_ & 262144) && ((variant_ & (8192 | 16384 | 131072)) != 0 || acc29_default);
-  acc29_mode_ = (variant_ & 131072) ? 2 : (variant_ & 16384) ? 0 : 1;
+  acc29_mode_ = (variant_ & 131072) ? 2 : (variant_ & 8192) ? 1 : 0;
   // G2: a lane pair per point with inline products by default (BLS12-381 G2
   // 2^24 accumulation 129 -> 113 ms, BN254 G2 2^22 16.3 -> 15.7 ms); bit 15
   // restores the one-lane kernel, bit 16 the pair with out-of-line 12-limb products

@@ -1,0 +1,143 @@
+"""The 9 x 29-bit BN254 Fq field of the G1 bucket accumulation
+(tachyon_amd/csrc/field/f29.h), host build: every operation checked against
+Python integers -- values mod p, the N-form limb shape and the value bounds
+the madd bound analysis (msm_impl.h, namespace acc29) relies on.  The device
+products (field/f29_asm.h) are the generator's output of the same columns;
+they are pinned here against tools/gen_f29_asm.py and on the GPU by the MSM
+golden tests (tests/test_gpu_msm.py, variant 8192)."""
+import importlib.util
+import os
+import random
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47
+R1 = pow(2, 261, P)  # R' = 2^261
+M29 = (1 << 29) - 1
+
+HARNESS = r"""
+#include <cstdio>
+#include <cstring>
+#include "f29.h"
+using namespace tachyon_amd::f29;
+static void rd(F29& x) { for (int i = 0; i < 9; ++i) scanf("%u", &x.l[i]); }
+static void wr(const F29& x) { for (int i = 0; i < 9; ++i) printf("%u ", x.l[i]); printf("\n"); }
+int main() {
+  char op[32];
+  while (scanf("%31s", op) == 1) {
+    F29 a, b, c, d;
+    if (!strcmp(op, "from32")) { uint32_t w[8]; for (int i = 0; i < 8; ++i) scanf("%u", &w[i]); wr(from32(w)); }
+    else if (!strcmp(op, "to32")) { rd(a); uint32_t w[8]; to32(a, w); for (int i = 0; i < 8; ++i) printf("%u ", w[i]); printf("\n"); }
+    else if (!strcmp(op, "mul")) { rd(a); rd(b); wr(mul(a, b)); }
+    else if (!strcmp(op, "mul_add")) { rd(a); rd(b); rd(c); wr(mul_add(a, b, c)); }
+    else if (!strcmp(op, "mul2_add")) { rd(a); rd(b); rd(c); rd(d); wr(mul2_add(a, b, c, d)); }
+    else if (!strcmp(op, "sqr")) { rd(a); wr(sqr(a)); }
+    else if (!strcmp(op, "sqr_add")) { rd(a); rd(b); wr(sqr_add(a, b)); }
+    else if (!strcmp(op, "iszero")) { rd(a); printf("%d\n", (int)is_zero_mod_p(a)); }
+  }
+  return 0;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    d = tmp_path_factory.mktemp("f29")
+    src, exe = d / "h.cpp", d / "h"
+    src.write_text(HARNESS)
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(ROOT, "tachyon_amd", "csrc", "field"),
+                    str(src), "-o", str(exe)], check=True)
+
+    def run(lines):
+        out = subprocess.run([str(exe)], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                             check=True).stdout.split("\n")
+        return [[int(t) for t in ln.split()] for ln in out[:len(lines)]]
+    return run
+
+
+def limbs(v):
+    """N-form limbs of v (limbs 0..7 exact, limb 8 the rest)."""
+    return [(v >> (29 * i)) & M29 for i in range(8)] + [v >> 232]
+
+
+def value(ls):
+    return sum(x << (29 * i) for i, x in enumerate(ls))
+
+
+def words(v):
+    return [(v >> (32 * i)) & 0xFFFFFFFF for i in range(8)]
+
+
+def n_form(ls):
+    return all(x <= M29 for x in ls[:8]) and ls[8] < (1 << 32)
+
+
+def fmt(op, *xs):
+    return " ".join([op] + [str(t) for x in xs for t in x])
+
+
+def test_from32_to32(harness):
+    rng = random.Random(1)
+    xs = [0, 1, P - 1, P, 2 * P - 1, (1 << 254) - 1] + [rng.randrange(2 * P) for _ in range(300)]
+    out = harness([fmt("from32", words(x)) for x in xs])
+    for x, r in zip(xs, out):
+        assert n_form(r)
+        v = value(r)
+        assert v < 3 * P and v % P == (x << 5) % P
+    ys = [0, 1, P, 16 * P - 1] + [rng.randrange(16 * P) for _ in range(300)]
+    ys += [value(limbs(y)) | ((1 << 29) - 1) for y in ys[:20]]  # all-ones low limbs
+    ys = [y for y in ys if y < 16 * P]
+    out = harness([fmt("to32", limbs(y)) for y in ys])
+    for y, w in zip(ys, out):
+        v = sum(t << (32 * i) for i, t in enumerate(w))
+        assert v < 2 * P and v % P == (y * pow(2, -5, P)) % P
+
+
+def test_products(harness):
+    rng = random.Random(2)
+    inv = pow(R1, -1, P)
+    cases = []
+    for _ in range(200):
+        a, b, c, d, e = (rng.randrange(10 * P) for _ in range(5))
+        cases.append((a, b, c, d, e))
+    cases.append((0, 0, 0, 0, 0))
+    cases.append((10 * P - 1,) * 5)
+    lines = []
+    for a, b, c, d, e in cases:
+        A, B, C, D, E = map(limbs, (a, b, c, d, e))
+        lines += [fmt("mul", A, B), fmt("mul_add", A, B, E), fmt("mul2_add", A, B, C, D), fmt("sqr", A),
+                  fmt("sqr_add", A, E)]
+    out = harness(lines)
+    for i, (a, b, c, d, e) in enumerate(cases):
+        want = [a * b * inv, a * b * inv + e, (a * b + c * d) * inv, a * a * inv, a * a * inv + e]
+        bound = [a * b / 2**261 + P, a * b / 2**261 + P + e, (a * b + c * d) / 2**261 + P,
+                 a * a / 2**261 + P, a * a / 2**261 + P + e]
+        for k in range(5):
+            r = out[5 * i + k]
+            assert n_form(r), (i, k)
+            assert value(r) % P == want[k] % P, (i, k)
+            assert value(r) < bound[k], (i, k)
+
+
+def test_is_zero(harness):
+    rng = random.Random(3)
+    xs = [k * P for k in range(32)] + [k * P + 1 for k in range(32)] + [rng.randrange(32 * P) for _ in range(100)]
+    out = harness([fmt("iszero", limbs(x)) for x in xs])
+    for x, r in zip(xs, out):
+        assert r[0] == int(x % P == 0)
+
+
+def test_asm_header_matches_generator():
+    spec = importlib.util.spec_from_file_location("gen_f29_asm", os.path.join(ROOT, "tools", "gen_f29_asm.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    with open(os.path.join(ROOT, "tachyon_amd", "csrc", "field", "f29_asm.h")) as f:
+        text = f.read()
+    assert text == mod.render()
+    # 9 x 9 products + 9 x 9 reduction mads per column set; mul2 has 81 more
+    per = {"mul": 162, "mul_add": 162, "mul2": 243, "mul2_add": 243, "sqr": 126, "sqr_add": 126}
+    for fn, n in per.items():
+        body = text.split(f"F29 {fn}(", 1)[1].split("\n}\n", 1)[0]
+        assert body.count("v_mad_u64_u32") == n, fn

@@ -345,6 +345,11 @@ def test_msm_schedule_variants_agree(curve, logn):
             if v in want:
                 s = m.last_schedule()
                 assert (s["fused_recode"], s["recode_fed_sort"], s["narrow_staging"]) == want[v], (hex(v), s)
+            s = m.last_schedule()
+            if curve == "bn254_g1":  # the 29-bit field by default; bit 18 the FIPS 32-bit field
+                assert s["acc29"] == (v != 262144), (hex(v), s)
+            else:  # G2: the lane pair by default; bit 15 the one-lane kernel
+                assert s["lane_pair"] == (v != 32768), (hex(v), s)
         for bad in (64, 1 << 19):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
