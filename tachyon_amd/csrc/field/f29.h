@@ -212,8 +212,7 @@ TA_HD void repack32(const F29& x, uint32_t* w) {
 // so the float estimate (relative error < 2^-21, times q < 64) minus one is
 // q* - 2 .. q*, q* = floor(v / p): 0 <= v - q p < 3p.
 constexpr float kInvPhi = 1.0f / 1702635872462389.0f;  // 1 / (p >> 203 + 1)
-TA_HD F29 from32(const uint32_t* w) {
-  const F29 v = shl5_repack(w);
+TA_HD F29 reduce_shl5(const F29& v) {
   const float vf = (float)v.l[8] * 536870912.0f + (float)v.l[7];
   int q = (int)(vf * kInvPhi) - 1;
   q = q < 0 ? 0 : q;
@@ -221,12 +220,13 @@ TA_HD F29 from32(const uint32_t* w) {
   int64_t carry = 0;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    const int64_t t = (int64_t)v.l[i] - (int64_t)q * kP29[i] + carry;
+    const int64_t t = (int64_t)(-q) * (int64_t)(int32_t)kP29[i] + ((int64_t)v.l[i] + carry);  // v_mad_i64_i32
     r.l[i] = i < 8 ? (uint32_t)t & kM29 : (uint32_t)t;
     carry = t >> 29;  // arithmetic: the borrow
   }
   return r;
 }
+TA_HD F29 from32(const uint32_t* w) { return reduce_shl5(shl5_repack(w)); }
 // R' form (N-form, value < 16p) -> R-form words, value < 2p: x' 2^-5 =
 // (x' + k p) / 32 with k = -x' p^-1 mod 32 (p = 7 mod 32, -7^-1 = 9 mod 32):
 // < (16 + 31) p / 32.  One digit of a Montgomery reduction by 2^5.

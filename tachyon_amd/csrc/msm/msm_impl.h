@@ -434,8 +434,9 @@ struct Acc {
   F29 x, y, zz, zzz;
 };
 
-__device__ __forceinline__ Acc from_affine(const Affine<Bn254Fq>& a) {
-  return {from32(a.x.v), from32(a.y.v), konst(kOne29), konst(kOne29)};
+// the first point of a run, from its coordinates already shifted for madd
+__device__ __forceinline__ Acc from_shifted(const F29& x2, const F29& y2) {
+  return {reduce_shl5(x2), reduce_shl5(y2), konst(kOne29), konst(kOne29)};
 }
 __device__ __forceinline__ XYZZ<Bn254Fq> to_xyzz(const Acc& a) {
   XYZZ<Bn254Fq> r;
@@ -504,9 +505,18 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
   const uint32_t prev_b = g0 > gbeg ? bucket_of_key(entry_key(ents[g0 - 1])) : kNoBucket;
   const uint32_t next_b = (g1 < gend) ? bucket_of_key(entry_key(ents[g1])) : kNoBucket;
   uint32_t flags = 0, runs = 0, cur = kNoBucket;
-  Acc acc;
+  Acc acc{};  // (any defined value: the stores mask it while acc_zero)
   bool acc_zero = true;
-  auto stored = [&]() { return acc_zero ? XYZZ<Bn254Fq>::zero() : to_xyzz(acc); };
+  auto stored = [&]() {  // the identity is zz = zzz = 0 (x, y are not read)
+    XYZZ<Bn254Fq> s = to_xyzz(acc);
+    const uint32_t keep = acc_zero ? 0u : ~0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s.zz.v[i] &= keep;
+      s.zzz.v[i] &= keep;
+    }
+    return s;
+  };
   uint64_t e0 = ents[g0];
   uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
   Affine<Bn254Fq> P;
@@ -554,12 +564,13 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
       }
       if (!P.is_zero_canonical()) {
         P.y = P.y.cond_neg_canonical(v0 & kSignBit);
+        const F29 x2 = shl5_repack(P.x.v), y2 = shl5_repack(P.y.v);  // both paths
         if (acc_zero) {
-          acc = from_affine(P);
+          acc = from_shifted(x2, y2);
           acc_zero = false;
         } else {
           int special = 0;
-          const Acc nxt = madd(acc, shl5_repack(P.x.v), shl5_repack(P.y.v), &special);
+          const Acc nxt = madd(acc, x2, y2, &special);
           if (special == 0) acc = nxt;
           else if (special == 1) acc_zero = true;
           else acc = dbl_slow(acc);
