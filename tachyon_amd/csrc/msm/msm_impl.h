@@ -570,10 +570,9 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
           acc_zero = false;
         } else {
           int special = 0;
-          const Acc nxt = madd(acc, x2, y2, &special);
-          if (special == 0) acc = nxt;
-          else if (special == 1) acc_zero = true;
-          else acc = dbl_slow(acc);
+          acc = madd(acc, x2, y2, &special);  // (unchanged when special)
+          if (special == 1) acc_zero = true;
+          else if (special == 2) acc = dbl_slow(acc);
         }
       }
     }
