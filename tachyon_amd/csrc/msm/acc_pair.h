@@ -153,4 +153,60 @@ __device__ __forceinline__ Acc<H> dbl(const Acc<H>& A, bool h) {
   return c;
 }
 
+// The identity (1, 1, 0, 0): this lane's components (Fq2 one = 1 + 0 u)
+template <class H>
+__device__ __forceinline__ Acc<H> zero(bool h) {
+  using F = decltype(H{}.v);
+  const H one{h ? F::zero() : F::one()}, nil{F::zero()};
+  return {one, one, nil, nil};
+}
+
+// add-2008-s (point_xyzz_impl.h:45-97) on lane-pair values, identities
+// (zz = 0) handled: the bucket / window reduction's point sum
+template <class H>
+__device__ __forceinline__ Acc<H> add(const Acc<H>& A, const Acc<H>& B, bool h) {
+  if (A.zz.is_zero()) return B;
+  if (B.zz.is_zero()) return A;
+  const H u1 = A.x.mul(B.zz, h), s1 = A.y.mul(B.zzz, h);
+  const H p = B.x.mul(A.zz, h) - u1;
+  const H r = B.y.mul(A.zzz, h) - s1;
+  if (p.is_zero()) return r.is_zero() ? dbl(A, h) : zero<H>(h);
+  const H pp = p.sqr(h);
+  const H ppp = p.mul(pp, h);
+  const H q = u1.mul(pp, h);
+  Acc<H> c;
+  c.x = r.sqr(h) - ppp - q.dbl();
+  c.y = r.mul(q - c.x, h) - s1.mul(ppp, h);
+  c.zz = A.zz.mul(B.zz, h).mul(pp, h);
+  c.zzz = A.zzz.mul(B.zzz, h).mul(ppp, h);
+  return c;
+}
+
+// m P for a small m (double-and-add from the top bit)
+template <class H>
+__device__ __forceinline__ Acc<H> small_mul(const Acc<H>& P, uint32_t m, bool h) {
+  if (m == 0 || P.zz.is_zero()) return zero<H>(h);
+  Acc<H> r = P;
+  for (int bit = 30 - __builtin_clz(m); bit >= 0; --bit) {
+    r = dbl(r, h);
+    if ((m >> bit) & 1) r = add(r, P, h);
+  }
+  return r;
+}
+
+// point i of an XYZZ<Fq2> array: this lane's components (x0 x1 y0 y1 zz0 ...)
+template <class H, class Fb>
+__device__ __forceinline__ Acc<H> load(const Fb* pts, size_t i, uint32_t h) {
+  const Fb* o = pts + 8 * i;
+  return {H{o[h]}, H{o[2 + h]}, H{o[4 + h]}, H{o[6 + h]}};
+}
+template <class H, class Fb>
+__device__ __forceinline__ void store(Fb* pts, size_t i, uint32_t h, const Acc<H>& a) {
+  Fb* o = pts + 8 * i;
+  o[h] = a.x.v;
+  o[2 + h] = a.y.v;
+  o[4 + h] = a.zz.v;
+  o[6 + h] = a.zzz.v;
+}
+
 }  // namespace tachyon_amd::msm::pair

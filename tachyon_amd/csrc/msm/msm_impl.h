@@ -674,10 +674,9 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typen
           acc_zero = false;
         } else {
           int special = 0;
-          const Acc<H> nxt = madd(acc, px, py, h != 0, &special);
-          if (special == 0) acc = nxt;
-          else if (special == 1) acc_zero = true;
-          else acc = pair::dbl(acc, h != 0);
+          acc = madd(acc, px, py, h != 0, &special);  // (unchanged when special)
+          if (special == 1) acc_zero = true;
+          else if (special == 2) acc = pair::dbl(acc, h != 0);
         }
       }
     }
@@ -837,6 +836,83 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_segment
   }
   acc = acc + small_mul(R, j * L);
   reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
+}
+
+// The G2 reductions with a lane pair per point (acc_pair.h): the one-lane
+// XYZZ<Fq2> additions hold two points and their temporaries (BLS12-381:
+// 220-460 spilled VGPRs per kernel, 21 ms of a 2^24 MSM); split by component
+// they stay in registers.  Same schedules as the one-lane kernels above.
+template <class Curve>
+struct PairTypes {
+  using Fb = typename Curve::F::Base;
+  using H = pair::Half<HotFp<Fb>, Fb::N == 12>;
+  using A = pair::Acc<H>;
+};
+
+template <class Curve>
+__global__ __launch_bounds__(kBlock, 2) void seg_reduce_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
+                                                                 const uint32_t* __restrict__ beg,
+                                                                 const uint32_t* __restrict__ end,
+                                                                 const uint32_t* __restrict__ out_off, uint32_t nseg,
+                                                                 unsigned K2, XYZZ<typename Curve::F>* __restrict__ out,
+                                                                 const uint32_t* __restrict__ bucket,
+                                                                 XYZZ<typename Curve::F>* __restrict__ bucket_sum) {
+  using T = PairTypes<Curve>;
+  using Fb = typename T::Fb;
+  using H = typename T::H;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= out_off[nseg]) return;  // both lanes of the pair
+  const uint32_t s = find_segment(out_off, nseg, t);
+  const uint32_t e0 = beg[s] + (t - out_off[s]) * K2;
+  const uint32_t e1 = min(end[s], e0 + K2);
+  const Fb* src = reinterpret_cast<const Fb*>(in);
+  pair::Acc<H> acc = pair::load<H>(src, e0, h);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = pair::add(acc, pair::load<H>(src, e, h), h != 0);
+  if (bucket) pair::store(reinterpret_cast<Fb*>(bucket_sum), bucket[s], h, acc);
+  else pair::store(reinterpret_cast<Fb*>(out), t, h, acc);
+}
+
+template <class Curve>
+__global__ __launch_bounds__(kBlock, 2) void window_segment_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+                                                                     unsigned W, unsigned B, unsigned L,
+                                                                     XYZZ<typename Curve::F>* __restrict__ out) {
+  using T = PairTypes<Curve>;
+  using Fb = typename T::Fb;
+  using H = typename T::H;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t S = B / L;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W * S) return;
+  const uint32_t w = t / S, j = t - w * S;
+  const Fb* bs = reinterpret_cast<const Fb*>(bucket_sum);
+  const size_t b0 = (size_t)w * B + (size_t)j * L;
+  pair::Acc<H> R = pair::zero<H>(h != 0), acc = R;
+  for (int k = (int)L - 1; k >= 0; --k) {
+    R = pair::add(R, pair::load<H>(bs, b0 + k, h), h != 0);
+    acc = pair::add(acc, R, h != 0);
+  }
+  acc = pair::add(acc, pair::small_mul(R, j * L, h != 0), h != 0);
+  pair::store(reinterpret_cast<Fb*>(out), t, h, acc);
+}
+
+template <class Curve>
+__global__ __launch_bounds__(kBlock, 2) void reduce_uniform_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
+                                                                     unsigned W, unsigned S_in, unsigned K2,
+                                                                     XYZZ<typename Curve::F>* __restrict__ out) {
+  using T = PairTypes<Curve>;
+  using Fb = typename T::Fb;
+  using H = typename T::H;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t S_out = (S_in + K2 - 1) / K2;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W * S_out) return;
+  const uint32_t w = t / S_out, q = t - w * S_out;
+  const uint32_t e0 = q * K2, e1 = min(S_in, e0 + K2);
+  const Fb* src = reinterpret_cast<const Fb*>(in) + (size_t)8 * w * S_in;
+  pair::Acc<H> acc = pair::load<H>(src, e0, h);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = pair::add(acc, pair::load<H>(src, e, h), h != 0);
+  pair::store(reinterpret_cast<Fb*>(out), t, h, acc);
 }
 
 // Window reduction, stage 2: sum K2 consecutive segment sums per window.
@@ -1240,6 +1316,20 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   }
   if (profile_) TA_HIP(hipEventRecord(ev_[4], stream_));        // last accumulation done
 
+  // G2: the lane-pair reductions with the lane-pair accumulation (set_variant bit 15 restores both)
+  constexpr bool kG2 = std::is_same_v<Curve, Bn254G2> || std::is_same_v<Curve, Bls381G2>;
+  const bool pair_reduce = kG2 && pair_acc_;
+  const unsigned lanes = pair_reduce ? 2 : 1;  // threads per point
+  auto* seg_reduce = &seg_reduce_kernel<Curve>;
+  auto* win_segment = &window_segment_kernel<Curve>;
+  auto* win_reduce = &reduce_uniform_kernel<Curve>;
+  if constexpr (kG2) {
+    if (pair_reduce) {
+      seg_reduce = &seg_reduce_pair_kernel<Curve>;
+      win_segment = &window_segment_pair_kernel<Curve>;
+      win_reduce = &reduce_uniform_pair_kernel<Curve>;
+    }
+  }
   // ---- join buckets that cross thread boundaries ----
   hipLaunchKernelGGL(chain_mark_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, stream_, tflags, (uint32_t)T,
                      is_start);
@@ -1276,8 +1366,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
                                      rocprim::plus<uint32_t>(), stream_));
       size_t out_items = cur_items / plan.K2 + nchains + 1;
       Point* dst = dst_bufs[l & 1];
-      hipLaunchKernelGGL(seg_reduce_kernel<Curve>, dim3(grid_for(out_items)), dim3(kBlock), 0, stream_, cur, cur_beg,
-                         cur_end, loff, nchains, plan.K2, dst, last ? cbucket : nullptr, bucket_sum);
+      hipLaunchKernelGGL(seg_reduce, dim3(grid_for(lanes * out_items)), dim3(kBlock), 0, stream_, cur, cur_beg, cur_end,
+                         loff, nchains, plan.K2, dst, last ? cbucket : nullptr, bucket_sum);
       TA_HIP(hipGetLastError());
       if (!last) {
         // next level reads this level's compact output: segment s = [loff[s], loff[s+1])
@@ -1324,8 +1414,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   unsigned S = B / plan.seg;
   Point* seg_a = static_cast<Point*>(seg_a_.ensure((size_t)W * S * sizeof(Point)));
   Point* seg_b = static_cast<Point*>(seg_b_.ensure((size_t)W * S * sizeof(Point)));
-  hipLaunchKernelGGL(window_segment_kernel<Curve>, dim3(grid_for((size_t)W * S)), dim3(kBlock), 0, stream_,
-                     bucket_sum, W, B, plan.seg, seg_a);
+  hipLaunchKernelGGL(win_segment, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, bucket_sum, W, B,
+                     plan.seg, seg_a);
   TA_HIP(hipGetLastError());
   Point* s_cur = seg_a;
   Point* s_nxt = seg_b;
@@ -1336,8 +1426,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   while (S > 1) {
     unsigned S_out = (S + KW - 1) / KW;
     Point* dst = (S_out == 1) ? d_windows : s_nxt;
-    hipLaunchKernelGGL(reduce_uniform_kernel<Curve>, dim3(grid_for((size_t)W * S_out)), dim3(kBlock), 0, stream_,
-                       s_cur, W, S, KW, dst);
+    hipLaunchKernelGGL(win_reduce, dim3(grid_for(lanes * (size_t)W * S_out)), dim3(kBlock), 0, stream_, s_cur, W, S,
+                       KW, dst);
     TA_HIP(hipGetLastError());
     std::swap(s_cur, s_nxt);
     S = S_out;
