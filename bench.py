@@ -44,11 +44,15 @@ SEED = 0x7AC40001
 MULMOD_PEAK_G = 138.6
 MULMOD_PEAK_NOTE = ("measured BN254 FIPS Montgomery-product ceiling of the chip, 138.6 G/s with >= 2 "
                     "independent chains per lane or >= 4 waves/SIMD (tools/microbench/mulmod_rates.hip)")
-# madd-2008-s (point_xyzz_impl.h:129-176): 8 multiplications + 2 squarings, in
-# 256-bit Montgomery-product equivalents of v_mad_u64_u32 work (128 each): 6
-# products, the y coordinate's fused a*b - c*d (192 = 2 products, one
-# reduction) and 2 FIPS squares (100 each) -> 1160 / 128 = 9.06
-MADD_MULMODS = (6 * 128 + 192 + 2 * 100) / 128
+# The accumulation's VALU roofline: mixed additions (madd-2008-s,
+# point_xyzz_impl.h:129-176) per second against the chip's ceiling for the same
+# field code measured in registers with no gathers or run logic
+# (tools/microbench/madd_rates.hip, 3 waves/SIMD; profiles/r03c/madd_rates.log):
+# the 29-bit-limb field of the BN254 G1 accumulation, and the 32-bit FIPS field
+# (set_variant bit 18).
+MADD_PEAK_G = {"seg_acc29_kernel": 19.40, "seg_acc_kernel": 13.67}
+MADD_PEAK_NOTE = ("mixed additions/s of the same field code in registers, no gathers or run logic "
+                  "(tools/microbench/madd_rates.hip, whole chip, 3 waves/SIMD)")
 
 
 def pmc_traffic(kernel):
@@ -475,8 +479,9 @@ def main():
     acc_gbs = points_per_launch * MSM_BYTES_PER_POINT / (acc_ms * 1e-3) / 1e9
     units = n * rank_windows / launches  # mixed additions (point, window) per launch
     gather_gbs = units * (64 + 8) / (acc_ms * 1e-3) / 1e9
-    acc_traffic, acc_traffic_src, acc_traffic_raw = pmc_traffic("seg_acc_kernel")
-    acc_gmulmod = units * MADD_MULMODS / (acc_ms * 1e-3) / 1e9
+    acc_kernel = "seg_acc29_kernel" if msm.last_schedule()["acc29"] else "seg_acc_kernel"
+    acc_traffic, acc_traffic_src, acc_traffic_raw = pmc_traffic(acc_kernel)
+    acc_gmadd = units / (acc_ms * 1e-3) / 1e9
     stream_gbs = stream_copy_gbs()
 
     out = {
@@ -510,7 +515,7 @@ def main():
                                            "+ WRITE_SIZE; the 64-B base gathers are an uncalibrated width, so the "
                                            "uncorrected FETCH_SIZE is given as traffic_fetch_raw",
                      "pmc_gbs": (acc_traffic / (acc_ms * 1e-3)) if acc_traffic else None,
-                     "kernel": "seg_acc_kernel (bucket accumulation)", "kernel_ms": acc_ms,
+                     "kernel": f"{acc_kernel} (bucket accumulation)", "kernel_ms": acc_ms,
                      "launches_per_msm": launches, "points_per_launch": points_per_launch,
                      "algorithmic_bytes_per_launch": points_per_launch * MSM_BYTES_PER_POINT,
                      "gather_gbs": gather_gbs, "gathers_per_launch": units,
@@ -518,14 +523,13 @@ def main():
                      "note": "algorithmic bytes = SURVEY 8(d)'s 96 B per point (base + scalar read once) x the n "
                              "points one launch covers / the launch's HIP-event time; gather_gbs = the W x (64 B "
                              "base + 8 B entry) per point the kernel gathers; the kernel is VALU-bound "
-                             "(v_mad_u64_u32, valu_roofline), see DESIGN.md; peak = the guide's nominal 8 TB/s, "
+                             "(valu_roofline), see DESIGN.md; peak = the guide's nominal 8 TB/s, "
                              "stream_copy_gbs = a device-to-device copy measured on this box"},
         "msm_phase_ms": phases,
-        "valu_roofline": {"bound": "valu", "kernel": "seg_acc_kernel", "achieved": acc_gmulmod,
-                          "peak": MULMOD_PEAK_G, "unit": "G mulmod/s", "frac": acc_gmulmod / MULMOD_PEAK_G,
-                          "note": "n x windows mixed additions x 9.06 Montgomery-product equivalents (6 products, "
-                                  "a fused a*b - c*d, 2 squares: 1160 v_mad_u64_u32) per launch / launch time; "
-                                  "peak = " + MULMOD_PEAK_NOTE},
+        "valu_roofline": {"bound": "valu", "kernel": acc_kernel, "achieved": acc_gmadd,
+                          "peak": MADD_PEAK_G[acc_kernel], "unit": "G mixed additions/s",
+                          "frac": acc_gmadd / MADD_PEAK_G[acc_kernel],
+                          "note": "n x windows mixed additions per launch / launch time; peak = " + MADD_PEAK_NOTE},
     }
 
     # ---- configs[1] sweep (2^16, 2^20 .. 2^24: prefixes of the same device-resident input) ----

@@ -3,9 +3,11 @@
 directory, per-kernel averages of every counter (per dispatch), plus the
 derived figures DESIGN.md quotes: VALU instructions per dispatch, INT64 share,
 VALU-active fraction of the wave cycles, resident waves per SIMD
-(MeanOccupancyPerCU / 4), per-SIMD VALU issue utilisation from the instruction
-mix (INT64 = v_mad_u64_u32-class at 4 SIMD cycles per wave64 instruction, other
-VALU at 2) over the dispatch's SIMD-cycles (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs... per XCD 128)."""
+(MeanOccupancyPerCU / 4), the effective clock (GRBM_GUI_ACTIVE is summed over
+the 8 XCDs: / 8 / dispatch time from the kernel trace) and the per-SIMD VALU
+issue utilisation 4 x SQ_INSTS_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): a
+wave64 VALU instruction holds its SIMD for 4 cycles (profiles/r03c: the
+in-register madd microbenchmark issues at 99 % of that at 2.36 GHz)."""
 import collections
 import csv
 import json
@@ -30,8 +32,20 @@ def stats(d, sub):
     print()
 
 
-def pmc(d, sub, want=("seg_acc_kernel", "seg_acc29_kernel", "dif_pass_kernel", "rocprim::onesweep_iteration",
-                      "recode_scatter_kernel", "recode_hist_kernel", "window_segment_kernel")):
+def trace_ms(d):
+    """average dispatch ms per short kernel name over the trace passes"""
+    ms = {}
+    for sub in ("trace", "g2_trace"):
+        p = os.path.join(d, sub, "run_kernel_stats.csv")
+        if os.path.exists(p):
+            for r in csv.DictReader(open(p)):
+                ms.setdefault(short(r["Name"]), float(r["AverageNs"]) / 1e6)
+    return ms
+
+
+def pmc(d, sub, want=("seg_acc_kernel", "seg_acc29_kernel", "seg_acc_pair_kernel", "dif_pass_kernel",
+                      "rocprim::onesweep_iteration", "recode_scatter_kernel", "recode_hist_kernel",
+                      "window_segment", "seg_reduce", "k29", "k32")):
     p = os.path.join(d, sub, "run_counter_collection.csv")
     if not os.path.exists(p):
         return {}
@@ -58,11 +72,11 @@ def derived(c):
         r["int64_share"] = c["SQ_INSTS_VALU_INT64"] / max(1.0, c["SQ_INSTS_VALU"])
     if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c:
         r["valu_active_per_wave_cycle"] = c["SQ_ACTIVE_INST_VALU"] / max(1.0, c["SQ_WAVE_CYCLES"])
-    if "GRBM_GUI_ACTIVE" in c and "SQ_INSTS_VALU" in c and "SQ_INSTS_VALU_INT64" in c:
+    if "GRBM_GUI_ACTIVE" in c and "SQ_INSTS_VALU" in c:
         gui = c["GRBM_GUI_ACTIVE"] / 8  # per-XCD cycles of the dispatch (rocprofv3 sums the 8 XCDs)
-        simd_cycles = gui * 1024
-        issue = 4 * c["SQ_INSTS_VALU_INT64"] + 2 * (c["SQ_INSTS_VALU"] - c["SQ_INSTS_VALU_INT64"])
-        r["simd_valu_util_model"] = issue / max(1.0, simd_cycles)
+        r["simd_valu_issue_util"] = 4 * c["SQ_INSTS_VALU"] / max(1.0, gui * 1024)
+        if c.get("avg_ms"):
+            r["clock_ghz"] = gui / (c["avg_ms"] * 1e6)
     if "MeanOccupancyPerCU" in c:
         r["waves_per_simd"] = c["MeanOccupancyPerCU"] / 4
     return r
@@ -73,8 +87,13 @@ def main(d):
     for sub in ("trace", "g2_trace"):
         stats(d, sub)
     res = {}
-    for sub in ("fetch", "write", "valu", "occ", "g2_fetch", "g2_write", "g2_valu", "ab_valu", "ab_occ"):
+    ms = trace_ms(d)
+    for sub in ("fetch", "write", "valu", "occ", "g2_fetch", "g2_write", "g2_valu", "ab_valu", "ab_occ",
+                "micro_valu"):
         res[sub] = pmc(d, sub)
+        for k, c in res[sub].items():
+            if k in ms and not sub.startswith("micro"):
+                c["avg_ms"] = ms[k]
     print("## PMC per dispatch (averages)\n")
     for sub, ks in res.items():
         if not ks:
