@@ -41,7 +41,7 @@ struct MsmPlan {
   unsigned windows = 0;  // W
   unsigned buckets = 0;  // B = 2^(c-1) buckets per window (|digit| in [1, B])
   unsigned K = 0;        // entries per accumulation chunk
-  unsigned K2 = 16;      // fan-in of the partial-reduction levels
+  unsigned K2 = 16;      // fan-in of the partial-reduction levels (4 for long chains at run time)
   unsigned levels = 0;   // number of K2 levels
   unsigned seg = 0;      // buckets per running-sum segment
   unsigned seg_tree = 0; // the same for the workgroup-tree window reduction (no fix-up: shorter)
@@ -97,7 +97,9 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, u
                                             : std::clamp<size_t>(entries >> 18, 16, 64);
   if (p.group == 1) k = n >> 18;  // ~1024 workgroups per window launch
   p.K = (unsigned)std::clamp<size_t>(k, 8, 256);
-  p.K2 = 16;  // (binary levels measured slower here: more launches and level traffic)
+  // first-level fan-in; the join drops to 4-ary levels when the longest chain
+  // is longer than 16 pieces (kJoinFanLong, chosen after the chain read-back)
+  p.K2 = 16;
   size_t maxchunks = (n + p.K - 1) / p.K;  // worst case: all entries of a window in one bucket
   p.levels = 0;
   while (maxchunks > 1) {

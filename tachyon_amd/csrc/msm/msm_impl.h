@@ -765,6 +765,8 @@ __global__ __launch_bounds__(kBlock) void seg_count_kernel(const uint32_t* __res
   }
 }
 
+constexpr unsigned kJoinFanLong = 4;  // chain-join fan-in for chains longer than MsmPlan::K2
+
 // largest s in [0, nseg) with off[s] <= t  (off non-decreasing)
 __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ off, uint32_t nseg, uint32_t t) {
   uint32_t lo = 0, hi = nseg;
@@ -1146,7 +1148,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   uint64_t* ents2 = static_cast<uint64_t*>(ents2_.ensure(entries * 8));
   Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * sizeof(Point)));
   Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * sizeof(Point)));
-  Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / plan.K2 + T + 2) * sizeof(Point)));
+  Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / kJoinFanLong + T + 2) * sizeof(Point)));
   uint32_t* tflags = static_cast<uint32_t*>(start_.ensure(T * 4));
   uint32_t* tlast = static_cast<uint32_t*>(end_.ensure(T * 4));
   uint32_t* is_start = static_cast<uint32_t*>(cnt_.ensure((T + 1) * 4));
@@ -1344,8 +1346,16 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   TA_HIP(hipMemcpyAsync(h_max_, dscal, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   TA_HIP(hipStreamSynchronize(stream_));
   const uint32_t nchains = h_max_[0], max_len = h_max_[1];
+  // Fan-in: 16, or 4-ary levels when a chain is longer than 16 pieces and the
+  // accumulation ran fewer than 2^20 threads (the small MSMs' large buckets:
+  // there each level's serial additions are latency-bound, 3 per 4-ary level
+  // against 15 per 16-ary one: 2^16 reduction 0.48 -> 0.41 ms; with many
+  // threads the levels are throughput-bound and an extra level of scans costs
+  // more: 2^24 / 2^26 reduction 3.07 / 3.74 -> 3.24 / 4.34 ms 4-ary;
+  // profiles/r03c/ab_join_fan_in.log)
+  const unsigned K2 = (max_len > plan.K2 && T < (size_t(1) << 20)) ? kJoinFanLong : plan.K2;
   unsigned levels = 0;
-  for (size_t len = max_len; len > 1; len = (len + plan.K2 - 1) / plan.K2) ++levels;
+  for (size_t len = max_len; len > 1; len = (len + K2 - 1) / K2) ++levels;
   last_levels_ = levels;
   if (nchains > 0) {
     size_t scan2_bytes = 0;
@@ -1359,15 +1369,15 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     Point* dst_bufs[2] = {lvl_buf, pieces};  // pieces is free once level 0 has read it
     for (unsigned l = 0; l < levels; ++l) {
       const bool last = (l + 1 == levels);
-      if (l > 0)
+      if (l > 0 || K2 != plan.K2)  // (level 0's counts came with the read-back, for plan.K2)
         hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, stream_, cur_beg,
-                           cur_end, nullptr, nchains, plan.K2, lcnt, nullptr);
+                           cur_end, nullptr, nchains, K2, lcnt, nullptr);
       TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
                                      rocprim::plus<uint32_t>(), stream_));
-      size_t out_items = cur_items / plan.K2 + nchains + 1;
+      size_t out_items = cur_items / K2 + nchains + 1;
       Point* dst = dst_bufs[l & 1];
       hipLaunchKernelGGL(seg_reduce, dim3(grid_for(lanes * out_items)), dim3(kBlock), 0, stream_, cur, cur_beg, cur_end,
-                         loff, nchains, plan.K2, dst, last ? cbucket : nullptr, bucket_sum);
+                         loff, nchains, K2, dst, last ? cbucket : nullptr, bucket_sum);
       TA_HIP(hipGetLastError());
       if (!last) {
         // next level reads this level's compact output: segment s = [loff[s], loff[s+1])
@@ -1626,7 +1636,7 @@ size_t MsmGpu<Curve>::work_bytes(size_t n) const {
   const size_t entries = n * p.active();
   const size_t T = (entries + p.K - 1) / p.K;
   size_t bytes = entries * 16 + entries / 2;                 // entries (x2) + onesweep scratch
-  bytes += (2 * T + 2 * T / p.K2 + T + 2) * sizeof(Point);   // pieces + first join level
+  bytes += (2 * T + 2 * T / kJoinFanLong + T + 2) * sizeof(Point);  // pieces + first join level
   bytes += (T + 2) * 4 * 9;                                  // flags, last bucket, chain tables
   bytes += (size_t)p.active() * p.buckets * sizeof(Point);    // bucket sums
   bytes += 2 * (size_t)p.active() * (p.buckets / p.seg) * sizeof(Point);
