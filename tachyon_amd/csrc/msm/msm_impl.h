@@ -767,6 +767,40 @@ __global__ __launch_bounds__(kBlock) void seg_count_kernel(const uint32_t* __res
 
 constexpr unsigned kJoinFanLong = 4;  // chain-join fan-in for chains longer than MsmPlan::K2
 
+// A join level's output offsets in ONE workgroup when there are few chains:
+// off[s] = sum over s' < s of ceil(len_s' / K2), len_s = end[s] - beg[s]
+// (end = nullptr: end[s] = beg[s + 1]).  Replaces seg_count + rocPRIM's
+// two-kernel scan (three launches of a few microseconds on a latency-bound
+// level) for nseg <= kJoinSmallChains.
+constexpr unsigned kJoinOffBlock = 1024, kJoinSmallChains = 64 * 1024;
+__global__ __launch_bounds__(kJoinOffBlock) void join_offsets_kernel(const uint32_t* __restrict__ beg,
+                                                                     const uint32_t* __restrict__ end, uint32_t nseg,
+                                                                     unsigned K2, uint32_t* __restrict__ off) {
+  __shared__ uint32_t part[kJoinOffBlock];
+  const uint32_t t = threadIdx.x, per = (nseg + kJoinOffBlock - 1) / kJoinOffBlock;
+  const uint32_t s0 = min(nseg, t * per), s1 = min(nseg, s0 + per);
+  auto count = [&](uint32_t s) {
+    const uint32_t len = (end ? end[s] : beg[s + 1]) - beg[s];
+    return (len + K2 - 1) / K2;
+  };
+  uint32_t sum = 0;
+  for (uint32_t s = s0; s < s1; ++s) sum += count(s);
+  part[t] = sum;
+  __syncthreads();
+  for (unsigned d = 1; d < kJoinOffBlock; d <<= 1) {  // inclusive scan of the per-thread sums
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;  // exclusive prefix of this thread's range
+  for (uint32_t s = s0; s < s1; ++s) {
+    off[s] = run;
+    run += count(s);
+  }
+  if (t == kJoinOffBlock - 1) off[nseg] = part[t];
+}
+
 // largest s in [0, nseg) with off[s] <= t  (off non-decreasing)
 __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ off, uint32_t nseg, uint32_t t) {
   uint32_t lo = 0, hi = nseg;
@@ -1154,13 +1188,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   uint32_t* is_start = static_cast<uint32_t*>(cnt_.ensure((T + 1) * 4));
   uint32_t* cid = static_cast<uint32_t*>(off_a_.ensure((T + 1) * 4));
   // chain tables: beg, end, bucket, level counts/offsets (<= T chains)
-  uint32_t* ctab = static_cast<uint32_t*>(off_b_.ensure((5 * (T + 2) + 4) * 4));
+  uint32_t* ctab = static_cast<uint32_t*>(off_b_.ensure((6 * (T + 2) + 4) * 4));
   uint32_t* cbeg = ctab;
   uint32_t* cend = ctab + (T + 2);
   uint32_t* cbucket = ctab + 2 * (T + 2);
   uint32_t* lcnt = ctab + 3 * (T + 2);
-  uint32_t* loff = ctab + 4 * (T + 2);
-  uint32_t* dscal = ctab + 5 * (T + 2);  // [0] nchains, [1] max chain length
+  uint32_t* loffs[2] = {ctab + 4 * (T + 2), ctab + 5 * (T + 2)};  // join levels' output offsets, ping-pong
+  uint32_t* dscal = ctab + 6 * (T + 2);  // [0] nchains, [1] max chain length
 
   unsigned wbits = 0;
   while ((1u << wbits) < W) ++wbits;
@@ -1358,8 +1392,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   for (size_t len = max_len; len > 1; len = (len + K2 - 1) / K2) ++levels;
   last_levels_ = levels;
   if (nchains > 0) {
+    const bool small = nchains <= kJoinSmallChains;  // offsets in one workgroup
     size_t scan2_bytes = 0;
-    TA_HIP(rocprim::exclusive_scan(nullptr, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
+    TA_HIP(rocprim::exclusive_scan(nullptr, scan2_bytes, lcnt, loffs[0], 0u, (size_t)nchains + 1,
                                    rocprim::plus<uint32_t>(), stream_));
     if (scan2_bytes > scan_bytes) scan_tmp = scan_tmp_.ensure(scan2_bytes);  // (nchains <= T: never grows)
     const Point* cur = pieces;
@@ -1369,11 +1404,17 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     Point* dst_bufs[2] = {lvl_buf, pieces};  // pieces is free once level 0 has read it
     for (unsigned l = 0; l < levels; ++l) {
       const bool last = (l + 1 == levels);
-      if (l > 0 || K2 != plan.K2)  // (level 0's counts came with the read-back, for plan.K2)
-        hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, stream_, cur_beg,
-                           cur_end, nullptr, nchains, K2, lcnt, nullptr);
-      TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
-                                     rocprim::plus<uint32_t>(), stream_));
+      uint32_t* loff = loffs[l & 1];
+      if (small) {
+        hipLaunchKernelGGL(join_offsets_kernel, dim3(1), dim3(kJoinOffBlock), 0, stream_, cur_beg,
+                           l == 0 ? cur_end : nullptr, nchains, K2, loff);
+      } else {
+        if (l > 0 || K2 != plan.K2)  // (level 0's counts came with the read-back, for plan.K2)
+          hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, stream_, cur_beg,
+                             cur_end, nullptr, nchains, K2, lcnt, nullptr);
+        TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
+                                       rocprim::plus<uint32_t>(), stream_));
+      }
       size_t out_items = cur_items / K2 + nchains + 1;
       Point* dst = dst_bufs[l & 1];
       hipLaunchKernelGGL(seg_reduce, dim3(grid_for(lanes * out_items)), dim3(kBlock), 0, stream_, cur, cur_beg, cur_end,
@@ -1381,11 +1422,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       TA_HIP(hipGetLastError());
       if (!last) {
         // next level reads this level's compact output: segment s = [loff[s], loff[s+1])
-        // (copy the offsets: lcnt/loff are rewritten by the next level)
-        uint32_t* nbeg = cbeg;  // the chain begin/end tables are no longer needed after level 0
-        TA_HIP(hipMemcpyAsync(nbeg, loff, ((size_t)nchains + 1) * 4, hipMemcpyDeviceToDevice, stream_));
-        cur_beg = nbeg;
-        cur_end = nbeg + 1;
+        // (its own offsets go to the other buffer)
+        cur_beg = loff;
+        cur_end = loff + 1;
         cur = dst;
         cur_items = out_items;
       }
