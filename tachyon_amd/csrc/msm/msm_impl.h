@@ -421,11 +421,12 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_acc_kernel
 // K - x, K a raised multiple of p) and Y3 = R (Q - X3) - Y1 PPP as one
 // reduction of R T + (4p - Y1) PPP.  Value bounds (in units of p; a product
 // of A and B leaves < A B / 128 + 1 + addend), invariant acc X < 10,
-// Y, ZZ, ZZZ < 2; base coordinates x~ << 5 < 32:
-//   P   = x2 ZZ1 + (16p - X1)  < 17.5     R  = y2 ZZZ1 + (4p - Y1) < 5.5
-//   PP  = P^2 < 3.4   PPP = P PP < 1.47   Q  = X1 PP < 1.27
-//   X3  = R^2 + (8p - PPP - 2Q) < 9.24    T  = Q + (16p - X3) < 17.3
-//   Y3  = R T + (4p - Y1) PPP < 1.8       ZZ3, ZZZ3 < 1.05
+// Y, ZZ, ZZZ < 3 (a run's first point and the doubling's output come in
+// through from32, < 3p); base coordinates x~ << 5 < 32:
+//   P   = x2 ZZ1 + (16p - X1)  < 17.75    R  = y2 ZZZ1 + (4p - Y1) < 5.75
+//   PP  = P^2 < 3.47  PPP = P PP < 1.49   Q  = X1 PP < 1.28
+//   X3  = R^2 + (8p - PPP - 2Q) < 9.26    T  = Q + (16p - X3) < 17.3
+//   Y3  = R T + (4p - Y1) PPP < 1.83      ZZ3, ZZZ3 < 1.09
 // Column sums stay below 2^64: the widest, R T + (4p - Y1) PPP + m p, is
 // < 13.5 2^60 (T's limbs < 1.41 2^30, 4p - Y1's < 2^30).
 namespace acc29 {
