@@ -46,13 +46,13 @@ MULMOD_PEAK_NOTE = ("measured BN254 FIPS Montgomery-product ceiling of the chip,
                     "independent chains per lane or >= 4 waves/SIMD (tools/microbench/mulmod_rates.hip)")
 # The accumulation's VALU roofline: mixed additions (madd-2008-s,
 # point_xyzz_impl.h:129-176) per second against the chip's ceiling for the same
-# field code measured in registers with no gathers or run logic
-# (tools/microbench/madd_rates.hip, 3 waves/SIMD; profiles/r03c/madd_rates.log):
-# the 29-bit-limb field of the BN254 G1 accumulation, and the 32-bit FIPS field
-# (set_variant bit 18).
+# field code in registers with no gathers or run logic, measured live on this
+# box (tachyon_mi355x_msm_madd_ceiling; boxes differ by up to ~8 % in clock).
+# The fallback constants are one box's figures (profiles/r03c/madd_rates.log):
+# the 29-bit-limb field of the BN254 G1 accumulation and the 32-bit FIPS field.
 MADD_PEAK_G = {"seg_acc29_kernel": 19.40, "seg_acc_kernel": 13.67}
-MADD_PEAK_NOTE = ("mixed additions/s of the same field code in registers, no gathers or run logic "
-                  "(tools/microbench/madd_rates.hip, whole chip, 3 waves/SIMD)")
+MADD_PEAK_NOTE = ("mixed additions/s of the same field code in registers, no gathers or run logic, "
+                  "whole chip at 3 waves/SIMD (tachyon_mi355x_msm_madd_ceiling, measured in this run)")
 
 
 def pmc_traffic(kernel):
@@ -482,6 +482,11 @@ def main():
     acc_kernel = "seg_acc29_kernel" if msm.last_schedule()["acc29"] else "seg_acc_kernel"
     acc_traffic, acc_traffic_src, acc_traffic_raw = pmc_traffic(acc_kernel)
     acc_gmadd = units / (acc_ms * 1e-3) / 1e9
+    try:
+        madd_peak = msm.madd_ceiling(29 if acc_kernel == "seg_acc29_kernel" else 32) or MADD_PEAK_G[acc_kernel]
+        madd_peak_src = "measured in this run"
+    except Exception:  # noqa: BLE001 -- a diagnostic; the committed figure stands in
+        madd_peak, madd_peak_src = MADD_PEAK_G[acc_kernel], "profiles/r03c/madd_rates.log"
     stream_gbs = stream_copy_gbs()
 
     out = {
@@ -527,8 +532,8 @@ def main():
                              "stream_copy_gbs = a device-to-device copy measured on this box"},
         "msm_phase_ms": phases,
         "valu_roofline": {"bound": "valu", "kernel": acc_kernel, "achieved": acc_gmadd,
-                          "peak": MADD_PEAK_G[acc_kernel], "unit": "G mixed additions/s",
-                          "frac": acc_gmadd / MADD_PEAK_G[acc_kernel],
+                          "peak": madd_peak, "peak_source": madd_peak_src, "unit": "G mixed additions/s",
+                          "frac": acc_gmadd / madd_peak,
                           "note": "n x windows mixed additions per launch / launch time; peak = " + MADD_PEAK_NOTE},
     }
 

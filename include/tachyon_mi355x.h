@@ -345,6 +345,12 @@ TACHYON_C_EXPORT size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const v
  * counts, bit 2 7-byte LDS staging in the recode scatter, bit 3 the BN254 G1
  * accumulation over the 29-bit-limb field, bit 4 the lane-pair G2 accumulation. */
 TACHYON_C_EXPORT unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx);
+/* Diagnostic: mixed additions per second (G/s) of the curve's bucket
+ * accumulation field code in registers on the current device (no gathers, no
+ * bucket runs; ~0.1 s): the VALU ceiling the bench prices the accumulation
+ * against.  field_bits 29 (BN254 G1's 29-bit-limb field) or 32 (FIPS);
+ * returns 0 for other curves or widths. */
+TACHYON_C_EXPORT double tachyon_mi355x_msm_madd_ceiling(int curve, int field_bits);
 /* One process, several MI355X: every later MSM of this context splits its
  * points into `count` contiguous shards, shard k on device device_ids[k]
  * (its own host thread and stream; host inputs are uploaded per shard over

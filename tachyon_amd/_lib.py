@@ -121,6 +121,7 @@ SIGNATURES = [
     ("tachyon_mi355x_msm_gpu_set_variant", i32, [i32, vp, i32]),
     ("tachyon_mi355x_msm_gpu_last_divisions", sz, [i32, vp]),
     ("tachyon_mi355x_msm_gpu_last_schedule", ctypes.c_uint, [i32, vp]),
+    ("tachyon_mi355x_msm_madd_ceiling", ctypes.c_double, [i32, i32]),
     ("tachyon_mi355x_msm_gpu_set_devices", i32, [i32, vp, ctypes.POINTER(ctypes.c_int), sz]),
     ("tachyon_mi355x_msm_gpu_last_shards", sz, [i32, vp, fp, ctypes.POINTER(ctypes.c_size_t),
                                               ctypes.POINTER(ctypes.c_int), sz]),

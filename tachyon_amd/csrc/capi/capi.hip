@@ -431,6 +431,10 @@ unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx) {
   GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.last_schedule()) GUARD_END
   return 0;
 }
+double tachyon_mi355x_msm_madd_ceiling(int curve, int field_bits) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, return msm::MsmGpu<C>::madd_ceiling(field_bits)) GUARD_END
+  return 0.0;
+}
 size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx) {
   GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.last_divisions()) GUARD_END
   return 0;

@@ -163,6 +163,11 @@ class MsmGpu {
   Point run_window_range(const void* bases, const void* scalars, size_t n, unsigned w_begin, unsigned w_end);
 
   static Point combine_windows(const std::vector<Point>& window_sums, unsigned c);
+  // Mixed additions per second (G/s) of this curve's accumulation field code
+  // in registers on the current device -- no gathers, no run logic: the VALU
+  // ceiling the bench prices the accumulation against, measured on the same
+  // box.  field_bits 29 (BN254 G1's default field) or 32 (FIPS); 0 for others.
+  static double madd_ceiling(int field_bits);
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)

@@ -1566,6 +1566,83 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   }
 }
 
+// The accumulation's madd in registers: a chain of `iters` additions of one
+// point per thread (no gathers, no bucket runs, 3 waves per SIMD as the
+// accumulation kernels).  The result is stored so nothing is dead code.
+namespace detail {
+namespace {
+__global__ __launch_bounds__(kBlock, 3) void madd_ceiling29_kernel(const Affine<Bn254Fq>* __restrict__ pts,
+                                                                   XYZZ<Bn254Fq>* __restrict__ out, int iters) {
+  using namespace acc29;
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  const Affine<Bn254Fq> p = pts[t & 1023], q = pts[(t + 5) & 1023];
+  const F29 x2 = shl5_repack(q.x.v), y2 = shl5_repack(q.y.v);
+  Acc acc = from_shifted(shl5_repack(p.x.v), shl5_repack(p.y.v));
+  int special = 0;
+  for (int i = 0; i < iters; ++i) acc = madd(acc, x2, y2, &special);
+  XYZZ<Bn254Fq> r = to_xyzz(acc);
+  r.zz.v[0] ^= (uint32_t)special;
+  out[t] = r;
+}
+__global__ __launch_bounds__(kBlock, 3) void madd_ceiling32_kernel(const Affine<Bn254Fq>* __restrict__ pts,
+                                                                   XYZZ<Bn254Fq>* __restrict__ out, int iters) {
+  using F = HotFp<Bn254Fq>;
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  const Affine<F> p{pts[t & 1023].x, pts[t & 1023].y}, q{pts[(t + 5) & 1023].x, pts[(t + 5) & 1023].y};
+  XYZZ<F> acc{p.x, p.y, F::one(), F::one()};
+  bool zero = false;
+  for (int i = 0; i < iters; ++i) acc = acc.madd_nz(q, &zero);
+  out[t] = XYZZ<Bn254Fq>{acc.x, acc.y, zero ? Bn254Fq::zero() : Bn254Fq(acc.zz), acc.zzz};
+}
+}  // namespace
+}  // namespace detail
+
+template <class Curve>
+double MsmGpu<Curve>::madd_ceiling(int field_bits) {
+  if constexpr (!std::is_same_v<Curve, Bn254G1>) {
+    (void)field_bits;
+    return 0.0;
+  } else {
+    if (field_bits != 29 && field_bits != 32) return 0.0;
+    require_gpu();
+    constexpr int kBlocks = 256 * 12, kIters = 400;
+    std::vector<Affine<Bn254Fq>> h(1024);  // field values below p (not curve points: the formula does not care)
+    uint64_t s = 0x9e3779b97f4a7c15ull;
+    for (auto& a : h)
+      for (Bn254Fq* f : {&a.x, &a.y})
+        for (int j = 0; j < 8; ++j) {
+          s = s * 6364136223846793005ull + 1442695040888963407ull;
+          f->v[j] = j == 7 ? (uint32_t)(s >> 32) & 0x0fffffffu : (uint32_t)(s >> 32);
+        }
+    Affine<Bn254Fq>* pts = nullptr;
+    XYZZ<Bn254Fq>* out = nullptr;
+    hipEvent_t e0, e1;
+    TA_HIP(hipMalloc(&pts, h.size() * sizeof(h[0])));
+    TA_HIP(hipMalloc(&out, (size_t)kBlocks * kBlock * sizeof(XYZZ<Bn254Fq>)));
+    TA_HIP(hipMemcpy(pts, h.data(), h.size() * sizeof(h[0]), hipMemcpyHostToDevice));
+    TA_HIP(hipEventCreate(&e0));
+    TA_HIP(hipEventCreate(&e1));
+    auto* kern = field_bits == 29 ? &madd_ceiling29_kernel : &madd_ceiling32_kernel;
+    hipLaunchKernelGGL(kern, dim3(kBlocks), dim3(kBlock), 0, 0, pts, out, 4);
+    float best = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+      TA_HIP(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL(kern, dim3(kBlocks), dim3(kBlock), 0, 0, pts, out, kIters);
+      TA_HIP(hipEventRecord(e1, 0));
+      TA_HIP(hipEventSynchronize(e1));
+      float ms = 0;
+      TA_HIP(hipEventElapsedTime(&ms, e0, e1));
+      best = std::min(best, ms);
+    }
+    TA_HIP(hipGetLastError());
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(pts);
+    (void)hipFree(out);
+    return (double)kBlocks * kBlock * kIters / (best * 1e-3) / 1e9;
+  }
+}
+
 // Horner over windows, high to low, c doublings in between
 // (PippengerBase::AccumulateWindowSums, pippenger_base.h:59-77).
 template <class Curve>

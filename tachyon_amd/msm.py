@@ -132,6 +132,12 @@ class VariableBaseMSMGpu:
         k = lib().tachyon_mi355x_msm_gpu_last_shards(self.curve_id, self._ctx, ms, pts, dev, cap)
         return [(dev[i], pts[i], ms[i]) for i in range(min(k, cap))]
 
+    def madd_ceiling(self, field_bits: int = 29) -> float:
+        """In-register mixed additions/s (G) of this curve's accumulation field
+        code on the current device (tachyon_mi355x_msm_madd_ceiling): 29 = the
+        29-bit-limb field, 32 = FIPS; 0.0 where not provided."""
+        return float(lib().tachyon_mi355x_msm_madd_ceiling(self.curve_id, int(field_bits)))
+
     def last_schedule(self) -> dict:
         """Schedule of the last run: fused recode + first radix pass, recode-fed
         onesweep passes, 7-byte LDS staging (tachyon_mi355x_msm_gpu_last_schedule)."""

@@ -355,3 +355,15 @@ def test_msm_schedule_variants_agree(curve, logn):
                 m.set_variant(bad)
     finally:
         m.set_variant(0)
+
+
+@pytest.mark.gpu
+def test_madd_ceiling():
+    """The bench's VALU ceiling (tachyon_mi355x_msm_madd_ceiling): a positive
+    rate for BN254 G1's two field widths, 0 where not provided."""
+    from tachyon_amd import msm as M
+    g1 = M.VariableBaseMSMGpu("bn254_g1")
+    r29, r32 = g1.madd_ceiling(29), g1.madd_ceiling(32)
+    assert 1.0 < r29 < 200.0 and 1.0 < r32 < 200.0, (r29, r32)
+    assert g1.madd_ceiling(31) == 0.0
+    assert M.VariableBaseMSMGpu("bn254_g2").madd_ceiling(29) == 0.0
