@@ -166,6 +166,13 @@ TA_HD F29 add_ksub(const F29& a, const uint32_t (&k)[9], const F29& x) {
   for (int i = 0; i < 9; ++i) r.l[i] = a.l[i] + (k[i] - x.l[i]);
   return r;
 }
+// k a limb-wise (a small k: k times the limb bound)
+TA_HD F29 times(const F29& a, uint32_t k) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.l[i] = a.l[i] * k;
+  return r;
+}
 TA_HD F29 ksub2(const uint32_t (&k)[9], const F29& a, const F29& b) {
   F29 r;
 #pragma unroll

@@ -478,6 +478,87 @@ __device__ __forceinline__ Acc madd(const Acc& A, const F29& x2, const F29& y2, 
   C.zzz = mul(A.zzz, PPP);
   return C;
 }
+
+// The bucket-sum reductions over the same field (chain join, window sums).
+// Invariant of their points: X < 10p, Y, ZZ, ZZZ < 3p (from32 of R-form
+// values gives < 3p).  add-2008-s (point_xyzz_impl.h:45-97), both operands
+// not the identity; *special as madd's:
+//   U1 = X1 ZZ2 < 1.24   S1 = Y1 ZZZ2 < 1.08
+//   P  = X2 ZZ1 + (4p - U1) < 5.24       R = Y2 ZZZ1 + (4p - S1) < 5.08
+//   PP < 1.22  PPP < 1.05  Q = U1 PP < 1.02
+//   X3 = R^2 + (8p - PPP - 2Q) < 9.21    T = Q + (16p - X3) < 17.1
+//   Y3 = R T + (4p - S1) PPP < 1.72      ZZ3 = (ZZ1 ZZ2) PP, ZZZ3 < 1.02
+__device__ __forceinline__ Acc add(const Acc& A, const Acc& B, int* special) {
+  const F29 U1 = mul(A.x, B.zz), S1 = mul(A.y, B.zzz);
+  const F29 P = mul_add(B.x, A.zz, ksub(kK4, U1));
+  const F29 R = mul_add(B.y, A.zzz, ksub(kK4, S1));
+  if (is_zero_mod_p(P)) {
+    *special = is_zero_mod_p(R) ? 2 : 1;
+    return A;
+  }
+  const F29 PP = sqr(P);
+  const F29 PPP = mul(P, PP);
+  const F29 Q = mul(U1, PP);
+  Acc C;
+  C.x = sqr_add(R, ksub2(kK8, PPP, Q));
+  const F29 T = add_ksub(Q, kK16, C.x);
+  C.y = mul2_add(R, T, ksub(kK4, S1), PPP);
+  C.zz = mul(mul(A.zz, B.zz), PP);
+  C.zzz = mul(mul(A.zzz, B.zzz), PPP);
+  return C;
+}
+// dbl-2008-s-1 (a = 0; point_xyzz_impl.h:199-236) under the same invariant:
+//   U = 2 Y1 < 6   V = U^2 < 1.29   W = U V < 1.07   S = X1 V < 1.11
+//   M = X1 (3 X1) < 3.35 (3 X1's limbs < 1.5 2^30)
+//   X3 = M^2 + (8p - 2S) < 9.09      Y3 = M (S + 16p - X3) + (4p - W) Y1 < 1.55
+//   ZZ3 = V ZZ1, ZZZ3 = W ZZZ1 < 1.04
+// (the widest column, M T + (4p - W) Y1 + m p, < 10.2 2^60)
+__device__ __forceinline__ Acc dbl(const Acc& A) {
+  const F29 U = times(A.y, 2);
+  const F29 V = sqr(U);
+  const F29 W = mul(U, V);
+  const F29 S = mul(A.x, V);
+  const F29 M = mul(A.x, times(A.x, 3));
+  F29 zero{};
+  Acc C;
+  C.x = sqr_add(M, ksub2(kK8, zero, S));
+  C.y = mul2_add(M, add_ksub(S, kK16, C.x), ksub(kK4, W), A.y);
+  C.zz = mul(V, A.zz);
+  C.zzz = mul(W, A.zzz);
+  return C;
+}
+
+// A reduction operand with its identity flag, to and from the R-form arrays
+struct Pt {
+  Acc a;
+  bool zero;
+};
+__device__ __forceinline__ Pt load_pt(const XYZZ<Bn254Fq>* __restrict__ p, size_t i) {
+  const XYZZ<Bn254Fq> q = p[i];
+  if (q.is_zero()) return {Acc{}, true};
+  return {{from32(q.x.v), from32(q.y.v), from32(q.zz.v), from32(q.zzz.v)}, false};
+}
+__device__ __forceinline__ void store_pt(XYZZ<Bn254Fq>* __restrict__ p, size_t i, const Pt& v) {
+  p[i] = v.zero ? XYZZ<Bn254Fq>::zero() : to_xyzz(v.a);
+}
+__device__ __forceinline__ Pt add(const Pt& a, const Pt& b) {
+  if (a.zero) return b;
+  if (b.zero) return a;
+  int special = 0;
+  const Acc s = add(a.a, b.a, &special);
+  if (special == 1) return {Acc{}, true};
+  return {special == 2 ? dbl(a.a) : s, false};
+}
+// m P for a small m (double-and-add from the top bit)
+__device__ __forceinline__ Pt small_mul(const Pt& P, uint32_t m) {
+  if (m == 0 || P.zero) return {Acc{}, true};
+  Pt r = P;
+  for (int bit = 30 - __builtin_clz(m); bit >= 0; --bit) {
+    r.a = dbl(r.a);  // (no point of this prime-order group doubles to the identity)
+    if ((m >> bit) & 1) r = add(r, P);
+  }
+  return r;
+}
 }  // namespace acc29
 
 // kPrefetch: 0 = gather each base at its own iteration; 1 = the next base in
@@ -952,6 +1033,57 @@ __global__ __launch_bounds__(kBlock, 2) void reduce_uniform_pair_kernel(const XY
   pair::store(reinterpret_cast<Fb*>(out), t, h, acc);
 }
 
+// The BN254 G1 reductions over the 29-bit field (acc29::add / dbl; R-form
+// arrays in and out, converted on load and store): the chain join and the
+// window sums are chains of dependent point additions that run at one or two
+// waves per SIMD, so an addition's instruction count is its latency.
+__global__ __launch_bounds__(kBlock, 2) void seg_reduce29_kernel(const XYZZ<Bn254Fq>* __restrict__ in,
+                                                                const uint32_t* __restrict__ beg,
+                                                                const uint32_t* __restrict__ end,
+                                                                const uint32_t* __restrict__ out_off, uint32_t nseg,
+                                                                unsigned K2, XYZZ<Bn254Fq>* __restrict__ out,
+                                                                const uint32_t* __restrict__ bucket,
+                                                                XYZZ<Bn254Fq>* __restrict__ bucket_sum) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= out_off[nseg]) return;
+  const uint32_t s = find_segment(out_off, nseg, t);
+  const uint32_t e0 = beg[s] + (t - out_off[s]) * K2;
+  const uint32_t e1 = min(end[s], e0 + K2);
+  acc29::Pt acc = acc29::load_pt(in, e0);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc29::add(acc, acc29::load_pt(in, e));
+  if (bucket) acc29::store_pt(bucket_sum, bucket[s], acc);
+  else acc29::store_pt(out, t, acc);
+}
+__global__ __launch_bounds__(kBlock, 2) void window_segment29_kernel(const XYZZ<Bn254Fq>* __restrict__ bucket_sum,
+                                                                    unsigned W, unsigned B, unsigned L,
+                                                                    XYZZ<Bn254Fq>* __restrict__ out) {
+  const uint32_t S = B / L;
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= W * S) return;
+  const uint32_t w = t / S, j = t - w * S;
+  const size_t b0 = (size_t)w * B + (size_t)j * L;
+  acc29::Pt R{acc29::Acc{}, true}, acc = R;
+  for (int k = (int)L - 1; k >= 0; --k) {
+    R = acc29::add(R, acc29::load_pt(bucket_sum, b0 + k));
+    acc = acc29::add(acc, R);
+  }
+  acc = acc29::add(acc, acc29::small_mul(R, j * L));
+  acc29::store_pt(out, t, acc);
+}
+__global__ __launch_bounds__(kBlock, 2) void reduce_uniform29_kernel(const XYZZ<Bn254Fq>* __restrict__ in, unsigned W,
+                                                                    unsigned S_in, unsigned K2,
+                                                                    XYZZ<Bn254Fq>* __restrict__ out) {
+  const uint32_t S_out = (S_in + K2 - 1) / K2;
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= W * S_out) return;
+  const uint32_t w = t / S_out, q = t - w * S_out;
+  const uint32_t e0 = q * K2, e1 = min(S_in, e0 + K2);
+  const XYZZ<Bn254Fq>* src = in + (size_t)w * S_in;
+  acc29::Pt acc = acc29::load_pt(src, e0);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc29::add(acc, acc29::load_pt(src, e));
+  acc29::store_pt(out, t, acc);
+}
+
 // Window reduction, stage 2: sum K2 consecutive segment sums per window.
 template <class Curve>
 __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void reduce_uniform_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
@@ -1365,6 +1497,15 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       seg_reduce = &seg_reduce_pair_kernel<Curve>;
       win_segment = &window_segment_pair_kernel<Curve>;
       win_reduce = &reduce_uniform_pair_kernel<Curve>;
+    }
+  }
+  // BN254 G1: the reductions over the 29-bit field with the 29-bit accumulation
+  // (set_variant bit 18 restores the FIPS field for both)
+  if constexpr (std::is_same_v<Curve, Bn254G1>) {
+    if (acc29_) {
+      seg_reduce = &seg_reduce29_kernel;
+      win_segment = &window_segment29_kernel;
+      win_reduce = &reduce_uniform29_kernel;
     }
   }
   // ---- join buckets that cross thread boundaries ----
