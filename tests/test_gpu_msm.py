@@ -367,3 +367,40 @@ def test_madd_ceiling():
     assert 1.0 < r29 < 200.0 and 1.0 < r32 < 200.0, (r29, r32)
     assert g1.madd_ceiling(31) == 0.0
     assert M.VariableBaseMSMGpu("bn254_g2").madd_ceiling(29) == 0.0
+
+
+def _neg_point(curve, p: bytes) -> bytes:
+    """-P of an affine point (y -> -y componentwise in the base field)."""
+    fq = "bn254_fq" if curve.startswith("bn254") else "bls12_381_fq"
+    half = len(p) // 2
+    return p[:half] + O.field_op(fq, "neg", p[half:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve,variant", [("bn254_g1", 0), ("bn254_g1", 262144), ("bn254_g2", 0),
+                                           ("bls12_381_g1", 0), ("bls12_381_g2", 0), ("bls12_381_g2", 32768)])
+def test_msm_reduction_edge_cases(curve, variant):
+    """Inputs that drive the chain join and the window sums through their
+    special cases: every base the same point (equal bucket pieces and equal
+    running sums -> the doubling branch of the reduction additions), bases
+    alternating P, -P under one repeated scalar (pieces and bucket sums that
+    cancel -> the identity branch), and one repeated base and scalar.
+    Default schedule (29-bit reductions on BN254 G1, lane-pair reductions on
+    G2) and the FIPS / one-lane ones (bits 18 / 15)."""
+    pb, fr = O.CURVE_INFO[curve]
+    n = 1 << 13
+    g = O.gen_bases(curve, 31, 1, 1).tobytes()
+    m = ctx(curve)
+    m.set_variant(variant)
+    try:
+        same = g * n
+        scalars = O.gen_scalars(fr, 31, n).tobytes()
+        assert m.run(same, scalars) == O.msm(curve, same, scalars)[0]
+        alt = (g + _neg_point(curve, g)) * (n // 2)
+        one = O.gen_scalars(fr, 32, 1).tobytes() * n
+        expect = O.msm(curve, alt, one)[0]
+        assert expect == bytes(pb)  # the identity, (0, 0)
+        assert m.run(alt, one) == expect
+        assert m.run(same, one) == O.msm(curve, same, one)[0]
+    finally:
+        m.set_variant(0)
