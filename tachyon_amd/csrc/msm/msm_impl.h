@@ -549,6 +549,29 @@ __device__ __forceinline__ Pt add(const Pt& a, const Pt& b) {
   if (special == 1) return {Acc{}, true};
   return {special == 2 ? dbl(a.a) : s, false};
 }
+// A bucket or piece as the 29-bit accumulation leaves it (R' form, 4 x 9
+// limbs, 144 B; all-zero limbs = the identity): the accumulation's run-end
+// stores skip the four R-form conversions (they run in the loop's divergent
+// branch whenever any lane of the wave changes bucket) and the 29-bit
+// reductions read it without converting.
+struct alignas(16) Raw {
+  F29 x, y, zz, zzz;
+};
+__device__ __forceinline__ Raw raw_of(const Acc& a, bool zero) {
+  if (zero) return Raw{};
+  return {a.x, a.y, a.zz, a.zzz};
+}
+__device__ __forceinline__ Pt load_raw(const void* __restrict__ p, size_t i) {
+  const Raw r = static_cast<const Raw*>(p)[i];
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) nz |= r.zz.l[k];
+  return {{r.x, r.y, r.zz, r.zzz}, nz == 0};
+}
+__device__ __forceinline__ void store_raw(void* __restrict__ p, size_t i, const Pt& v) {
+  static_cast<Raw*>(p)[i] = raw_of(v.a, v.zero);
+}
+
 // m P for a small m (double-and-add from the top bit)
 __device__ __forceinline__ Pt small_mul(const Pt& P, uint32_t m) {
   if (m == 0 || P.zero) return {Acc{}, true};
@@ -566,7 +589,7 @@ __device__ __forceinline__ Pt small_mul(const Pt& P, uint32_t m) {
 // LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR destination, so the
 // kernel keeps its 3-wave register budget with the gather one iteration ahead)
 typedef __attribute__((address_space(3))) void lds_void_t;
-template <int kPrefetch>
+template <int kPrefetch, bool kRaw>
 __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
                                                            const uint64_t* __restrict__ ents, uint32_t c,
                                                            uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
@@ -589,15 +612,21 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
   uint32_t flags = 0, runs = 0, cur = kNoBucket;
   Acc acc{};  // (any defined value: the stores mask it while acc_zero)
   bool acc_zero = true;
-  auto stored = [&]() {  // the identity is zz = zzz = 0 (x, y are not read)
-    XYZZ<Bn254Fq> s = to_xyzz(acc);
-    const uint32_t keep = acc_zero ? 0u : ~0u;
+  // kRaw: the accumulator as it is (Raw); otherwise R form, the identity as
+  // zz = zzz = 0 (x, y are not read)
+  auto put = [&](XYZZ<Bn254Fq>* dst, size_t i) {
+    if constexpr (kRaw) {
+      reinterpret_cast<Raw*>(dst)[i] = raw_of(acc, acc_zero);
+    } else {
+      XYZZ<Bn254Fq> s = to_xyzz(acc);
+      const uint32_t keep = acc_zero ? 0u : ~0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      s.zz.v[i] &= keep;
-      s.zzz.v[i] &= keep;
+      for (int k = 0; k < 8; ++k) {
+        s.zz.v[k] &= keep;
+        s.zzz.v[k] &= keep;
+      }
+      dst[i] = s;
     }
-    return s;
   };
   uint64_t e0 = ents[g0];
   uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
@@ -636,9 +665,8 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
     if (b != kNoBucket) {
       if (b != cur) {
         if (cur != kNoBucket) {
-          const XYZZ<Bn254Fq> s = stored();
-          if (runs == 1 && cur == prev_b) { pieces[2 * t] = s; flags |= kHead; }
-          else bucket_sum[cur] = s;
+          if (runs == 1 && cur == prev_b) { put(pieces, 2 * t); flags |= kHead; }
+          else put(bucket_sum, cur);
         }
         cur = b;
         ++runs;
@@ -663,18 +691,18 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
     if constexpr (kPrefetch == 1) P = Pn;
   }
   if (cur != kNoBucket) {
-    const XYZZ<Bn254Fq> s = stored();
     const bool head = runs == 1 && cur == prev_b;
     const bool tail = cur == next_b;
-    if (head) { pieces[2 * t] = s; flags |= kHead; }
+    if (head) { put(pieces, 2 * t); flags |= kHead; }
     if (tail) flags |= kTail;
-    if (tail && !head) pieces[2 * t + 1] = s;
-    if (!head && !tail) bucket_sum[cur] = s;
+    if (tail && !head) put(pieces, 2 * t + 1);
+    if (!head && !tail) put(bucket_sum, cur);
   }
   if (runs <= 1) flags |= kSingle;
-  if (!(flags & kHead)) pieces[2 * t] = XYZZ<Bn254Fq>::zero();
+  acc_zero = true;  // absent pieces are the identity
+  if (!(flags & kHead)) put(pieces, 2 * t);
   const bool through = (flags & kHead) && (flags & kTail) && (flags & kSingle);
-  if (!(flags & kTail) || through) pieces[2 * t + 1] = XYZZ<Bn254Fq>::zero();
+  if (!(flags & kTail) || through) put(pieces, 2 * t + 1);
   tflags[t] = flags;
   tlast[t] = cur;
 }
@@ -1037,6 +1065,7 @@ __global__ __launch_bounds__(kBlock, 2) void reduce_uniform_pair_kernel(const XY
 // arrays in and out, converted on load and store): the chain join and the
 // window sums are chains of dependent point additions that run at one or two
 // waves per SIMD, so an addition's instruction count is its latency.
+template <bool kInRaw, bool kOutRaw>
 __global__ __launch_bounds__(kBlock, 2) void seg_reduce29_kernel(const XYZZ<Bn254Fq>* __restrict__ in,
                                                                 const uint32_t* __restrict__ beg,
                                                                 const uint32_t* __restrict__ end,
@@ -1049,11 +1078,17 @@ __global__ __launch_bounds__(kBlock, 2) void seg_reduce29_kernel(const XYZZ<Bn25
   const uint32_t s = find_segment(out_off, nseg, t);
   const uint32_t e0 = beg[s] + (t - out_off[s]) * K2;
   const uint32_t e1 = min(end[s], e0 + K2);
-  acc29::Pt acc = acc29::load_pt(in, e0);
-  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc29::add(acc, acc29::load_pt(in, e));
-  if (bucket) acc29::store_pt(bucket_sum, bucket[s], acc);
-  else acc29::store_pt(out, t, acc);
+  auto load = [&](uint32_t e) { return kInRaw ? acc29::load_raw(in, e) : acc29::load_pt(in, e); };
+  acc29::Pt acc = load(e0);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc29::add(acc, load(e));
+  if (bucket) {
+    if constexpr (kOutRaw) acc29::store_raw(bucket_sum, bucket[s], acc);
+    else acc29::store_pt(bucket_sum, bucket[s], acc);
+  } else {
+    acc29::store_pt(out, t, acc);
+  }
 }
+template <bool kRaw>
 __global__ __launch_bounds__(kBlock, 2) void window_segment29_kernel(const XYZZ<Bn254Fq>* __restrict__ bucket_sum,
                                                                     unsigned W, unsigned B, unsigned L,
                                                                     XYZZ<Bn254Fq>* __restrict__ out) {
@@ -1064,7 +1099,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_segment29_kernel(const XYZZ<
   const size_t b0 = (size_t)w * B + (size_t)j * L;
   acc29::Pt R{acc29::Acc{}, true}, acc = R;
   for (int k = (int)L - 1; k >= 0; --k) {
-    R = acc29::add(R, acc29::load_pt(bucket_sum, b0 + k));
+    R = acc29::add(R, kRaw ? acc29::load_raw(bucket_sum, b0 + k) : acc29::load_pt(bucket_sum, b0 + k));
     acc = acc29::add(acc, R);
   }
   acc = acc29::add(acc, acc29::small_mul(R, j * L));
@@ -1313,8 +1348,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
 
   uint64_t* ents = static_cast<uint64_t*>(ents_.ensure(entries * 8));
   uint64_t* ents2 = static_cast<uint64_t*>(ents2_.ensure(entries * 8));
-  Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * sizeof(Point)));
-  Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * sizeof(Point)));
+  // bucket sums and pieces in the 144-byte Raw format after the 29-bit
+  // accumulation (not with the workgroup-tree window sums, an A/B path in R form)
+  bool raw = false;
+  if constexpr (std::is_same_v<Curve, Bn254G1>) raw = acc29_ && !tree_reduce_;
+  const size_t slot = raw ? sizeof(acc29::Raw) : sizeof(Point);
+  Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * slot));
+  Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * slot));
   Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / kJoinFanLong + T + 2) * sizeof(Point)));
   uint32_t* tflags = static_cast<uint32_t*>(start_.ensure(T * 4));
   uint32_t* tlast = static_cast<uint32_t*>(end_.ensure(T * 4));
@@ -1391,7 +1431,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   }
   TA_HIP(hipGetLastError());
   // every bucket without an entry stays the identity
-  TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * sizeof(Point), stream_));
+  TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * slot, stream_));
   TA_HIP(hipMemsetAsync(dscal, 0, 2 * sizeof(uint32_t), stream_));
   TA_HIP(hipEventRecord(ev_[2], stream_));  // recode done (also the profile mark)
   if (sort_stream != stream_) TA_HIP(hipStreamWaitEvent(sort_stream, ev_[2], 0));
@@ -1450,8 +1490,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
       if (acc29_) last_schedule_ |= kSchedAcc29;
       if (acc29_)  // 29-bit-limb accumulation (BN254 G1 default; set_variant bits 13 / 17: base prefetch A/B)
-        hipLaunchKernelGGL(acc29_mode_ == 2 ? seg_acc29_kernel<2> : acc29_mode_ == 1 ? seg_acc29_kernel<1>
-                                                                            : seg_acc29_kernel<0>,
+        hipLaunchKernelGGL(acc29_mode_ == 2 ? (raw ? seg_acc29_kernel<2, true> : seg_acc29_kernel<2, false>)
+                           : acc29_mode_ == 1 ? (raw ? seg_acc29_kernel<1, true> : seg_acc29_kernel<1, false>)
+                                              : (raw ? seg_acc29_kernel<0, true> : seg_acc29_kernel<0, false>),
                            dim3(grid_for(Tg)),
                            dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
@@ -1503,8 +1544,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // (set_variant bit 18 restores the FIPS field for both)
   if constexpr (std::is_same_v<Curve, Bn254G1>) {
     if (acc29_) {
-      seg_reduce = &seg_reduce29_kernel;
-      win_segment = &window_segment29_kernel;
+      seg_reduce = &seg_reduce29_kernel<false, false>;
+      win_segment = raw ? &window_segment29_kernel<true> : &window_segment29_kernel<false>;
       win_reduce = &reduce_uniform29_kernel;
     }
   }
@@ -1559,8 +1600,14 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       }
       size_t out_items = cur_items / K2 + nchains + 1;
       Point* dst = dst_bufs[l & 1];
-      hipLaunchKernelGGL(seg_reduce, dim3(grid_for(lanes * out_items)), dim3(kBlock), 0, stream_, cur, cur_beg, cur_end,
-                         loff, nchains, K2, dst, last ? cbucket : nullptr, bucket_sum);
+      auto* level_kernel = seg_reduce;
+      if constexpr (std::is_same_v<Curve, Bn254G1>) {
+        if (raw)  // Raw pieces into level 0, Raw bucket sums out of the last level
+          level_kernel = l == 0 ? (last ? &seg_reduce29_kernel<true, true> : &seg_reduce29_kernel<true, false>)
+                                : (last ? &seg_reduce29_kernel<false, true> : &seg_reduce29_kernel<false, false>);
+      }
+      hipLaunchKernelGGL(level_kernel, dim3(grid_for(lanes * out_items)), dim3(kBlock), 0, stream_, cur, cur_beg,
+                         cur_end, loff, nchains, K2, dst, last ? cbucket : nullptr, bucket_sum);
       TA_HIP(hipGetLastError());
       if (!last) {
         // next level reads this level's compact output: segment s = [loff[s], loff[s+1])
@@ -1894,9 +1941,11 @@ size_t MsmGpu<Curve>::work_bytes(size_t n) const {
   const size_t entries = n * p.active();
   const size_t T = (entries + p.K - 1) / p.K;
   size_t bytes = entries * 16 + entries / 2;                 // entries (x2) + onesweep scratch
-  bytes += (2 * T + 2 * T / kJoinFanLong + T + 2) * sizeof(Point);  // pieces + first join level
-  bytes += (T + 2) * 4 * 9;                                  // flags, last bucket, chain tables
-  bytes += (size_t)p.active() * p.buckets * sizeof(Point);    // bucket sums
+  // (pieces and bucket sums in the 144-byte Raw format of the BN254 G1 accumulation)
+  const size_t slot = std::is_same_v<Curve, Bn254G1> ? std::max<size_t>(sizeof(Point), 144) : sizeof(Point);
+  bytes += 2 * T * slot + (2 * T / kJoinFanLong + T + 2) * sizeof(Point);  // pieces + first join level
+  bytes += (T + 2) * 4 * 9;                                                // flags, last bucket, chain tables
+  bytes += (size_t)p.active() * p.buckets * slot;                           // bucket sums
   bytes += 2 * (size_t)p.active() * (p.buckets / p.seg) * sizeof(Point);
   return bytes + bytes / 10;
 }
