@@ -56,9 +56,10 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
   uint32_t carry = 0;
   for (unsigned w = 0; w < w0 + wr; ++w) {
     uint32_t coeff = (limbs[0] & mask) + carry;
-    // shift the scalar right by c (c < 32), constant-indexed limbs only
+    // shift the scalar right by c (c < 32), constant-indexed limbs only: one
+    // funnel shift (v_alignbit_b32) per limb
 #pragma unroll
-    for (int k = 0; k < N - 1; ++k) limbs[k] = (limbs[k] >> c) | (limbs[k + 1] << (32 - c));
+    for (int k = 0; k < N - 1; ++k) limbs[k] = __builtin_amdgcn_alignbit(limbs[k + 1], limbs[k], c);
     limbs[N - 1] >>= c;
     uint32_t key, sign;
     if (w + 1 < W) {
@@ -101,21 +102,13 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 // 32-byte scalars and one write.
 constexpr unsigned kRecodeSpt = 2;  // default scalars per thread of the fused recode
 
-// LDS bin counters with one atomic per wave when every active lane hits the
+// LDS bin ranks with one atomic per wave when every active lane hits the
 // same bin -- NonUniform(n, 1) scalars (variable_base_msm_test_set.h:43-53),
 // small scalars' empty high windows -- instead of 64 serialised atomics on
 // one address (2^26 NonUniform recode 12.8 -> see DESIGN.md); otherwise one
 // atomic per lane.  The test is wave-uniform (ballots), so no divergence.
-__device__ __forceinline__ void lds_count(uint32_t* cnt, uint32_t bin) {
-  const uint32_t b0 = __builtin_amdgcn_readfirstlane(bin);
-  const uint64_t active = __ballot(1);
-  if (__ballot(bin == b0) == active) {
-    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)active) - 1)) atomicAdd(&cnt[b0], (uint32_t)__popcll(active));
-  } else {
-    atomicAdd(&cnt[bin], 1u);
-  }
-}
-// the same for a returning add of 1: this lane's slot in bin's run
+// (recode_hist_kernel makes the same test once per entry for its three bins.)
+// A returning add of 1: this lane's slot in bin's run
 __device__ __forceinline__ uint32_t lds_rank(uint32_t* cur, uint32_t bin) {
   const uint32_t b0 = __builtin_amdgcn_readfirstlane(bin);
   const uint64_t active = __ballot(1);
@@ -150,9 +143,22 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
     const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + t;
     if (i < n)
       recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned, uint32_t key, uint32_t) {
-        lds_count(cnt[0], key & 255);
-        if (places > 0) lds_count(cnt[1], (key >> 8) & 255);
-        if (places > 1) lds_count(cnt[2], (key >> 16) & 255);
+        // one wave-uniformity test for the entry's three bins (equal keys
+        // have equal bins): NonUniform inputs take one atomic per wave
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+        const uint64_t active = __ballot(1);
+        if (__ballot(key == k0) == active) {
+          if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)active) - 1)) {
+            const uint32_t m = (uint32_t)__popcll(active);
+            atomicAdd(&cnt[0][k0 & 255], m);
+            if (places > 0) atomicAdd(&cnt[1][(k0 >> 8) & 255], m);
+            if (places > 1) atomicAdd(&cnt[2][(k0 >> 16) & 255], m);
+          }
+        } else {
+          atomicAdd(&cnt[0][key & 255], 1u);
+          if (places > 0) atomicAdd(&cnt[1][(key >> 8) & 255], 1u);
+          if (places > 1) atomicAdd(&cnt[2][(key >> 16) & 255], 1u);
+        }
       });
   }
   __syncthreads();
