@@ -194,6 +194,9 @@ class MsmGpu {
   size_t held_bytes() const;
   size_t memory_divisions(size_t n, size_t resident_bytes) const;
   void ensure_group_events(unsigned groups);
+  void build_chains(const uint32_t* flags, const uint32_t* last, size_t T, unsigned K2, uint32_t* is_start,
+                    uint32_t* cid, uint32_t* cbeg, uint32_t* cend, uint32_t* cbucket, uint32_t* lcnt, uint32_t* dscal,
+                    hipStream_t s);
   hipError_t sort_entries(void* tmp, size_t& bytes, const uint64_t* in, uint64_t* out, size_t count,
                           unsigned begin_bit, unsigned end_bit, hipStream_t s);
 
@@ -205,7 +208,7 @@ class MsmGpu {
   MsmTimings timings_;
   DeviceBuffer bases_, scalars_, ents_, ents2_, sort_tmp_, scan_tmp_;
   DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_, buckets_;
-  hipEvent_t ev_[8] = {};
+  hipEvent_t ev_[9] = {};  // 0-5 phase marks, 6 sorted, 7 chain tables read back, 8 join offsets
   hipStream_t sort_stream_ = nullptr;  // group sorts run here, overlapping the accumulation on stream_
   std::vector<hipEvent_t> gev_sorted_, gev_acc0_, gev_acc1_;
   unsigned acc_launches_ = 0;
@@ -226,7 +229,7 @@ class MsmGpu {
   hipEvent_t copy_done_ = nullptr;
   std::vector<hipEvent_t> chunk_ev_;  // host-resident pipeline: chunk k uploaded
   DeviceBuffer hist_, hscan_tmp_;
-  DeviceBuffer maxlen_;
+  DeviceBuffer maxlen_, lofs_;  // lofs_: every join level's output offsets
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;
   size_t last_divisions_ = 1;

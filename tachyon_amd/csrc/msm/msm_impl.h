@@ -133,9 +133,12 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
                                                              unsigned W, unsigned w0, unsigned wr,
                                                              uint32_t nblocks, uint32_t spt, uint32_t places,
                                                              uint32_t* __restrict__ hist,
-                                                             uint32_t* __restrict__ later) {
+                                                             uint32_t* __restrict__ later,
+                                                             uint4* __restrict__ zero, size_t zero_n) {
   __shared__ uint32_t cnt[3][256];
   const uint32_t t = threadIdx.x;
+  // the bucket sums start as the identity (all-zero words): cleared here, not by a memset launch
+  for (size_t i = (size_t)blockIdx.x * kBlock + t; i < zero_n; i += (size_t)nblocks * kBlock) zero[i] = uint4{0, 0, 0, 0};
   cnt[0][t] = 0;
   cnt[1][t] = 0;
   cnt[2][t] = 0;
@@ -743,9 +746,58 @@ __device__ __forceinline__ bool chain_end(uint32_t f) {
   return (f & kHead) && !through;
 }
 
+// The accumulation's run flags (kHead / kTail / kSingle) and last bucket of
+// every thread, from the sorted keys alone: the values seg_acc*_kernel writes
+// (head = the first run continues the previous thread's last bucket, tail =
+// the last run continues into the next thread, single = at most one run).  So
+// the chain tables below can be built on a second stream WHILE the
+// accumulation runs, and the host's read-back of the chain count and length
+// hides behind it (small MSMs: the tables, the read-back and the join-level
+// offsets were ~90 us on the critical path of a 0.7 ms 2^16 MSM).  Keys are
+// sorted, so equal first and last buckets mean one run; the loop runs only
+// when an end of the range holds digit-0 entries (no bucket).
+__global__ __launch_bounds__(kBlock) void chain_flags_kernel(const uint64_t* __restrict__ ents, uint32_t c,
+                                                             uint64_t gbeg, uint64_t gend, uint32_t K, uint32_t T,
+                                                             uint32_t* __restrict__ tflags,
+                                                             uint32_t* __restrict__ tlast) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= T) return;
+  const uint64_t g0 = gbeg + (uint64_t)t * K, g1 = min(g0 + K, gend);
+  const uint32_t dmask = (1u << c) - 1;
+  auto bucket = [&](uint64_t g) -> uint32_t {
+    const uint32_t key = entry_key(ents[g]), d = key & dmask;
+    return d ? ((key >> c) << (c - 1)) + (d - 1) : kNoBucket;
+  };
+  const uint32_t prev_b = g0 > gbeg ? bucket(g0 - 1) : kNoBucket;
+  const uint32_t next_b = g1 < gend ? bucket(g1) : kNoBucket;
+  uint32_t first = bucket(g0), last = bucket(g1 - 1);
+  bool single = first == last;
+  if (first == kNoBucket || last == kNoBucket) {
+    uint32_t runs = 0, cur = kNoBucket;
+    first = kNoBucket;
+    for (uint64_t g = g0; g < g1; ++g) {
+      const uint32_t b = bucket(g);
+      if (b != kNoBucket && b != cur) {
+        if (runs == 0) first = b;
+        cur = b;
+        ++runs;
+      }
+    }
+    last = cur;
+    single = runs <= 1;
+  }
+  uint32_t flags = single ? kSingle : 0u;
+  if (first != kNoBucket && first == prev_b) flags |= kHead;
+  if (last != kNoBucket && last == next_b) flags |= kTail;
+  tflags[t] = flags;
+  tlast[t] = last;
+}
+
 __global__ __launch_bounds__(kBlock) void chain_mark_kernel(const uint32_t* __restrict__ tflags, uint32_t T,
-                                                            uint32_t* __restrict__ is_start) {
+                                                            uint32_t* __restrict__ is_start,
+                                                            uint32_t* __restrict__ max_len) {
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t == 0) *max_len = 0;  // seg_count_kernel's atomicMax target (no memset launch)
   if (t > T) return;
   is_start[t] = (t < T && chain_start(tflags[t])) ? 1u : 0u;
 }
@@ -1025,6 +1077,30 @@ __global__ __launch_bounds__(kBlock, 2) void window_segment29_kernel(const XYZZ<
   acc = acc29::add(acc, acc29::small_mul(R, j * L));
   acc29::store_pt(out, t, acc);
 }
+// The last levels of the window sums in ONE launch per MSM: workgroup w
+// reduces window w's S <= kBlock segment sums by a binary tree through LDS
+// (log2 S dependent additions, as the one-launch-per-level binary tree,
+// without a launch per level: 2^16 has S = 64 -> 6 launches of ~12 us, each
+// mostly one latency-bound addition).  (Computing the segment sums in this
+// kernel too, window_segment29_kernel's loop, gave wrong window sums on the
+// GPU although the loop is the same code -- not understood, so not used.)
+__global__ __launch_bounds__(kBlock, 2) void window_tree29_kernel(const XYZZ<Bn254Fq>* __restrict__ in, unsigned S,
+                                                                 XYZZ<Bn254Fq>* __restrict__ out) {
+  __shared__ acc29::Raw sh[kBlock];
+  const uint32_t w = blockIdx.x, j = threadIdx.x;
+  acc29::Pt v{acc29::Acc{}, true};
+  if (j < S) v = acc29::load_pt(in, (size_t)w * S + j);
+  unsigned span = 1;
+  while (span < S) span <<= 1;
+  for (unsigned half = span >> 1; half >= 1; half >>= 1) {
+    if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
+    __syncthreads();
+    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
+    __syncthreads();
+  }
+  if (j == 0) acc29::store_pt(out, w, v);
+}
+
 __global__ __launch_bounds__(kBlock, 2) void reduce_uniform29_kernel(const XYZZ<Bn254Fq>* __restrict__ in, unsigned W,
                                                                     unsigned S_in, unsigned K2,
                                                                     XYZZ<Bn254Fq>* __restrict__ out) {
@@ -1237,6 +1313,28 @@ hipError_t MsmGpu<Curve>::sort_entries(void* tmp, size_t& bytes, const uint64_t*
   }
 }
 
+// Chain tables from the per-thread run flags: a chain = the pieces of one
+// bucket across consecutive threads (head/tail pieces), numbered by a scan
+// of the chain starts; then each chain's first-level piece count, the chain
+// count and the longest chain, read back into h_max_ (pinned) on stream s.
+template <class Curve>
+void MsmGpu<Curve>::build_chains(const uint32_t* flags, const uint32_t* last, size_t T, unsigned K2,
+                                 uint32_t* is_start, uint32_t* cid, uint32_t* cbeg, uint32_t* cend,
+                                 uint32_t* cbucket, uint32_t* lcnt, uint32_t* dscal, hipStream_t s) {
+  hipLaunchKernelGGL(chain_mark_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, s, flags, (uint32_t)T, is_start,
+                     dscal + 1);
+  size_t scan_bytes = 0;
+  TA_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, is_start, cid, 0u, T + 1, rocprim::plus<uint32_t>(), s));
+  void* scan_tmp = scan_tmp_.ensure(scan_bytes);
+  TA_HIP(rocprim::exclusive_scan(scan_tmp, scan_bytes, is_start, cid, 0u, T + 1, rocprim::plus<uint32_t>(), s));
+  hipLaunchKernelGGL(chain_build_kernel, dim3(grid_for(T)), dim3(kBlock), 0, s, flags, last, cid, (uint32_t)T, cbeg,
+                     cend, cbucket, dscal);
+  hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, s, cbeg, cend, dscal, (uint32_t)T, K2,
+                     lcnt, dscal + 1);
+  TA_HIP(hipGetLastError());
+  TA_HIP(hipMemcpyAsync(h_max_, dscal, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+}
+
 template <class Curve>
 void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan,
                             Point* d_windows) {
@@ -1276,8 +1374,14 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * slot));
   Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * slot));
   Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / kJoinFanLong + T + 2) * sizeof(Point)));
-  uint32_t* tflags = static_cast<uint32_t*>(start_.ensure(T * 4));
-  uint32_t* tlast = static_cast<uint32_t*>(end_.ensure(T * 4));
+  // one sort + accumulation group (the default): the chain tables are built
+  // from the sorted keys on a second stream beside the accumulation (see
+  // chain_flags_kernel), from their own copy of the flags
+  const bool early_chains = ngroups == 1;
+  uint32_t* tflags = static_cast<uint32_t*>(start_.ensure(2 * T * 4));
+  uint32_t* tlast = static_cast<uint32_t*>(end_.ensure(2 * T * 4));
+  uint32_t* cflags = early_chains ? tflags + T : tflags;  // what the chain kernels read
+  uint32_t* clast = early_chains ? tlast + T : tlast;
   uint32_t* is_start = static_cast<uint32_t*>(cnt_.ensure((T + 1) * 4));
   uint32_t* cid = static_cast<uint32_t*>(off_a_.ensure((T + 1) * 4));
   // chain tables: beg, end, bucket, level counts/offsets (<= T chains)
@@ -1286,7 +1390,6 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   uint32_t* cend = ctab + (T + 2);
   uint32_t* cbucket = ctab + 2 * (T + 2);
   uint32_t* lcnt = ctab + 3 * (T + 2);
-  uint32_t* loffs[2] = {ctab + 4 * (T + 2), ctab + 5 * (T + 2)};  // join levels' output offsets, ping-pong
   uint32_t* dscal = ctab + 6 * (T + 2);  // [0] nchains, [1] max chain length
 
   unsigned wbits = 0;
@@ -1318,12 +1421,14 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     uint32_t* later = hist + 2 * hn;
     uint32_t* digit_cnt = later + later_places * hn;  // 2 x 256 counts, 2 x 256 offsets, 256 spare
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       Wt, wr0, W, nblocks, spt, later_places, hist, later);
+                       Wt, wr0, W, nblocks, spt, later_places, hist, later, reinterpret_cast<uint4*>(bucket_sum),
+                       nb * slot / 16);
     TA_HIP(hipGetLastError());
     if (later_places > 0) {
       digit_off = digit_cnt + 2 * 256;
       TA_HIP(hipMemsetAsync(digit_cnt, 0, 2 * 256 * 4, stream_));
-      const uint32_t per_chunk = 128, chunks = (nblocks + per_chunk - 1) / per_chunk;
+      // (>= 256 chunks: a 2^16 MSM's 128 recode blocks in one chunk took 17 us of serial loads)
+      const uint32_t per_chunk = std::clamp<uint32_t>(nblocks / 256, 4, 128), chunks = (nblocks + per_chunk - 1) / per_chunk;
       hipLaunchKernelGGL(digit_count_kernel, dim3(chunks, later_places), dim3(kBlock), 0, stream_, later, nblocks,
                          per_chunk, digit_cnt);
       hipLaunchKernelGGL(digit_scan_kernel, dim3(later_places), dim3(kBlock), 0, stream_, digit_cnt, digit_off);
@@ -1350,9 +1455,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
                        Wt, wr0, W, ents);
   }
   TA_HIP(hipGetLastError());
-  // every bucket without an entry stays the identity
-  TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * slot, stream_));
-  TA_HIP(hipMemsetAsync(dscal, 0, 2 * sizeof(uint32_t), stream_));
+  // every bucket without an entry stays the identity (the fused recode clears them)
+  if (!fused) TA_HIP(hipMemsetAsync(bucket_sum, 0, nb * slot, stream_));
   TA_HIP(hipEventRecord(ev_[2], stream_));  // recode done (also the profile mark)
   if (sort_stream != stream_) TA_HIP(hipStreamWaitEvent(sort_stream, ev_[2], 0));
 
@@ -1405,8 +1509,19 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       TA_HIP(hipStreamWaitEvent(stream_, copy_done_, 0));
       pending_host_bases_ = nullptr;
     }
-    if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     const size_t Tg = (ecount + K - 1) / K;
+    if (early_chains) {
+      // chain tables on the side stream, overlapping the accumulation below
+      if (!sort_stream_) TA_HIP(hipStreamCreateWithFlags(&sort_stream_, hipStreamNonBlocking));
+      TA_HIP(hipEventRecord(ev_[6], stream_));  // sorted
+      TA_HIP(hipStreamWaitEvent(sort_stream_, ev_[6], 0));
+      hipLaunchKernelGGL(chain_flags_kernel, dim3(grid_for(T)), dim3(kBlock), 0, sort_stream_, ents2, c, (uint64_t)e0,
+                         (uint64_t)(e0 + ecount), K, (uint32_t)T, cflags, clast);
+      TA_HIP(hipGetLastError());
+      build_chains(cflags, clast, T, plan.K2, is_start, cid, cbeg, cend, cbucket, lcnt, dscal, sort_stream_);
+      TA_HIP(hipEventRecord(ev_[7], sort_stream_));
+    }
+    if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
       if (acc29_) last_schedule_ |= kSchedAcc29;
       if (acc29_)  // 29-bit-limb accumulation (BN254 G1 default; set_variant bits 13 / 17: base prefetch A/B)
@@ -1470,19 +1585,18 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     }
   }
   // ---- join buckets that cross thread boundaries ----
-  hipLaunchKernelGGL(chain_mark_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, stream_, tflags, (uint32_t)T,
-                     is_start);
-  size_t scan_bytes = 0;
-  TA_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, is_start, cid, 0u, T + 1, rocprim::plus<uint32_t>(), stream_));
-  void* scan_tmp = scan_tmp_.ensure(scan_bytes);
-  TA_HIP(rocprim::exclusive_scan(scan_tmp, scan_bytes, is_start, cid, 0u, T + 1, rocprim::plus<uint32_t>(), stream_));
-  hipLaunchKernelGGL(chain_build_kernel, dim3(grid_for(T)), dim3(kBlock), 0, stream_, tflags, tlast, cid,
-                     (uint32_t)T, cbeg, cend, cbucket, dscal);
-  hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for(T + 1)), dim3(kBlock), 0, stream_, cbeg, cend, dscal,
-                     (uint32_t)T, plan.K2, lcnt, dscal + 1);
-  TA_HIP(hipMemcpyAsync(h_max_, dscal, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
-  TA_HIP(hipStreamSynchronize(stream_));
+  // (the chain count and the longest chain decide the levels: read back, from
+  // the side stream while the accumulation still runs when early_chains)
+  if (early_chains) {
+    TA_HIP(hipEventSynchronize(ev_[7]));
+  } else {
+    build_chains(cflags, clast, T, plan.K2, is_start, cid, cbeg, cend, cbucket, lcnt, dscal, stream_);
+    TA_HIP(hipStreamSynchronize(stream_));
+  }
   const uint32_t nchains = h_max_[0], max_len = h_max_[1];
+  // the join levels' offsets depend only on the chain tables: computed on the
+  // side stream (early_chains) ahead of the levels themselves
+  hipStream_t off_stream = early_chains ? sort_stream_ : stream_;
   // Fan-in: 16, or 4-ary levels when a chain is longer than 16 pieces and the
   // accumulation ran fewer than 2^20 threads (the small MSMs' large buckets:
   // there each level's serial additions are latency-bound, 3 per 4-ary level
@@ -1494,30 +1608,48 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   unsigned levels = 0;
   for (size_t len = max_len; len > 1; len = (len + K2 - 1) / K2) ++levels;
   last_levels_ = levels;
-  if (nchains > 0) {
+  if (nchains > 0 && levels > 0) {
     const bool small = nchains <= kJoinSmallChains;  // offsets in one workgroup
+    // phase 1: every level's output offsets (level l's table: segment s of
+    // level l + 1 = [off_l[s], off_l[s + 1])), one table per level
+    const size_t stride = (size_t)nchains + 2;
+    uint32_t* ltab = static_cast<uint32_t*>(lofs_.ensure(levels * stride * 4));
     size_t scan2_bytes = 0;
-    TA_HIP(rocprim::exclusive_scan(nullptr, scan2_bytes, lcnt, loffs[0], 0u, (size_t)nchains + 1,
-                                   rocprim::plus<uint32_t>(), stream_));
-    if (scan2_bytes > scan_bytes) scan_tmp = scan_tmp_.ensure(scan2_bytes);  // (nchains <= T: never grows)
+    void* scan_tmp = nullptr;
+    if (!small) {
+      TA_HIP(rocprim::exclusive_scan(nullptr, scan2_bytes, lcnt, ltab, 0u, (size_t)nchains + 1,
+                                     rocprim::plus<uint32_t>(), off_stream));
+      scan_tmp = scan_tmp_.ensure(scan2_bytes);
+    }
+    for (unsigned l = 0; l < levels; ++l) {
+      uint32_t* loff = ltab + l * stride;
+      const uint32_t* pbeg = l == 0 ? cbeg : ltab + (l - 1) * stride;
+      const uint32_t* pend = l == 0 ? cend : pbeg + 1;
+      if (small) {
+        hipLaunchKernelGGL(join_offsets_kernel, dim3(1), dim3(kJoinOffBlock), 0, off_stream, pbeg,
+                           l == 0 ? pend : nullptr, nchains, K2, loff);
+      } else {
+        if (l > 0 || K2 != plan.K2)  // (level 0's counts came with the read-back, for plan.K2)
+          hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, off_stream,
+                             pbeg, pend, nullptr, nchains, K2, lcnt, nullptr);
+        TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
+                                       rocprim::plus<uint32_t>(), off_stream));
+      }
+    }
+    TA_HIP(hipGetLastError());
+    if (early_chains) {
+      TA_HIP(hipEventRecord(ev_[8], off_stream));
+      TA_HIP(hipStreamWaitEvent(stream_, ev_[8], 0));
+    }
+    // phase 2: the levels, back to back on the MSM stream
     const Point* cur = pieces;
-    const uint32_t* cur_beg = cbeg;
-    const uint32_t* cur_end = cend;
     size_t cur_items = 2 * T;
     Point* dst_bufs[2] = {lvl_buf, pieces};  // pieces is free once level 0 has read it
     for (unsigned l = 0; l < levels; ++l) {
       const bool last = (l + 1 == levels);
-      uint32_t* loff = loffs[l & 1];
-      if (small) {
-        hipLaunchKernelGGL(join_offsets_kernel, dim3(1), dim3(kJoinOffBlock), 0, stream_, cur_beg,
-                           l == 0 ? cur_end : nullptr, nchains, K2, loff);
-      } else {
-        if (l > 0 || K2 != plan.K2)  // (level 0's counts came with the read-back, for plan.K2)
-          hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, stream_, cur_beg,
-                             cur_end, nullptr, nchains, K2, lcnt, nullptr);
-        TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
-                                       rocprim::plus<uint32_t>(), stream_));
-      }
+      const uint32_t* loff = ltab + l * stride;
+      const uint32_t* cur_beg = l == 0 ? cbeg : ltab + (l - 1) * stride;
+      const uint32_t* cur_end = l == 0 ? cend : cur_beg + 1;
       size_t out_items = cur_items / K2 + nchains + 1;
       Point* dst = dst_bufs[l & 1];
       auto* level_kernel = seg_reduce;
@@ -1529,14 +1661,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       hipLaunchKernelGGL(level_kernel, dim3(grid_for(lanes * out_items)), dim3(kBlock), 0, stream_, cur, cur_beg,
                          cur_end, loff, nchains, K2, dst, last ? cbucket : nullptr, bucket_sum);
       TA_HIP(hipGetLastError());
-      if (!last) {
-        // next level reads this level's compact output: segment s = [loff[s], loff[s+1])
-        // (its own offsets go to the other buffer)
-        cur_beg = loff;
-        cur_end = loff + 1;
-        cur = dst;
-        cur_items = out_items;
-      }
+      cur = dst;
+      cur_items = out_items;
     }
   }
 
@@ -1570,6 +1696,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     return;
   }
   unsigned S = B / plan.seg;
+  // BN254 G1 (29-bit reductions): the binary levels until <= kBlock segment
+  // sums per window are left, then one launch for the rest of the tree
+  bool tree29 = false;
+  if constexpr (std::is_same_v<Curve, Bn254G1>) tree29 = acc29_;
   Point* seg_a = static_cast<Point*>(seg_a_.ensure((size_t)W * S * sizeof(Point)));
   Point* seg_b = static_cast<Point*>(seg_b_.ensure((size_t)W * S * sizeof(Point)));
   hipLaunchKernelGGL(win_segment, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, bucket_sum, W, B,
@@ -1582,6 +1712,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // (fan-in 16 -> 2 saved ~0.4 ms at 2^21..2^23)
   constexpr unsigned KW = 2;
   while (S > 1) {
+    if constexpr (std::is_same_v<Curve, Bn254G1>) {
+      if (tree29 && S <= kBlock) {
+        hipLaunchKernelGGL(window_tree29_kernel, dim3(W), dim3(kBlock), 0, stream_, s_cur, S, d_windows);
+        TA_HIP(hipGetLastError());
+        break;
+      }
+    }
     unsigned S_out = (S + KW - 1) / KW;
     Point* dst = (S_out == 1) ? d_windows : s_nxt;
     hipLaunchKernelGGL(win_reduce, dim3(grid_for(lanes * (size_t)W * S_out)), dim3(kBlock), 0, stream_, s_cur, W, S,
@@ -1864,7 +2001,8 @@ size_t MsmGpu<Curve>::work_bytes(size_t n) const {
   // (pieces and bucket sums in the 144-byte Raw format of the BN254 G1 accumulation)
   const size_t slot = std::is_same_v<Curve, Bn254G1> ? std::max<size_t>(sizeof(Point), 144) : sizeof(Point);
   bytes += 2 * T * slot + (2 * T / kJoinFanLong + T + 2) * sizeof(Point);  // pieces + first join level
-  bytes += (T + 2) * 4 * 9;                                                // flags, last bucket, chain tables
+  bytes += (T + 2) * 4 * 11;                                               // flags (x2), last bucket (x2), chain tables
+  bytes += (T + 2) * 4 * 8;                                                // join-level offsets (<= 8 levels of <= T chains)
   bytes += (size_t)p.active() * p.buckets * slot;                           // bucket sums
   bytes += 2 * (size_t)p.active() * (p.buckets / p.seg) * sizeof(Point);
   return bytes + bytes / 10;
@@ -1874,7 +2012,7 @@ template <class Curve>
 size_t MsmGpu<Curve>::held_bytes() const {
   const DeviceBuffer* bufs[] = {&ents_,  &ents2_, &sort_tmp_, &scan_tmp_, &start_, &end_,
                                 &cnt_,   &off_a_, &off_b_, &part_a_, &part_b_,  &seg_a_,    &seg_b_, &buckets_,
-                                &hist_, &hscan_tmp_};
+                                &hist_, &hscan_tmp_, &lofs_};
   size_t s = 0;
   for (const DeviceBuffer* b : bufs) s += b->capacity();
   return s;
