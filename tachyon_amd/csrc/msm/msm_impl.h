@@ -1101,6 +1101,37 @@ __global__ __launch_bounds__(kBlock, 2) void window_tree29_kernel(const XYZZ<Bn2
   if (j == 0) acc29::store_pt(out, w, v);
 }
 
+// Window sums of windows with B <= kBlock buckets (c <= 9: the 2^16 MSM) in
+// one launch, workgroup w = window w: sum_b (b + 1) B_b = sum_k T_k with the
+// suffix sums T_k = sum_{b >= k} B_b, by a Hillis-Steele scan through LDS
+// (log2 B levels of one addition) and a binary tree over the T_k (log2 B
+// more): 14 dependent additions at B = 128 against window_segment29's L = 2
+// running sums plus the (jL) R fix-up (~17) and the tree of the segment sums
+// (6), and one launch instead of two.
+template <bool kRaw>
+__global__ __launch_bounds__(kBlock, 2) void window_scan29_kernel(const XYZZ<Bn254Fq>* __restrict__ bucket_sum,
+                                                                 unsigned B, XYZZ<Bn254Fq>* __restrict__ out) {
+  __shared__ acc29::Raw sh[kBlock];
+  const uint32_t w = blockIdx.x, j = threadIdx.x;
+  acc29::Pt v{acc29::Acc{}, true};
+  if (j < B) v = kRaw ? acc29::load_raw(bucket_sum, (size_t)w * B + j) : acc29::load_pt(bucket_sum, (size_t)w * B + j);
+  for (unsigned d = 1; d < B; d <<= 1) {  // v = T_j
+    acc29::store_raw(sh, j, v);
+    __syncthreads();
+    if (j + d < B) v = acc29::add(v, acc29::load_raw(sh, j + d));
+    __syncthreads();
+  }
+  unsigned span = 1;
+  while (span < B) span <<= 1;
+  for (unsigned half = span >> 1; half >= 1; half >>= 1) {
+    if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
+    __syncthreads();
+    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
+    __syncthreads();
+  }
+  if (j == 0) acc29::store_pt(out, w, v);
+}
+
 __global__ __launch_bounds__(kBlock, 2) void reduce_uniform29_kernel(const XYZZ<Bn254Fq>* __restrict__ in, unsigned W,
                                                                     unsigned S_in, unsigned K2,
                                                                     XYZZ<Bn254Fq>* __restrict__ out) {
@@ -1699,7 +1730,16 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // BN254 G1 (29-bit reductions): the binary levels until <= kBlock segment
   // sums per window are left, then one launch for the rest of the tree
   bool tree29 = false;
-  if constexpr (std::is_same_v<Curve, Bn254G1>) tree29 = acc29_;
+  if constexpr (std::is_same_v<Curve, Bn254G1>) {
+    tree29 = acc29_;
+    if (tree29 && B <= kBlock) {
+      auto* scan = raw ? &window_scan29_kernel<true> : &window_scan29_kernel<false>;
+      hipLaunchKernelGGL(scan, dim3(W), dim3(kBlock), 0, stream_, bucket_sum, B, d_windows);
+      TA_HIP(hipGetLastError());
+      if (profile_) TA_HIP(hipEventRecord(ev_[5], stream_));
+      return;
+    }
+  }
   Point* seg_a = static_cast<Point*>(seg_a_.ensure((size_t)W * S * sizeof(Point)));
   Point* seg_b = static_cast<Point*>(seg_b_.ensure((size_t)W * S * sizeof(Point)));
   hipLaunchKernelGGL(win_segment, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, bucket_sum, W, B,
