@@ -208,7 +208,7 @@ class MsmGpu {
   MsmTimings timings_;
   DeviceBuffer bases_, scalars_, ents_, ents2_, sort_tmp_, scan_tmp_;
   DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_, buckets_;
-  hipEvent_t ev_[9] = {};  // 0-5 phase marks, 6 sorted, 7 chain tables read back, 8 join offsets
+  hipEvent_t ev_[8] = {};  // 0-5 phase marks, 7 chain count read back (early chain tables)
   hipStream_t sort_stream_ = nullptr;  // group sorts run here, overlapping the accumulation on stream_
   std::vector<hipEvent_t> gev_sorted_, gev_acc0_, gev_acc1_;
   unsigned acc_launches_ = 0;

@@ -847,18 +847,16 @@ __global__ __launch_bounds__(kBlock) void seg_count_kernel(const uint32_t* __res
   }
 }
 
-constexpr unsigned kJoinFanLong = 4;  // chain-join fan-in for chains longer than MsmPlan::K2
-
 // A join level's output offsets in ONE workgroup when there are few chains:
 // off[s] = sum over s' < s of ceil(len_s' / K2), len_s = end[s] - beg[s]
 // (end = nullptr: end[s] = beg[s + 1]).  Replaces seg_count + rocPRIM's
 // two-kernel scan (three launches of a few microseconds on a latency-bound
 // level) for nseg <= kJoinSmallChains.
 constexpr unsigned kJoinOffBlock = 1024, kJoinSmallChains = 64 * 1024;
-__global__ __launch_bounds__(kJoinOffBlock) void join_offsets_kernel(const uint32_t* __restrict__ beg,
-                                                                     const uint32_t* __restrict__ end, uint32_t nseg,
-                                                                     unsigned K2, uint32_t* __restrict__ off) {
-  __shared__ uint32_t part[kJoinOffBlock];
+enum ChainMode { kChainsInStream, kChainsBefore, kChainsAfter };  // see MsmGpu::enqueue
+__device__ __forceinline__ void join_offsets_body(const uint32_t* __restrict__ beg, const uint32_t* __restrict__ end,
+                                                  uint32_t nseg, unsigned K2, uint32_t* __restrict__ off,
+                                                  uint32_t* part) {
   const uint32_t t = threadIdx.x, per = (nseg + kJoinOffBlock - 1) / kJoinOffBlock;
   const uint32_t s0 = min(nseg, t * per), s1 = min(nseg, s0 + per);
   auto count = [&](uint32_t s) {
@@ -881,6 +879,46 @@ __global__ __launch_bounds__(kJoinOffBlock) void join_offsets_kernel(const uint3
     run += count(s);
   }
   if (t == kJoinOffBlock - 1) off[nseg] = part[t];
+}
+__global__ __launch_bounds__(kJoinOffBlock) void join_offsets_kernel(const uint32_t* __restrict__ beg,
+                                                                     const uint32_t* __restrict__ end, uint32_t nseg,
+                                                                     unsigned K2, uint32_t* __restrict__ off) {
+  __shared__ uint32_t part[kJoinOffBlock];
+  join_offsets_body(beg, end, nseg, K2, off, part);
+}
+
+// The join levels' count and fan-in from the longest chain (the host makes
+// the same choice from the read-back): 4-ary levels when a chain is longer
+// than K2 pieces and the accumulation ran fewer than 2^20 threads
+constexpr unsigned kJoinFanLong = 4;  // chain-join fan-in for chains longer than MsmPlan::K2
+__host__ __device__ __forceinline__ unsigned join_fan_in(uint32_t max_len, unsigned K2, size_t T) {
+  return (max_len > K2 && T < (size_t(1) << 20)) ? kJoinFanLong : K2;
+}
+__host__ __device__ __forceinline__ unsigned join_levels(uint32_t max_len, unsigned K2) {
+  unsigned levels = 0;
+  for (uint32_t len = max_len; len > 1; len = (len + K2 - 1) / K2) ++levels;
+  return levels;
+}
+
+// Every join level's output offsets in one workgroup, BEFORE the
+// accumulation (small MSMs): the chain count and the longest chain come from
+// the chain tables in device memory (dscal), so nothing waits for the host;
+// level l's table at ltab + l * stride (stride = T + 2 >= chains + 2).
+__global__ __launch_bounds__(kJoinOffBlock) void join_offsets_all_kernel(const uint32_t* __restrict__ beg,
+                                                                         const uint32_t* __restrict__ end,
+                                                                         const uint32_t* __restrict__ dscal,
+                                                                         unsigned K2base, uint32_t T, unsigned lv_max,
+                                                                         size_t stride, uint32_t* __restrict__ ltab) {
+  __shared__ uint32_t part[kJoinOffBlock];
+  const uint32_t nseg = dscal[0], max_len = dscal[1];
+  if (nseg == 0) return;
+  const unsigned K2 = join_fan_in(max_len, K2base, T);
+  const unsigned levels = min(join_levels(max_len, K2), lv_max);
+  for (unsigned l = 0; l < levels; ++l) {
+    const uint32_t* pbeg = l == 0 ? beg : ltab + (l - 1) * stride;
+    join_offsets_body(pbeg, l == 0 ? end : nullptr, nseg, K2, ltab + l * stride, part);
+    __syncthreads();  // the next level reads this table
+  }
 }
 
 // largest s in [0, nseg) with off[s] <= t  (off non-decreasing)
@@ -1405,10 +1443,32 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * slot));
   Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * slot));
   Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / kJoinFanLong + T + 2) * sizeof(Point)));
-  // one sort + accumulation group (the default): the chain tables are built
-  // from the sorted keys on a second stream beside the accumulation (see
-  // chain_flags_kernel), from their own copy of the flags
-  const bool early_chains = ngroups == 1;
+  // Where the chain tables (and the join levels' offsets) are built -- they
+  // depend only on the sorted keys (chain_flags_kernel), so they need not wait
+  // for the accumulation:
+  //  * kChainsInStream: windows with <= 16 K buckets in all (2^16, 2^17):
+  //    before the accumulation, with every level's offsets by one workgroup
+  //    from the device-side counts (join_offsets_all_kernel); the host reads
+  //    the chain count back while the accumulation runs;
+  //  * kChainsBefore: other MSMs of < 2^21 accumulation threads: the tables
+  //    before the accumulation, the read-back during it, the offsets after;
+  //  * kChainsAfter: from the accumulation's flags after it (large MSMs,
+  //    where the tables cost more than the read-back gap they hide, and
+  //    window-group pipelines).
+  // All on the MSM's one stream: a second stream for the tables measured the
+  // same alone, but it shifts the process's stream -> hardware-queue
+  // round-robin (4 queues), which put the Groth16 prover's G1 and G2 MSM
+  // streams on one queue and serialised them (2^20 proof 12.9 -> 14.3 ms,
+  // profiles/r03e/ab_groth16_side_stream.log).
+  const ChainMode chain_mode = ngroups != 1                                        ? kChainsAfter
+                               : (size_t)W * B <= 16384 && T < (size_t(1) << 20) ? kChainsInStream
+                               : T < (size_t(1) << 21)                            ? kChainsBefore
+                                                                                  : kChainsAfter;
+  const bool early_chains = chain_mode != kChainsAfter;
+  const unsigned lv_max =
+      chain_mode == kChainsInStream ? join_levels((uint32_t)std::min<size_t>(2 * T, ~0u), kJoinFanLong) + 1 : 0;
+  uint32_t* early_ltab =
+      chain_mode == kChainsInStream ? static_cast<uint32_t*>(lofs_.ensure(lv_max * (T + 2) * 4)) : nullptr;
   uint32_t* tflags = static_cast<uint32_t*>(start_.ensure(2 * T * 4));
   uint32_t* tlast = static_cast<uint32_t*>(end_.ensure(2 * T * 4));
   uint32_t* cflags = early_chains ? tflags + T : tflags;  // what the chain kernels read
@@ -1541,16 +1601,21 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       pending_host_bases_ = nullptr;
     }
     const size_t Tg = (ecount + K - 1) / K;
-    if (early_chains) {
-      // chain tables on the side stream, overlapping the accumulation below
-      if (!sort_stream_) TA_HIP(hipStreamCreateWithFlags(&sort_stream_, hipStreamNonBlocking));
-      TA_HIP(hipEventRecord(ev_[6], stream_));  // sorted
-      TA_HIP(hipStreamWaitEvent(sort_stream_, ev_[6], 0));
-      hipLaunchKernelGGL(chain_flags_kernel, dim3(grid_for(T)), dim3(kBlock), 0, sort_stream_, ents2, c, (uint64_t)e0,
+    if (chain_mode == kChainsInStream) {
+      hipLaunchKernelGGL(chain_flags_kernel, dim3(grid_for(T)), dim3(kBlock), 0, stream_, ents2, c, (uint64_t)e0,
                          (uint64_t)(e0 + ecount), K, (uint32_t)T, cflags, clast);
       TA_HIP(hipGetLastError());
-      build_chains(cflags, clast, T, plan.K2, is_start, cid, cbeg, cend, cbucket, lcnt, dscal, sort_stream_);
-      TA_HIP(hipEventRecord(ev_[7], sort_stream_));
+      build_chains(cflags, clast, T, plan.K2, is_start, cid, cbeg, cend, cbucket, lcnt, dscal, stream_);
+      hipLaunchKernelGGL(join_offsets_all_kernel, dim3(1), dim3(kJoinOffBlock), 0, stream_, cbeg, cend, dscal,
+                         plan.K2, (uint32_t)T, lv_max, (size_t)T + 2, early_ltab);
+      TA_HIP(hipGetLastError());
+      TA_HIP(hipEventRecord(ev_[7], stream_));  // chain count and longest chain read back
+    } else if (chain_mode == kChainsBefore) {
+      hipLaunchKernelGGL(chain_flags_kernel, dim3(grid_for(T)), dim3(kBlock), 0, stream_, ents2, c, (uint64_t)e0,
+                         (uint64_t)(e0 + ecount), K, (uint32_t)T, cflags, clast);
+      TA_HIP(hipGetLastError());
+      build_chains(cflags, clast, T, plan.K2, is_start, cid, cbeg, cend, cbucket, lcnt, dscal, stream_);
+      TA_HIP(hipEventRecord(ev_[7], stream_));
     }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
@@ -1616,8 +1681,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     }
   }
   // ---- join buckets that cross thread boundaries ----
-  // (the chain count and the longest chain decide the levels: read back, from
-  // the side stream while the accumulation still runs when early_chains)
+  // (the chain count and the longest chain decide the levels: read back
+  // while the accumulation runs when early_chains)
   if (early_chains) {
     TA_HIP(hipEventSynchronize(ev_[7]));
   } else {
@@ -1625,52 +1690,43 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     TA_HIP(hipStreamSynchronize(stream_));
   }
   const uint32_t nchains = h_max_[0], max_len = h_max_[1];
-  // the join levels' offsets depend only on the chain tables: computed on the
-  // side stream (early_chains) ahead of the levels themselves
-  hipStream_t off_stream = early_chains ? sort_stream_ : stream_;
-  // Fan-in: 16, or 4-ary levels when a chain is longer than 16 pieces and the
-  // accumulation ran fewer than 2^20 threads (the small MSMs' large buckets:
-  // there each level's serial additions are latency-bound, 3 per 4-ary level
-  // against 15 per 16-ary one: 2^16 reduction 0.48 -> 0.41 ms; with many
-  // threads the levels are throughput-bound and an extra level of scans costs
-  // more: 2^24 / 2^26 reduction 3.07 / 3.74 -> 3.24 / 4.34 ms 4-ary;
-  // profiles/r03c/ab_join_fan_in.log)
-  const unsigned K2 = (max_len > plan.K2 && T < (size_t(1) << 20)) ? kJoinFanLong : plan.K2;
-  unsigned levels = 0;
-  for (size_t len = max_len; len > 1; len = (len + K2 - 1) / K2) ++levels;
+  const unsigned K2 = join_fan_in(max_len, plan.K2, T);
+  const unsigned levels = join_levels(max_len, K2);
   last_levels_ = levels;
   if (nchains > 0 && levels > 0) {
-    const bool small = nchains <= kJoinSmallChains;  // offsets in one workgroup
     // phase 1: every level's output offsets (level l's table: segment s of
-    // level l + 1 = [off_l[s], off_l[s + 1])), one table per level
-    const size_t stride = (size_t)nchains + 2;
-    uint32_t* ltab = static_cast<uint32_t*>(lofs_.ensure(levels * stride * 4));
-    size_t scan2_bytes = 0;
-    void* scan_tmp = nullptr;
-    if (!small) {
-      TA_HIP(rocprim::exclusive_scan(nullptr, scan2_bytes, lcnt, ltab, 0u, (size_t)nchains + 1,
-                                     rocprim::plus<uint32_t>(), off_stream));
-      scan_tmp = scan_tmp_.ensure(scan2_bytes);
-    }
-    for (unsigned l = 0; l < levels; ++l) {
-      uint32_t* loff = ltab + l * stride;
-      const uint32_t* pbeg = l == 0 ? cbeg : ltab + (l - 1) * stride;
-      const uint32_t* pend = l == 0 ? cend : pbeg + 1;
-      if (small) {
-        hipLaunchKernelGGL(join_offsets_kernel, dim3(1), dim3(kJoinOffBlock), 0, off_stream, pbeg,
-                           l == 0 ? pend : nullptr, nchains, K2, loff);
-      } else {
-        if (l > 0 || K2 != plan.K2)  // (level 0's counts came with the read-back, for plan.K2)
-          hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, off_stream,
-                             pbeg, pend, nullptr, nchains, K2, lcnt, nullptr);
-        TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
+    // level l + 1 = [off_l[s], off_l[s + 1])), one table per level -- already
+    // on the device for the small MSMs (join_offsets_all_kernel)
+    const bool in_stream = chain_mode == kChainsInStream;
+    if (in_stream && levels > lv_max) throw std::runtime_error("tachyon_mi355x: MSM join levels exceed their bound");
+    const size_t stride = in_stream ? T + 2 : (size_t)nchains + 2;
+    uint32_t* ltab = in_stream ? early_ltab : static_cast<uint32_t*>(lofs_.ensure(levels * stride * 4));
+    hipStream_t off_stream = stream_;
+    if (!in_stream) {
+      const bool small = nchains <= kJoinSmallChains;  // offsets in one workgroup
+      size_t scan2_bytes = 0;
+      void* scan_tmp = nullptr;
+      if (!small) {
+        TA_HIP(rocprim::exclusive_scan(nullptr, scan2_bytes, lcnt, ltab, 0u, (size_t)nchains + 1,
                                        rocprim::plus<uint32_t>(), off_stream));
+        scan_tmp = scan_tmp_.ensure(scan2_bytes);
       }
-    }
-    TA_HIP(hipGetLastError());
-    if (early_chains) {
-      TA_HIP(hipEventRecord(ev_[8], off_stream));
-      TA_HIP(hipStreamWaitEvent(stream_, ev_[8], 0));
+      for (unsigned l = 0; l < levels; ++l) {
+        uint32_t* loff = ltab + l * stride;
+        const uint32_t* pbeg = l == 0 ? cbeg : ltab + (l - 1) * stride;
+        const uint32_t* pend = l == 0 ? cend : pbeg + 1;
+        if (small) {
+          hipLaunchKernelGGL(join_offsets_kernel, dim3(1), dim3(kJoinOffBlock), 0, off_stream, pbeg,
+                             l == 0 ? pend : nullptr, nchains, K2, loff);
+        } else {
+          if (l > 0 || K2 != plan.K2)  // (level 0's counts came with the read-back, for plan.K2)
+            hipLaunchKernelGGL(seg_count_kernel, dim3(grid_for((size_t)nchains + 1)), dim3(kBlock), 0, off_stream,
+                               pbeg, pend, nullptr, nchains, K2, lcnt, nullptr);
+          TA_HIP(rocprim::exclusive_scan(scan_tmp, scan2_bytes, lcnt, loff, 0u, (size_t)nchains + 1,
+                                         rocprim::plus<uint32_t>(), off_stream));
+        }
+      }
+      TA_HIP(hipGetLastError());
     }
     // phase 2: the levels, back to back on the MSM stream
     const Point* cur = pieces;
@@ -2042,7 +2098,7 @@ size_t MsmGpu<Curve>::work_bytes(size_t n) const {
   const size_t slot = std::is_same_v<Curve, Bn254G1> ? std::max<size_t>(sizeof(Point), 144) : sizeof(Point);
   bytes += 2 * T * slot + (2 * T / kJoinFanLong + T + 2) * sizeof(Point);  // pieces + first join level
   bytes += (T + 2) * 4 * 11;                                               // flags (x2), last bucket (x2), chain tables
-  bytes += (T + 2) * 4 * 8;                                                // join-level offsets (<= 8 levels of <= T chains)
+  bytes += (T + 2) * 4 * 12;                                               // join-level offsets (<= 12 levels of <= T chains)
   bytes += (size_t)p.active() * p.buckets * slot;                           // bucket sums
   bytes += 2 * (size_t)p.active() * (p.buckets / p.seg) * sizeof(Point);
   return bytes + bytes / 10;
