@@ -35,5 +35,5 @@ mkdir -p $P
 cp $OUT/summary.md $OUT/summary_traffic.md $OUT/pmc_traffic.json $OUT/pmc_r03.json $OUT/micro.log $P/
 cp $OUT/trace/run_kernel_stats.csv $P/kernel_stats.csv
 cp $OUT/g2_trace/run_kernel_stats.csv $P/kernel_stats_bls12_381_g2_2_22.csv
-tail -n 1 $OUT/bench_under_trace.log > $P/bench_under_trace.json
+grep '^{' $OUT/bench_under_trace.log | tail -n 1 > $P/bench_under_trace.json
 echo done
