@@ -151,6 +151,35 @@ def test_msm_non_uniform_all_equal_scalars():
     assert ctx("bn254_g1").run(bases, scalars) == expect
 
 
+@pytest.mark.parametrize("logn", [14, 17, 19])
+@pytest.mark.parametrize("kind", ["random", "non_uniform", "three_scalars"])
+def test_msm_chain_table_modes(logn, kind):
+    """The bucket chains' tables are built from the sorted keys before the
+    accumulation (2^14 / 2^17: with every join level's offsets from the
+    device-side counts; 2^19: tables only) or from the accumulation's flags
+    after it (set_variant bit 2: one window per sort group).  Random scalars
+    (short chains), NonUniform(n, 1) (one bucket per window: the longest
+    chains, the most 4-ary levels) and three repeated scalars (a few long
+    chains among short ones) agree with the oracle in both schedules."""
+    n = 1 << logn
+    bases = O.gen_bases("bn254_g1", 40 + logn, n, 64).tobytes()
+    if kind == "random":
+        scalars = O.gen_scalars("bn254_fr", 40 + logn, n).tobytes()
+    elif kind == "non_uniform":
+        scalars = O.gen_scalars("bn254_fr", 40 + logn, 1).tobytes() * n
+    else:
+        three = O.gen_scalars("bn254_fr", 40 + logn, 3).tobytes()
+        scalars = b"".join(three[32 * (i % 3):32 * (i % 3) + 32] for i in range(n))
+    expect, _ = O.msm("bn254_g1", bases, scalars)
+    m = ctx("bn254_g1")
+    try:
+        for var in (0, 4):
+            m.set_variant(var)
+            assert m.run(bases, scalars) == expect, (logn, kind, var)
+    finally:
+        m.set_variant(0)
+
+
 def test_msm_window_sizes_agree():
     """Any window size gives the same point (MSMCtx only changes the schedule)."""
     n = 3000
