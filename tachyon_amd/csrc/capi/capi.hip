@@ -390,8 +390,10 @@ int tachyon_mi355x_msm_gpu_set_devices(int curve, void* ctx, const int* device_i
   GUARD_BEGIN CURVE_DISPATCH(curve, {
     auto* m = static_cast<MsmCtx<C>*>(ctx);
     m->multi.reset();
-    if (count > 1)
+    if (count > 1) {
       m->multi = std::make_unique<msm::MsmMultiDevice<C>>(std::vector<int>(device_ids, device_ids + count));
+      m->multi->copy_settings(m->impl);  // window bits, variant and profiling forced before set_devices
+    }
   }) GUARD_END
   return 1;
 }
@@ -413,22 +415,35 @@ size_t tachyon_mi355x_msm_gpu_last_shards(int curve, const void* ctx, float* sha
   return 0;
 }
 void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on) {
-  GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_profile(on != 0)) GUARD_END
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    auto* m = static_cast<MsmCtx<C>*>(ctx);
+    m->impl.set_profile(on != 0);
+    if (m->multi) m->multi->set_profile(on != 0);
+  }) GUARD_END
 }
 int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant) {
   if (variant < 0 || (variant & ~msm::kMsmVariantMask)) return 0;  // unknown bits: refused, nothing changed
-  GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.set_variant(variant)) GUARD_END
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    auto* m = static_cast<MsmCtx<C>*>(ctx);
+    m->impl.set_variant(variant);
+    if (m->multi) m->multi->set_variant(variant);
+  }) GUARD_END
   return 1;
 }
 void tachyon_mi355x_msm_gpu_last_timings(int curve, const void* ctx, float* out8) {
   GUARD_BEGIN CURVE_DISPATCH(curve, {
-    const msm::MsmTimings& t = static_cast<const MsmCtx<C>*>(ctx)->impl.timings();
+    // multi-device: the timings of the shard that ran the most points
+    auto* m = static_cast<const MsmCtx<C>*>(ctx);
+    const msm::MsmTimings& t = m->multi ? m->multi->lead().timings() : m->impl.timings();
     out8[0] = t.h2d; out8[1] = t.recode; out8[2] = t.sort; out8[3] = t.prep; out8[4] = t.acc; out8[5] = t.reduce;
     out8[6] = t.total; out8[7] = t.acc_launches;
   }) GUARD_END
 }
 unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx) {
-  GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.last_schedule()) GUARD_END
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    auto* m = static_cast<const MsmCtx<C>*>(ctx);
+    return m->multi ? m->multi->lead().last_schedule() : m->impl.last_schedule();
+  }) GUARD_END
   return 0;
 }
 double tachyon_mi355x_msm_madd_ceiling(int curve, int field_bits) {
@@ -436,7 +451,10 @@ double tachyon_mi355x_msm_madd_ceiling(int curve, int field_bits) {
   return 0.0;
 }
 size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx) {
-  GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.last_divisions()) GUARD_END
+  GUARD_BEGIN CURVE_DISPATCH(curve, {
+    auto* m = static_cast<const MsmCtx<C>*>(ctx);
+    return m->multi ? m->multi->last_divisions() : m->impl.last_divisions();
+  }) GUARD_END
   return 0;
 }
 void tachyon_mi355x_msm_plan(int curve, size_t size, unsigned* c, unsigned* windows) {

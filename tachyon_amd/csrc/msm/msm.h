@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0x7FFBF;
+constexpr int kMsmVariantMask = 0xFFFBF;  // bits 0-19 except 6
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
@@ -171,14 +171,17 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-11; see run_windows).  Every variant
+  // A/B tuning knobs (bits 0-5, 7-19; see run_windows).  Every variant
   // computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 11 are refused.
+  // experiment) and anything above bit 19 are refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;
   }
   void set_profile(bool on) { profile_ = on; }
+  unsigned force_window_bits() const { return force_c_; }
+  int variant() const { return variant_; }
+  bool profile() const { return profile_; }
   const MsmTimings& timings() const { return timings_; }
   hipStream_t stream() const { return stream_; }
   unsigned last_levels() const { return last_levels_; }

@@ -1138,6 +1138,38 @@ __global__ __launch_bounds__(kBlock, 2) void window_tree29_kernel(const XYZZ<Bn2
   }
   if (j == 0) acc29::store_pt(out, w, v);
 }
+// window_segment29 + window_tree29 in one launch (S = B / L <= kBlock segment
+// sums per window): thread j of workgroup w computes segment j's sum exactly
+// as window_segment29_kernel does, then the LDS tree.  Every thread reaches
+// every barrier (no early return).  set_variant bit 19 (A/B).
+template <bool kRaw>
+__global__ __launch_bounds__(kBlock, 2) void window_segtree29_kernel(const XYZZ<Bn254Fq>* __restrict__ bucket_sum,
+                                                                    unsigned B, unsigned L,
+                                                                    XYZZ<Bn254Fq>* __restrict__ out) {
+  __shared__ acc29::Raw sh[kBlock];
+  const uint32_t S = B / L;
+  const uint32_t w = blockIdx.x, j = threadIdx.x;
+  acc29::Pt v{acc29::Acc{}, true};
+  if (j < S) {
+    const size_t b0 = (size_t)w * B + (size_t)j * L;
+    acc29::Pt R{acc29::Acc{}, true};
+    v = R;
+    for (int k = (int)L - 1; k >= 0; --k) {
+      R = acc29::add(R, kRaw ? acc29::load_raw(bucket_sum, b0 + k) : acc29::load_pt(bucket_sum, b0 + k));
+      v = acc29::add(v, R);
+    }
+    v = acc29::add(v, acc29::small_mul(R, j * L));
+  }
+  unsigned span = 1;
+  while (span < S) span <<= 1;
+  for (unsigned half = span >> 1; half >= 1; half >>= 1) {
+    if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
+    __syncthreads();
+    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
+    __syncthreads();
+  }
+  if (j == 0) acc29::store_pt(out, w, v);
+}
 
 // Window sums of windows with B <= kBlock buckets (c <= 9: the 2^16 MSM) in
 // one launch, workgroup w = window w: sum_b (b + 1) B_b = sum_k T_k with the
@@ -1791,6 +1823,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if (tree29 && B <= kBlock) {
       auto* scan = raw ? &window_scan29_kernel<true> : &window_scan29_kernel<false>;
       hipLaunchKernelGGL(scan, dim3(W), dim3(kBlock), 0, stream_, bucket_sum, B, d_windows);
+      TA_HIP(hipGetLastError());
+      if (profile_) TA_HIP(hipEventRecord(ev_[5], stream_));
+      return;
+    }
+    if (tree29 && (variant_ & (1u << 19)) && S <= kBlock) {
+      auto* segtree = raw ? &window_segtree29_kernel<true> : &window_segtree29_kernel<false>;
+      hipLaunchKernelGGL(segtree, dim3(W), dim3(kBlock), 0, stream_, bucket_sum, B, plan.seg, d_windows);
       TA_HIP(hipGetLastError());
       if (profile_) TA_HIP(hipEventRecord(ev_[5], stream_));
       return;

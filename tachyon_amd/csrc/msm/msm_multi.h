@@ -77,8 +77,34 @@ class MsmMultiDevice {
   const std::vector<float>& last_shard_ms() const { return shard_ms_; }
   const std::vector<size_t>& last_shard_points() const { return shard_n_; }
 
+  // The single-device settings reach every shard (set_devices copies the
+  // context's current ones in with copy_settings).
   void set_force_window_bits(unsigned c) {
     for (auto& s : shards_) s->msm->set_force_window_bits(c);
+  }
+  void set_variant(int v) {
+    for (auto& s : shards_) s->msm->set_variant(v);
+  }
+  void set_profile(bool on) {
+    for (auto& s : shards_) s->msm->set_profile(on);
+  }
+  void copy_settings(const MsmGpu<Curve>& from) {
+    set_force_window_bits(from.force_window_bits());
+    set_variant(from.variant());
+    set_profile(from.profile());
+  }
+  // The shard that ran the most points in the last run (shard 0 unless it was
+  // empty): its timings / schedule stand for the run.
+  const MsmGpu<Curve>& lead() const {
+    size_t best = 0;
+    for (size_t k = 1; k < shard_n_.size(); ++k)
+      if (shard_n_[k] > shard_n_[best]) best = k;
+    return *shards_[best]->msm;
+  }
+  size_t last_divisions() const {
+    size_t d = 0;
+    for (auto& s : shards_) d = std::max(d, s->msm->last_divisions());
+    return d;
   }
 
   Point run(const void* bases, const void* scalars, size_t n) {

@@ -33,7 +33,7 @@ def test_msm_golden(curve):
         assert ctx(curve).run(bases, scalars).hex() == c["expected"], (c["n"], c.get("label"))
 
 
-@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096, 16384, 131072, 262144])
+@pytest.mark.parametrize("variant", [4096, 8192, 8192 | 4096, 16384, 131072, 262144, 524288])
 def test_msm_golden_bn254_g1_variants(variant):
     """The golden edge cases (zero scalars, identity bases, P + (-P), doubling
     inside a bucket, r - 1, Easy KAT) through the workgroup-tree window
@@ -43,6 +43,8 @@ def test_msm_golden_bn254_g1_variants(variant):
     g = json.load(open(os.path.join(GOLDEN, "msm.json")))["bn254_g1"]
     m = VariableBaseMSMGpu("bn254_g1")
     m.set_variant(variant)
+    if variant == 524288:  # bit 19 (one-launch segment sums + tree) needs S = B / L <= 256: c = 10
+        m.set_window_bits(10)
     for c in g["cases"]:
         bases = b"".join(bytes.fromhex(x) for x in c["bases"])
         scalars = b"".join(bytes.fromhex(x) for x in c["scalars"])
@@ -368,7 +370,7 @@ def test_msm_schedule_variants_agree(curve, logn):
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
         for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384,
-                  32768, 65536, 131072, 262144):
+                  32768, 65536, 131072, 262144, 524288):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
@@ -379,7 +381,7 @@ def test_msm_schedule_variants_agree(curve, logn):
                 assert s["acc29"] == (v != 262144), (hex(v), s)
             else:  # G2: the lane pair by default; bit 15 the one-lane kernel
                 assert s["lane_pair"] == (v != 32768), (hex(v), s)
-        for bad in (64, 1 << 19):
+        for bad in (64, 1 << 20):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:

@@ -96,6 +96,34 @@ def test_large_host_shards_pipelined():
     m.close()
 
 
+def test_settings_reach_every_shard():
+    """set_variant / set_profile / set_window_bits reach the shards, whether
+    they are set before or after set_devices, and last_schedule / last_timings
+    report a shard that ran (they used to report the idle
+    single-device context)."""
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    n = 1 << 13
+    bases = O.gen_bases("bn254_g1", 41, n, 64).tobytes()
+    scalars = O.gen_scalars("bn254_fr", 41, n).tobytes()
+    want, _ = O.msm("bn254_g1", bases, scalars)
+    m = VariableBaseMSMGpu("bn254_g1")
+    m.set_variant(262144)  # bit 18: the FIPS 32-bit field, visible in last_schedule
+    m.set_profile(True)
+    m.set_devices([0, 0])
+    assert m.run(bases, scalars) == want
+    s = m.last_schedule()
+    assert s["acc29"] is False, s
+    t = m.last_timings()
+    assert t["acc"] > 0 and t["total"] > 0, t
+    m.set_variant(0)  # after set_devices
+    assert m.run(bases, scalars) == want
+    assert m.last_schedule()["acc29"] is True
+    m.set_window_bits(7)
+    assert m.run(bases, scalars) == want
+    m.set_devices([])
+    m.close()
+
+
 def test_set_devices_refuses_bad_ids():
     from tachyon_amd.msm import VariableBaseMSMGpu
     m = VariableBaseMSMGpu("bn254_g1")
