@@ -248,6 +248,20 @@ def bench_bls(args, rank, world, barrier, dist, backend):
             dt = float(t.item())
         leg = out[curve.split("_")[-1]] = {"ms_per_msm": dt * 1e3, "scalars_per_s": n_total / dt,
                                            "consistent": res == ref, "points_per_gpu": n}
+        if world == 1 and not args.no_sweep:
+            # the per-rank shards of this MSM at N = 2, 4, 8 (prefixes of the same input) and the
+            # point-shard projection built on them
+            sw = {str(args.bls_log_n): {"ms": round(dt * 1e3, 3)}}
+            for k in range(args.bls_log_n - 3, args.bls_log_n):
+                msm.run(d_b, d_s, 1 << k)
+                ts = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    msm.run(d_b, d_s, 1 << k)
+                    ts.append(time.perf_counter() - t0)
+                sw[str(k)] = {"ms": round(sorted(ts)[1] * 1e3, 3), "scalars_per_s": (1 << k) / sorted(ts)[1]}
+            leg["shard_sweep"] = sw
+            leg["projected_scaling"] = project_msm_scaling(curve, args.bls_log_n, sw)
         msm.close()
         if world == 1 and not args.no_cpu_baseline:
             # the reference's GPU-vs-CPU check (variable_base_msm_gpu_unittest.cc:25-78) at the timed
@@ -309,6 +323,100 @@ def full_msm_equals(curve, n_total, sharded, rank, dist):
     t = torch.tensor([ok], dtype=torch.int32, device="cuda" if dist.get_backend() == "nccl" else "cpu")
     dist.broadcast(t, 0)
     return bool(t.item())
+
+
+# xGMI figures for the N-GPU projections (MI355X_MICROARCH.md: 7 links x ~153 GB/s
+# per GPU, taken as ~76 GB/s per direction per link) and a small-message RCCL
+# all-gather latency; both are ASSUMPTIONS (no multi-GPU box here), every other
+# term of a projection is measured in this run.
+XGMI_LINK_GBS = 76.0
+RCCL_SMALL_ALLGATHER_MS = 0.03
+
+
+def combine_cost_ms(curve, world, reps=20):
+    """Measured, on this GPU: the host side of D.sharded_msm's combine for
+    `world` ranks -- the partial to a device tensor, the gathered N-point buffer
+    back to the host, and the host group sum of N affine points (the RCCL
+    collective itself is RCCL_SMALL_ALLGATHER_MS, assumed)."""
+    import torch
+    from tachyon_amd import msm as M
+    from tachyon_amd._lib import CURVE_INFO
+    pb = CURVE_INFO[curve][0]
+    g = torch.empty(world * pb, dtype=torch.uint8, device="cuda")
+    M.gen_bases(curve, SEED + 9, world, 1, g.data_ptr())
+    torch.cuda.synchronize()
+    pts = g.cpu().numpy().tobytes()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        t = torch.frombuffer(bytearray(pts[:pb]), dtype=torch.uint8).to("cuda")
+        g[:pb].copy_(t)
+        blob = g.cpu().numpy().tobytes()
+        M.affine_sum(curve, blob)
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2] * 1e3
+
+
+def project_msm_scaling(curve, log_n, sweep):
+    """Point-shard projection of the 2^log_n MSM onto N = 2, 4, 8 GPUs from
+    THIS run's single-GPU shard times (the 2^(log_n - log N) entries of the
+    sweep, prefixes of the same input): per rank T_shard + the combine (host
+    side measured here + the assumed RCCL all-gather latency).  Efficiency =
+    projected value / (N x the 1-GPU value)."""
+    t1 = sweep[str(log_n)]["ms"]
+    out = {"model": "t(N) = t_1gpu(2^log_n / N points, measured above) + combine (measured host side + "
+                    f"{RCCL_SMALL_ALLGATHER_MS} ms assumed RCCL small all-gather)", "t1_ms": t1}
+    for lg_world in (1, 2, 3):
+        world = 1 << lg_world
+        key = str(log_n - lg_world)
+        if key not in sweep:
+            continue
+        comb = combine_cost_ms(curve, world) + RCCL_SMALL_ALLGATHER_MS
+        t = sweep[key]["ms"] + comb
+        out[f"n{world}"] = {"shard_log_n": log_n - lg_world, "shard_ms": sweep[key]["ms"],
+                            "combine_ms": round(comb, 4), "ms": round(t, 3),
+                            "scalars_per_s": (1 << log_n) / (t * 1e-3), "efficiency": round(t1 / (world * t), 3)}
+    return out
+
+
+def project_ntt_scaling(log_n, t1_ms, reps=20):
+    """Four-step projection of the 2^log_n NTT onto N = 2, 4, 8 GPUs: rank 0's
+    two local stages of the N-rank plan timed on this GPU (tachyon_mi355x_bn254_ntt4,
+    the same kernels the sharded bench runs) + the all-to-all as its per-pair
+    bytes over one xGMI link (XGMI_LINK_GBS, assumed; pairs run in parallel on
+    the N - 1 links) + RCCL_SMALL_ALLGATHER_MS of latency."""
+    import torch
+    from tachyon_amd import msm as M
+    from tachyon_amd.ntt import FourStepNtt
+    out = {"model": f"t(N) = rank 0's local stages (measured) + n/N^2 x 32 B per pair at {XGMI_LINK_GBS} GB/s "
+                    f"per xGMI link (assumed) + {RCCL_SMALL_ALLGATHER_MS} ms", "t1_ms": t1_ms}
+    for world in (2, 4, 8):
+        plan = FourStepNtt(log_n, world, 0)
+        m = plan.local_size
+        x = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
+        y = torch.empty_like(x)
+        M.gen_scalars("bn254_fr", SEED + 1, m, x.data_ptr())
+        torch.cuda.synchronize()
+        s = plan.torch_stream
+        for _ in range(2):
+            plan.run_stage(1, False, x, y)
+            plan.run_stage(2, False, y, x)
+        s.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            plan.run_stage(1, False, x, y)
+            plan.run_stage(2, False, y, x)
+        s.synchronize()
+        local = (time.perf_counter() - t0) / reps * 1e3
+        plan.close()
+        pair_bytes = (1 << log_n) // (world * world) * 32
+        a2a = pair_bytes / (XGMI_LINK_GBS * 1e9) * 1e3 + RCCL_SMALL_ALLGATHER_MS
+        t = local + a2a
+        out[f"n{world}"] = {"local_stages_ms": round(local, 4), "all_to_all_ms_model": round(a2a, 4),
+                            "ms": round(t, 4), "elems_per_s": (1 << log_n) / (t * 1e-3),
+                            "efficiency": round(t1_ms / (world * t), 3)}
+        del x, y
+    return out
 
 
 def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backend=None):
@@ -537,10 +645,13 @@ def main():
                           "note": "n x windows mixed additions per launch / launch time; peak = " + MADD_PEAK_NOTE},
     }
 
-    # ---- configs[1] sweep (2^16, 2^20 .. 2^24: prefixes of the same device-resident input) ----
+    # ---- configs[1] sweep (2^16, 2^20 .. 2^25: prefixes of the same device-resident input; 2^25 / 2^24 /
+    # 2^23 are the per-rank shards of the 2^26 MSM at N = 2 / 4 / 8, priced in projected_scaling) ----
     if world == 1 and args.log_n >= 24 and not args.no_sweep:
         sweep = {}
-        for k in (16, 20, 22, 24):
+        for k in (16, 20, 21, 22, 23, 24, 25):
+            if k >= args.log_n:
+                continue
             m = 1 << k
             msm.run(d_bases, d_scalars, m)
             ts = []
@@ -552,6 +663,7 @@ def main():
             sweep[str(k)] = {"ms": round(best * 1e3, 3), "scalars_per_s": m / best}
         sweep[str(args.log_n)] = {"ms": round(ms_per_step, 3), "scalars_per_s": value}
         out["msm_sweep"] = sweep
+        out["projected_scaling"] = {"msm": project_msm_scaling("bn254_g1", args.log_n, sweep)}
 
     # ---- NonUniform(n, 1) test set (variable_base_msm_test_set.h:43-53), the set of the reference's
     # published GPU table (benchmark/msm/README.md:97-111): every scalar equal, so every window puts
@@ -647,41 +759,66 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / (2 * reps)
         round_trip_ok = bool(torch.equal(x, orig))
+        # forward-only and inverse-only loops (back to back on the domain's
+        # stream, wall time / transform): the rooflines' denominator is the
+        # forward loop's time, not the profile-mode events (which add an event
+        # record between passes)
+        y = x.clone()
+        torch.cuda.synchronize()
+        dir_ms = {}
+        for inv in (False, True):
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                dom.transform_device(y.data_ptr(), inverse=inv)
+            s.synchronize()
+            dir_ms["inverse" if inv else "forward"] = (time.perf_counter() - t0) / reps * 1e3
+        del y
         dom.set_profile(True)
         dom.transform_device(x.data_ptr(), inverse=False)
         s.synchronize()
         tot, passes = dom.last_timings()
         dom.set_profile(False)
+        dom.transform_device(x.data_ptr(), inverse=True)  # back to orig
+        s.synchronize()
         ntt_in = orig.cpu().numpy()
-        ntt_gpu_out = x.cpu().numpy()  # FFT of the input (the round trips left x == orig)
-        avg_pass = sum(passes) / len(passes)
+        dom.transform_device(x.data_ptr(), inverse=False)
+        s.synchronize()
+        ntt_gpu_out = x.cpu().numpy()  # FFT of the input
+        fwd_ms = dir_ms["forward"]
         # 64 B per element per TRANSFORM (read + write the array
-        # once), over the transform's kernel time (all passes)
-        xform_ms = sum(passes)
-        xform_gbs = nn * NTT_BYTES_PER_ELEM / (xform_ms * 1e-3) / 1e9
+        # once), over the timed forward transform (all passes + launch gaps)
+        xform_gbs = nn * NTT_BYTES_PER_ELEM / (fwd_ms * 1e-3) / 1e9
+        # pass shares from the profile events, applied to the timed transform
+        share = [p / sum(passes) for p in passes]
+        pass_ms_timed = [round(fwd_ms * f, 4) for f in share]
+        avg_pass = fwd_ms / len(passes)
         pass_gbs = nn * NTT_BYTES_PER_ELEM / (avg_pass * 1e-3) / 1e9
         ntt_traffic, ntt_traffic_src, _ = pmc_traffic("dif_pass_kernel")
-        # algorithmic butterflies (one Montgomery product each) per pass: n/2 x log n / passes
-        ntt_gmulmod = nn // 2 * args.ntt_log_n / len(passes) / (avg_pass * 1e-3) / 1e9
+        # algorithmic butterflies (one product each) per transform: n/2 x log n
+        ntt_gmulmod = nn // 2 * args.ntt_log_n / (fwd_ms * 1e-3) / 1e9
         out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
-                      "round_trip_ok": round_trip_ok, "pass_ms": passes, "mode": "single GPU",
+                      "ms_forward": round(fwd_ms, 4), "ms_inverse": round(dir_ms["inverse"], 4),
+                      "round_trip_ok": round_trip_ok, "pass_ms_events": passes, "pass_ms": pass_ms_timed,
+                      "mode": "single GPU",
                       "roofline": {"bound": "hbm", "achieved": xform_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": xform_gbs / HBM_PEAK_GBS, "traffic": ntt_traffic,
                                    "traffic_unit": "GB per dif_pass_kernel launch",
                                    "traffic_source": ntt_traffic_src,
-                                   "kernel": "dif_pass_kernel (all passes of one transform)",
-                                   "transform_kernel_ms": xform_ms, "passes": len(passes), "kernel_ms": avg_pass,
+                                   "kernel": "dif_pass_kernel (all passes of one forward transform)",
+                                   "transform_ms": fwd_ms, "passes": len(passes), "kernel_ms": avg_pass,
                                    "per_pass_gbs": pass_gbs,
                                    "note": "algorithmic bytes = SURVEY 8(d)'s 64 B per element per transform / the "
-                                           "summed HIP-event time of the transform's passes; per_pass_gbs prices "
-                                           "one pass's own read + write",
+                                           "timed forward transform (back-to-back loop, wall / transform); "
+                                           "per_pass_gbs prices one pass's own read + write at the average pass",
                                    "stream_copy_gbs": stream_gbs, "frac_of_stream_copy": xform_gbs / stream_gbs},
                       "valu_roofline": {"bound": "valu", "kernel": "dif_pass_kernel", "achieved": ntt_gmulmod,
                                         "peak": MULMOD_PEAK_G, "unit": "G mulmod/s",
                                         "frac": ntt_gmulmod / MULMOD_PEAK_G,
-                                        "note": "n/2 x log n butterflies per transform / passes, one product "
-                                                "each (the add/sub of a butterfly are not counted); peak = "
-                                                + MULMOD_PEAK_NOTE}}
+                                        "note": "n/2 x log n butterflies per forward transform / its timed ms, "
+                                                "one product each (the add/sub of a butterfly are not counted); "
+                                                "peak = " + MULMOD_PEAK_NOTE}}
+        if not args.no_sweep and "projected_scaling" in out:
+            out["projected_scaling"]["ntt"] = project_ntt_scaling(args.ntt_log_n, dt * 1e3)
         if not args.no_host_resident:
             # reference semantics (fft_runner.h:53-58): host vector in, H2D + transform + D2H
             hv = ntt_in.copy()

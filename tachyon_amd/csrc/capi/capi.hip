@@ -799,6 +799,11 @@ void tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(tachyon_bn254
                                                                    int on) {
   d->impl->set_profile(on != 0);
 }
+int tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(tachyon_bn254_univariate_evaluation_domain* d,
+                                                                  int variant) {
+  GUARD_BEGIN return d->impl->set_variant(variant) ? 1 : 0; GUARD_END
+  return 0;
+}
 int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(const tachyon_bn254_univariate_evaluation_domain* d,
                                                                    float* total_ms, float* pass_ms, int max_passes) {
   const auto& t = d->impl->timings();

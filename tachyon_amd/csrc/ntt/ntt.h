@@ -64,6 +64,11 @@ class NttDomain {
 
   void set_profile(bool on) { profile_ = on; }
   const NttTimings& timings() const { return timings_; }
+  // A/B kernel variants; bit 0: BN254 Fr on the 8 x 32-bit-limb passes
+  // (dif_pass_kernel) instead of the 9 x 29-bit ones (dif29_pass_kernel, the
+  // default).  Unknown bits (or bit 0 on other fields): refused, returns false.
+  bool set_variant(int v);
+  int variant() const { return variant_; }
 
   struct Pass {
     uint32_t s0, k, log_m;
@@ -73,7 +78,10 @@ class NttDomain {
 
  private:
   void run(Fr* d_data, bool inverse, size_t batch);
+  void run29(Fr* d_data, bool inverse, size_t batch);
   void build_twiddles();
+  void build_tables29();
+  void ensure_tables32();
   void build_powers(const Fr& base, const Fr& scale, Fr* d_lo, Fr* d_hi);
 
   size_t n_ = 0;
@@ -90,6 +98,12 @@ class NttDomain {
   DeviceBuffer twm_fwd_, twm_inv_;  // Montgomery twiddles when tw_* hold Shoup entries (BN254 Fr)
   int shoup_mode_ = 2;              // Shoup twiddles: 0 never, 1 every pass, 2 all but the first pass
   int ntt_variant_ = 0;             // A/B kernel variants (TACHYON_NTT_VARIANT, see run())
+  // BN254 Fr: the 29-bit-limb passes and their tables -- R'-form entries for
+  // the first pass's stages [0, k0), Shoup entries for the later stages
+  int variant_ = 0;
+  bool tables32_ = false;  // the 32-bit Shoup tables (built on first use of variant bit 0)
+  size_t split29_ = 0;     // = n - (n >> k0): stage-table entries before the Shoup part
+  DeviceBuffer t29m_fwd_, t29m_inv_, t29s_fwd_, t29s_inv_, scratch29_;
   DeviceBuffer coset_lo_, coset_hi_, icoset_lo_, icoset_hi_;
   NttTimings timings_;
   std::vector<hipEvent_t> ev_;

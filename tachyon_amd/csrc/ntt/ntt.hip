@@ -3,6 +3,8 @@
 // univariate_evaluation_domain.h:141-232,464-489,518-566, radix2_twiddle_cache.h:57-121.
 #include "ntt.h"
 
+#include "../field/fr29.h"
+
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -224,6 +226,212 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// BN254 Fr passes over 9 x 29-bit limbs (field/fr29.h): the same DIF network,
+// pass plan, index maps, bit reversal and fused scalings as dif_pass_kernel,
+// with the butterflies of fr29::radix4 / radix2 (carry-free products, limb-wise
+// sums and differences).  Elements between passes are 36-byte F29 (normalized,
+// < 8p); the first pass reads the 32-byte Montgomery input, the final pass
+// writes canonical 32-byte values.  LDS holds the elements as 9 limb planes
+// of kMaxLdsElems words (a plane stride fixed at compile time: one ds_read_b32
+// per limb with an immediate offset).  Twiddles: R'-form (36 B) in the first
+// pass, whose stage tables stream from HBM; Shoup (72 B) in the later ones.
+using fr29::F29;
+template <class TwT>
+struct Tw29Table {
+  const TwT* tw;  // entry of (stage s, index j) at tw[(n - (n >> s)) - off + j]
+  uint32_t off;
+};
+
+__device__ __forceinline__ F29 lds29_load(const uint32_t* __restrict__ lds, uint32_t pos) {
+  F29 v;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) v.l[i] = lds[i * kMaxLdsElems + pos];
+  return v;
+}
+__device__ __forceinline__ void lds29_store(uint32_t* __restrict__ lds, uint32_t pos, const F29& v) {
+#pragma unroll
+  for (int i = 0; i < 9; ++i) lds[i * kMaxLdsElems + pos] = v.l[i];
+}
+
+template <int R, bool kLast, class TwT, class IndexFn>
+__device__ __forceinline__ void radix29_step(uint32_t* __restrict__ lds, Tw29Table<TwT> tt,
+                                             const PassArgs<Bn254Fr>& a, uint32_t t, IndexFn index) {
+  constexpr int E = 1 << R;
+  const uint32_t log_m = a.log_m, M = 1u << log_m;
+  const uint32_t n = 1u << a.L;
+  const uint32_t groups = (M << a.k) >> R;
+  const uint32_t qlog = a.k - t - R;
+  const uint32_t st = a.s0 + t;
+  const TwT* twA = tt.tw + ((n - (n >> st)) - tt.off);
+  const uint32_t gapA = (1u << (a.L - st - 1)) - 1;
+  for (uint32_t g = threadIdx.x; g < groups; g += kBlock) {
+    const uint32_t m = g & (M - 1);
+    const uint32_t rr = g >> log_m;
+    const uint32_t off = rr & ((1u << qlog) - 1);
+    const uint32_t a0 = ((rr >> qlog) << (qlog + R)) + off;
+    if constexpr (R == 2) {
+      // twiddles first: their loads overlap the LDS reads
+      TwT tA0, tA1, tB0, tB1;
+      if constexpr (kLast) {
+        tA1 = twA[1];  // stage L - 2 has the two entries {1, w_4}; everything else is 1
+      } else {
+        const TwT* twB = tt.tw + ((n - (n >> (st + 1))) - tt.off);
+        const uint32_t gapB = (1u << (a.L - st - 2)) - 1;
+        tA0 = twA[index(a0, m) & gapA];
+        tA1 = twA[index(a0 + (1u << qlog), m) & gapA];
+        tB0 = twB[index(a0, m) & gapB];
+        tB1 = twB[index(a0 + (2u << qlog), m) & gapB];
+      }
+      F29 x[4];
+#pragma unroll
+      for (int j = 0; j < E; ++j) x[j] = lds29_load(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m);
+      if constexpr (kLast) fr29::radix4_last(x, tA1);
+      else fr29::radix4(x, tA0, tA1, tB0, tB1);
+#pragma unroll
+      for (int j = 0; j < E; ++j) lds29_store(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m, x[j]);
+    } else {
+      TwT tA;
+      if constexpr (!kLast) tA = twA[index(a0, m) & gapA];
+      F29 x[2];
+#pragma unroll
+      for (int j = 0; j < E; ++j) x[j] = lds29_load(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m);
+      if constexpr (kLast) fr29::radix2_last(x);
+      else fr29::radix2(x, tA);
+#pragma unroll
+      for (int j = 0; j < E; ++j) lds29_store(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m, x[j]);
+    }
+  }
+}
+
+// kFirst: the input is the 32-byte Montgomery array (the transform's first
+// pass, R'-form twiddles); otherwise 36-byte F29 from the previous pass.
+template <bool kFirst, class TwT>
+__global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restrict__ in_v, void* __restrict__ out_v,
+                                                            Tw29Table<TwT> tt, PassArgs<Bn254Fr> a) {
+  __shared__ uint32_t lds[9 * kMaxLdsElems];
+  const uint32_t L = a.L, k = a.k, log_m = a.log_m;
+  const uint32_t M = 1u << log_m;
+  const uint32_t elems = M << k;
+  const uint32_t b = blockIdx.x;
+  uint32_t hi_shift = L - a.s0;
+  uint32_t mid_shift = L - a.s0 - k;
+  uint32_t hi = 0, lo_base = 0, r0 = 0;
+  if (!a.final_pass) {
+    uint32_t lo_blocks = (1u << mid_shift) >> log_m;
+    hi = b / lo_blocks;
+    lo_base = (b - hi * lo_blocks) << log_m;
+  } else {
+    r0 = b << log_m;
+  }
+  auto index = [&](uint32_t mid, uint32_t m) -> uint32_t {
+    if (!a.final_pass) return (hi << hi_shift) + (mid << mid_shift) + lo_base + m;
+    uint32_t h = bitrev(r0 + m, L - k);
+    return (h << k) + mid;
+  };
+
+  // ---- load ----
+  const size_t batch_off = (size_t)blockIdx.y << L;
+  for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
+    const uint32_t mid = e >> log_m, m = e & (M - 1);
+    const uint32_t i = index(mid, m);
+    F29 v;
+    if constexpr (kFirst) {
+      Bn254Fr x = static_cast<const Bn254Fr*>(in_v)[batch_off + i];
+      if (a.mode & kLoadCoset) x = x * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
+      v = fr29::from_words(x.v);
+    } else {
+      v = static_cast<const F29*>(in_v)[batch_off + i];
+    }
+    lds29_store(lds, e, v);
+  }
+  __syncthreads();
+
+  for (uint32_t t = 0; t < k;) {
+    const uint32_t R = min(2u, k - t);
+    const bool last = a.final_pass && t + R == k;
+    if (R == 2) {
+      if (last) radix29_step<2, true>(lds, tt, a, t, index);
+      else radix29_step<2, false>(lds, tt, a, t, index);
+    } else {
+      if (last) radix29_step<1, true>(lds, tt, a, t, index);
+      else radix29_step<1, false>(lds, tt, a, t, index);
+    }
+    t += R;
+    __syncthreads();
+  }
+
+  // ---- store ----
+  if (!a.final_pass) {
+    F29* out = static_cast<F29*>(out_v) + batch_off;
+    for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
+      const uint32_t mid = e >> log_m, m = e & (M - 1);
+      out[index(mid, m)] = lds29_load(lds, e);
+    }
+  } else {
+    Bn254Fr* out = static_cast<Bn254Fr*>(out_v) + batch_off;
+    for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
+      const uint32_t q = e >> log_m, m = e & (M - 1);
+      const uint32_t mid = bitrev(q, k);
+      Bn254Fr v;
+      fr29::to_canonical_words(lds29_load(lds, (mid << log_m) + m), v.v);
+      const uint32_t o = (q << (L - k)) + r0 + m;
+      if (a.mode & kStoreCoset) v = (v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits])).canonical();
+      else if (a.mode & kStoreScale) v = (v * a.scale).canonical();
+      out[o] = v;
+    }
+  }
+}
+
+// Montgomery twiddles (canonical w 2^256 mod p) -> the 29-bit tables: entries
+// [0, split) R'-form (w 2^261 mod p = 32 W mod p), entries [split, count)
+// Shoup {w, floor(w 2^261 / p)} with floor(w 2^261 / p) = 32 floor(w 2^256 /
+// p) + floor(32 W / p) (W = w 2^256 mod p, the Montgomery entry).
+__global__ __launch_bounds__(kBlock) void tw29_table_kernel(fr29::TwMont29* __restrict__ mont29,
+                                                            fr29::TwShoup29* __restrict__ shoup29,
+                                                            const Bn254Fr* __restrict__ in, uint32_t split,
+                                                            uint32_t count) {
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= count) return;
+  const Bn254Fr W = in[j].canonical();
+  if (j < split) {
+    Bn254Fr x = W;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) x = (x + x).canonical();
+    mont29[j].w = fr29::from_words(x.v);
+  } else {
+    const Bn254Fr w = W.from_mont();
+    const Bn254Fr q32 = Bn254Fr::shoup_quotient(w);
+    // t = floor(32 W / p): five doublings of W (< p, so 2r < 2p < 2^256),
+    // each followed by a subtraction of p when 2r >= p (one quotient bit)
+    uint32_t t = 0;
+    uint32_t r[8];
+    for (int i = 0; i < 8; ++i) r[i] = W.v[i];
+    for (int bit = 0; bit < 5; ++bit) {
+      uint32_t c = 0;
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t nc = r[i] >> 31;
+        r[i] = (r[i] << 1) | c;
+        c = nc;
+      }
+      uint32_t d[8], borrow = 0;
+      for (int i = 0; i < 8; ++i) {
+        const uint64_t s = (uint64_t)r[i] - fr29::kPWords[i] - borrow;
+        d[i] = (uint32_t)s;
+        borrow = (uint32_t)(s >> 63);
+      }
+      t = 2 * t + (borrow ? 0u : 1u);
+      if (!borrow)
+        for (int i = 0; i < 8; ++i) r[i] = d[i];
+    }
+    fr29::TwShoup29 e;
+    e.w = fr29::from_words(w.v);
+    e.wq = f29::shl5_repack(q32.v);
+    e.wq.l[0] |= t;  // the low 5 bits of 32 q32 are zero
+    shoup29[j - split] = e;
+  }
+}
+
 // T0[j] = w^j for j < n/2 from two small power tables: lo[j & mask] * hi[j >> bits]
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void twiddle_base_kernel(Fr* __restrict__ t0, uint32_t count,
@@ -405,11 +613,14 @@ void NttDomain<Fr>::build_twiddles() {
   const size_t hi_cnt = std::max<size_t>(1, half >> lb);
   using Tw = typename NttTw<Fr>::type;
   constexpr bool kShoup = !std::is_same_v<Tw, Fr>;
-  // Montgomery tables (kept: the first pass multiplies by them, see run())
-  // and, for Shoup fields, the Shoup entries derived from them
-  Tw* tab[2] = {static_cast<Tw*>(tw_fwd_.ensure(n_ * sizeof(Tw))), static_cast<Tw*>(tw_inv_.ensure(n_ * sizeof(Tw)))};
-  Fr* monts[2] = {kShoup ? static_cast<Fr*>(twm_fwd_.ensure(n_ * sizeof(Fr))) : nullptr,
-                  kShoup ? static_cast<Fr*>(twm_inv_.ensure(n_ * sizeof(Fr))) : nullptr};
+  // Montgomery stage tables (stage s holds w^(j 2^s), j < n / 2^(s+1), at
+  // offset n - (n >> s)): the twiddles of the 32-bit passes for fields without
+  // Shoup entries, and the source of every other table (BN254 Fr: the 29-bit
+  // tables now, the 32-bit Shoup ones on first use of set_variant bit 0)
+  Fr* monts[2] = {kShoup ? static_cast<Fr*>(twm_fwd_.ensure(n_ * sizeof(Fr)))
+                         : static_cast<Fr*>(tw_fwd_.ensure(n_ * sizeof(Tw))),
+                  kShoup ? static_cast<Fr*>(twm_inv_.ensure(n_ * sizeof(Fr)))
+                         : static_cast<Fr*>(tw_inv_.ensure(n_ * sizeof(Tw)))};
   DeviceBuffer lo_d, hi_d;
   Fr* lo = static_cast<Fr*>(lo_d.ensure(lo_cnt * sizeof(Fr)));
   Fr* hi = static_cast<Fr*>(hi_d.ensure(hi_cnt * sizeof(Fr)));
@@ -422,24 +633,67 @@ void NttDomain<Fr>::build_twiddles() {
     TA_HIP(hipMemcpyAsync(lo, lo_h.data(), lo_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
     TA_HIP(hipMemcpyAsync(hi, hi_h.data(), hi_cnt * sizeof(Fr), hipMemcpyHostToDevice, stream_));
     Fr* mont = monts[dir];
-    Fr* base = kShoup ? mont : reinterpret_cast<Fr*>(tab[dir]);
-    hipLaunchKernelGGL(twiddle_base_kernel<Fr>, dim3(ceil_div(half, kBlock)), dim3(kBlock), 0, stream_, base, half,
+    hipLaunchKernelGGL(twiddle_base_kernel<Fr>, dim3(ceil_div(half, kBlock)), dim3(kBlock), 0, stream_, mont, half,
                        lo, hi, lb);
-    if constexpr (kShoup)
-      hipLaunchKernelGGL(shoup_table_kernel<Fr>, dim3(ceil_div(half, kBlock)), dim3(kBlock), 0, stream_, tab[dir],
-                         mont, half);
     for (uint32_t s = 1; s < log_n_; ++s) {
       uint32_t cnt = (uint32_t)(n_ >> (s + 1));
-      Tw* ts = tab[dir] + (n_ - (n_ >> s));
-      hipLaunchKernelGGL(twiddle_stage_kernel<Tw>, dim3(ceil_div(cnt, kBlock)), dim3(kBlock), 0, stream_, ts,
-                         tab[dir], cnt, s);
-      if (kShoup)
-        hipLaunchKernelGGL(twiddle_stage_kernel<Fr>, dim3(ceil_div(cnt, kBlock)), dim3(kBlock), 0, stream_,
-                           mont + (n_ - (n_ >> s)), mont, cnt, s);
+      hipLaunchKernelGGL(twiddle_stage_kernel<Fr>, dim3(ceil_div(cnt, kBlock)), dim3(kBlock), 0, stream_,
+                         mont + (n_ - (n_ >> s)), mont, cnt, s);
     }
     TA_HIP(hipGetLastError());
     TA_HIP(hipStreamSynchronize(stream_));  // host vectors go out of scope
   }
+  if constexpr (kShoup) build_tables29();
+}
+
+// BN254 Fr: the 29-bit tables from the Montgomery stage tables (tw29_table_kernel)
+template <class Fr>
+void NttDomain<Fr>::build_tables29() {
+  if constexpr (std::is_same_v<Fr, Bn254Fr>) {
+    const uint32_t k0 = plan_.empty() ? log_n_ : plan_[0].k;
+    const size_t count = n_ - 1;  // all stage tables
+    split29_ = n_ - (n_ >> k0);
+    const size_t nshoup = count - split29_;
+    DeviceBuffer* bm[2] = {&t29m_fwd_, &t29m_inv_};
+    DeviceBuffer* bs[2] = {&t29s_fwd_, &t29s_inv_};
+    const Fr* mont[2] = {twm_fwd_.as<Fr>(), twm_inv_.as<Fr>()};
+    for (int dir = 0; dir < 2; ++dir) {
+      auto* m29 = static_cast<fr29::TwMont29*>(bm[dir]->ensure(std::max<size_t>(1, split29_) * sizeof(fr29::TwMont29)));
+      auto* s29 = static_cast<fr29::TwShoup29*>(bs[dir]->ensure(std::max<size_t>(1, nshoup) * sizeof(fr29::TwShoup29)));
+      hipLaunchKernelGGL(tw29_table_kernel, dim3(ceil_div(count, kBlock)), dim3(kBlock), 0, stream_, m29, s29,
+                         mont[dir], (uint32_t)split29_, (uint32_t)count);
+    }
+    TA_HIP(hipGetLastError());
+    TA_HIP(hipStreamSynchronize(stream_));
+  }
+}
+
+// The 32-bit Shoup tables {plain w, floor(w 2^256 / p)} of dif_pass_kernel's
+// later passes (BN254 Fr under set_variant bit 0)
+template <class Fr>
+void NttDomain<Fr>::ensure_tables32() {
+  using Tw = typename NttTw<Fr>::type;
+  if constexpr (!std::is_same_v<Tw, Fr>) {
+    if (tables32_ || log_n_ == 0) return;
+    const uint32_t count = (uint32_t)(n_ - 1);
+    Tw* tab[2] = {static_cast<Tw*>(tw_fwd_.ensure(n_ * sizeof(Tw))), static_cast<Tw*>(tw_inv_.ensure(n_ * sizeof(Tw)))};
+    const Fr* mont[2] = {twm_fwd_.as<Fr>(), twm_inv_.as<Fr>()};
+    for (int dir = 0; dir < 2; ++dir)
+      hipLaunchKernelGGL(shoup_table_kernel<Fr>, dim3(ceil_div(count, kBlock)), dim3(kBlock), 0, stream_, tab[dir],
+                         mont[dir], count);
+    TA_HIP(hipGetLastError());
+    TA_HIP(hipStreamSynchronize(stream_));
+    tables32_ = true;
+  }
+}
+
+template <class Fr>
+bool NttDomain<Fr>::set_variant(int v) {
+  if (v < 0 || v > 1) return false;
+  if (v == 1 && !std::is_same_v<Fr, Bn254Fr>) return false;
+  variant_ = v;
+  if (v & 1) ensure_tables32();
+  return true;
 }
 
 template <class Fr>
@@ -477,6 +731,9 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
     return;
   }
   if (batch > 65535) throw std::runtime_error("tachyon_mi355x: NTT batch exceeds the grid limit");
+  if constexpr (std::is_same_v<Fr, Bn254Fr>) {
+    if (!(variant_ & 1)) return run29(d_data, inverse, batch);
+  }
   using Tw = typename NttTw<Fr>::type;
   constexpr bool kShoup = !std::is_same_v<Tw, Fr>;
   const Tw* tw = inverse ? tw_inv_.as<Tw>() : tw_fwd_.as<Tw>();
@@ -551,6 +808,64 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
     timings_.passes.assign(plan_.size(), 0.f);
     for (size_t p = 0; p < plan_.size(); ++p) TA_HIP(hipEventElapsedTime(&timings_.passes[p], ev_[p], ev_[p + 1]));
     TA_HIP(hipEventElapsedTime(&timings_.total, ev_[0], ev_[plan_.size()]));
+  }
+}
+
+
+// BN254 Fr: the passes over 9 x 29-bit limbs (dif29_pass_kernel); the same
+// pass plan, modes and scratch discipline as run()
+template <class Fr>
+void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch) {
+  if constexpr (std::is_same_v<Fr, Bn254Fr>) {
+    const auto* tm = (inverse ? t29m_inv_ : t29m_fwd_).template as<fr29::TwMont29>();
+    const auto* ts = (inverse ? t29s_inv_ : t29s_fwd_).template as<fr29::TwShoup29>();
+    F29* scratch = plan_.size() > 1 ? static_cast<F29*>(scratch29_.ensure(batch * n_ * sizeof(F29))) : nullptr;
+    if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
+    for (size_t p = 0; p < plan_.size(); ++p) {
+      const Pass& ps = plan_[p];
+      PassArgs<Fr> a{};
+      a.L = log_n_;
+      a.s0 = ps.s0;
+      a.k = ps.k;
+      a.log_m = ps.log_m;
+      a.final_pass = ps.final_pass ? 1u : 0u;
+      a.pow_bits = pow_bits_;
+      a.mode = 0;
+      if (p == 0 && !inverse && has_offset_) {
+        a.mode |= kLoadCoset;
+        a.load_lo = coset_lo_.as<Fr>();
+        a.load_hi = coset_hi_.as<Fr>();
+      }
+      if (ps.final_pass && inverse) {
+        if (has_offset_) {
+          a.mode |= kStoreCoset;
+          a.store_lo = icoset_lo_.as<Fr>();
+          a.store_hi = icoset_hi_.as<Fr>();
+        } else {
+          a.mode |= kStoreScale;
+          a.scale = size_inv_;
+        }
+      }
+      // first pass: data (32 B) -> scratch (36 B); middle: scratch in place; last: scratch -> data
+      const void* src = (p == 0) ? static_cast<const void*>(d_data) : scratch;
+      void* dst = ps.final_pass ? static_cast<void*>(d_data) : scratch;
+      const uint32_t elems = (1u << ps.log_m) << ps.k;
+      const uint32_t blocks = (uint32_t)(n_ / elems);
+      if (p == 0)
+        hipLaunchKernelGGL((dif29_pass_kernel<true, fr29::TwMont29>), dim3(blocks, (uint32_t)batch), dim3(kBlock), 0,
+                           stream_, src, dst, Tw29Table<fr29::TwMont29>{tm, 0u}, a);
+      else
+        hipLaunchKernelGGL((dif29_pass_kernel<false, fr29::TwShoup29>), dim3(blocks, (uint32_t)batch), dim3(kBlock), 0,
+                           stream_, src, dst, Tw29Table<fr29::TwShoup29>{ts, (uint32_t)split29_}, a);
+      TA_HIP(hipGetLastError());
+      if (profile_) TA_HIP(hipEventRecord(ev_[p + 1], stream_));
+    }
+    if (profile_) {
+      TA_HIP(hipEventSynchronize(ev_[plan_.size()]));
+      timings_.passes.assign(plan_.size(), 0.f);
+      for (size_t p = 0; p < plan_.size(); ++p) TA_HIP(hipEventElapsedTime(&timings_.passes[p], ev_[p], ev_[p + 1]));
+      TA_HIP(hipEventElapsedTime(&timings_.total, ev_[0], ev_[plan_.size()]));
+    }
   }
 }
 

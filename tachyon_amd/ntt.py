@@ -144,6 +144,12 @@ class Radix2EvaluationDomain:
     def set_profile(self, on: bool):
         lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(self._d, 1 if on else 0)
 
+    def set_variant(self, variant: int):
+        """A/B kernel variant: 0 = the 9 x 29-bit-limb passes (default), 1 = the
+        8 x 32-bit-limb passes; both give the same canonical outputs."""
+        if not lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(self._d, variant):
+            raise ValueError(f"unknown NTT variant {variant}")
+
     def last_timings(self):
         total = ctypes.c_float()
         passes = (ctypes.c_float * 16)()

@@ -172,3 +172,45 @@ def test_transform_host_in_place():
     d.transform_host(arr)
     assert arr.tobytes() == O.fft(coeffs, n, five)
     d.close()
+
+
+@pytest.mark.parametrize("logn", [1, 2, 3, 7, 9, 11, 15, 17, 19, 21])
+def test_field29_and_field32_passes_vs_oracle(logn):
+    """The default 9 x 29-bit-limb passes (dif29_pass_kernel) and the 8 x
+    32-bit ones (set_variant(1)) on plain and coset domains, FFT and IFFT, at
+    sizes whose pass plans have odd stage counts (single radix-2 steps inside a
+    pass and as the transform's last step): both bytewise equal to the oracle."""
+    n = 1 << logn
+    five = O.field_op("bn254_fr", "to_mont", (5).to_bytes(32, "little"))
+    coeffs = O.gen_scalars("bn254_fr", 3000 + logn, n).tobytes()
+    want = O.fft(coeffs, n)
+    want_c = O.fft(coeffs, n, five)
+    for variant in (0, 1):
+        d = domain(n)
+        d.set_variant(variant)
+        ev = d.fft(coeffs)
+        assert ev == want, variant
+        assert d.ifft(ev) == O.ifft(ev, n), variant
+        d.set_offset(five)
+        evc = d.fft(coeffs)
+        assert evc == want_c, variant
+        assert d.ifft(evc) == O.ifft(evc, n, five), variant
+        d.close()
+    with pytest.raises(ValueError):
+        domain(n).set_variant(2)
+
+
+def test_field29_extreme_inputs():
+    """Inputs at the top of the field (every element p - 1, and p - 1 - i)
+    through both pass kernels."""
+    n = 1 << 12
+    p = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+    patterns = [(p - 1).to_bytes(32, "little") * n, b"".join(((p - 1 - i) % p).to_bytes(32, "little") for i in range(n))]
+    for v in patterns:
+        want = O.fft(v, n)
+        for variant in (0, 1):
+            d = domain(n)
+            d.set_variant(variant)
+            assert d.fft(v) == want, variant
+            assert d.ifft(want) == O.ifft(want, n), variant
+            d.close()
