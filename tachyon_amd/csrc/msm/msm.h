@@ -28,13 +28,13 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0xFFFBF;  // bits 0-19 except 6
+constexpr int kMsmVariantMask = 0x1FFFBF;  // bits 0-20 except 6
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
 // G2 accumulation
 constexpr unsigned kSchedFusedRecode = 1, kSchedRecodeFedSort = 2, kSchedNarrowStaging = 4, kSchedAcc29 = 8,
-                   kSchedLanePair = 16;
+                   kSchedLanePair = 16, kSchedAcc28 = 32;
 
 struct MsmPlan {
   unsigned c = 0;        // window bits
@@ -171,9 +171,9 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-19; see run_windows).  Every variant
+  // A/B tuning knobs (bits 0-5, 7-20; see run_windows).  Every variant
   // computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 19 are refused.
+  // experiment) and anything above bit 20 are refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;
@@ -222,6 +222,7 @@ class MsmGpu {
   bool acc29_ = false;         // BN254 G1 accumulation over 29-bit limbs (default; bit 18: FIPS 32-bit)
   int acc29_mode_ = 0;         // ... next base: 0 not prefetched, 1 in registers (bit 13), 2 via LDS-DMA (bit 17)
   bool pair_acc_ = false;      // G2 accumulation with a lane pair per point (bit 15)
+  bool acc28_ = false;         // BLS12-381 G1 accumulation over 28-bit limbs (default; bit 20: FIPS 32-bit)
   bool pair_inline_ = false;   // ... its 12-limb products inline (bit 16)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass

@@ -8,6 +8,7 @@
 #include "msm.h"
 #include "../field/f29.h"
 #include "acc29.h"
+#include "acc28.h"
 #include "acc_pair.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -507,19 +508,61 @@ __device__ __forceinline__ Pt small_mul(const Pt& P, uint32_t m) {
 }
 }  // namespace acc29
 
+// The field policies of seg_acc_limb_body: BN254 G1 over the 9 x 29-bit field
+// (Raw 144-byte stores, the rare doubling through the R-form FIPS field) and
+// BLS12-381 G1 over the 14 x 28-bit field (R-form stores for the FIPS
+// reductions, the doubling in 28-bit limbs).
+struct Pol29 {
+  using Fq = Bn254Fq;
+  using F = f29::F29;
+  using Acc = acc29::Acc;
+  using Raw = acc29::Raw;
+  static __device__ __forceinline__ F shift_repack(const uint32_t* w) { return f29::shl5_repack(w); }
+  static __device__ __forceinline__ Acc from_shifted(const F& x, const F& y) { return acc29::from_shifted(x, y); }
+  static __device__ __forceinline__ Acc madd(const Acc& a, const F& x, const F& y, int* sp) {
+    return acc29::madd(a, x, y, sp);
+  }
+  static __device__ __forceinline__ Acc dbl_slow(const Acc& a) { return acc29::dbl_slow(a); }
+  static __device__ __forceinline__ Raw raw_of(const Acc& a, bool zero) { return acc29::raw_of(a, zero); }
+  static __device__ __forceinline__ XYZZ<Fq> to_xyzz(const Acc& a) { return acc29::to_xyzz(a); }
+};
+struct Pol28 {
+  using Fq = Bls381Fq;
+  using F = f28::F28;
+  using Acc = acc28_core::Acc;
+  using Raw = Acc;  // (no raw stores: the BLS12-381 reductions are the FIPS kernels)
+  static __device__ __forceinline__ F shift_repack(const uint32_t* w) { return f28::shl8_repack(w); }
+  static __device__ __forceinline__ Acc from_shifted(const F& x, const F& y) { return acc28_core::from_shifted(x, y); }
+  static __device__ __forceinline__ Acc madd(const Acc& a, const F& x, const F& y, int* sp) {
+    return acc28_core::madd(a, x, y, sp);
+  }
+  static __device__ __forceinline__ Acc dbl_slow(const Acc& a) { return acc28_core::dbl(a); }
+  static __device__ __forceinline__ Raw raw_of(const Acc& a, bool) { return a; }
+  static __device__ __forceinline__ XYZZ<Fq> to_xyzz(const Acc& a) {
+    XYZZ<Fq> r;
+    f28::to32(a.x, r.x.v);
+    f28::to32(a.y, r.y.v);
+    f28::to32(a.zz, r.zz.v);
+    f28::to32(a.zzz, r.zzz.v);
+    return r;
+  }
+};
+
 // kPrefetch: 0 = gather each base at its own iteration; 1 = the next base in
 // registers (16 VGPRs: 186, two waves per SIMD); 2 = the next base through
 // LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR destination, so the
 // kernel keeps its 3-wave register budget with the gather one iteration ahead)
 typedef __attribute__((address_space(3))) void lds_void_t;
-template <int kPrefetch, bool kRaw>
-__global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
-                                                           const uint64_t* __restrict__ ents, uint32_t c,
-                                                           uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
-                                                           uint32_t idx_mask, XYZZ<Bn254Fq>* __restrict__ bucket_sum,
-                                                           XYZZ<Bn254Fq>* __restrict__ pieces,
-                                                           uint32_t* __restrict__ tflags, uint32_t* __restrict__ tlast) {
-  using namespace acc29;
+template <class Pol, int kPrefetch, bool kRaw>
+__device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>* __restrict__ bases,
+                                                  const uint64_t* __restrict__ ents, uint32_t c, uint64_t gbeg,
+                                                  uint64_t gend, uint64_t tbase, uint32_t K, uint32_t idx_mask,
+                                                  XYZZ<typename Pol::Fq>* __restrict__ bucket_sum,
+                                                  XYZZ<typename Pol::Fq>* __restrict__ pieces,
+                                                  uint32_t* __restrict__ tflags, uint32_t* __restrict__ tlast) {
+  using Fq = typename Pol::Fq;
+  using F = typename Pol::F;
+  using Acc = typename Pol::Acc;
   const uint64_t tl = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
   const uint64_t g0 = gbeg + tl * K;
   if (g0 >= gend) return;
@@ -537,14 +580,14 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
   bool acc_zero = true;
   // kRaw: the accumulator as it is (Raw); otherwise R form, the identity as
   // zz = zzz = 0 (x, y are not read)
-  auto put = [&](XYZZ<Bn254Fq>* dst, size_t i) {
+  auto put = [&](XYZZ<Fq>* dst, size_t i) {
     if constexpr (kRaw) {
-      reinterpret_cast<Raw*>(dst)[i] = raw_of(acc, acc_zero);
+      reinterpret_cast<typename Pol::Raw*>(dst)[i] = Pol::raw_of(acc, acc_zero);
     } else {
-      XYZZ<Bn254Fq> s = to_xyzz(acc);
+      XYZZ<Fq> s = Pol::to_xyzz(acc);
       const uint32_t keep = acc_zero ? 0u : ~0u;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < Fq::N; ++k) {
         s.zz.v[k] &= keep;
         s.zzz.v[k] &= keep;
       }
@@ -553,7 +596,7 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
   };
   uint64_t e0 = ents[g0];
   uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
-  Affine<Bn254Fq> P;
+  Affine<Fq> P;
   // LDS-DMA staging: [slot][wave][16-byte chunk][lane], 32 KiB per workgroup; a
   // wave-instruction writes its 64 lanes' chunks contiguously (base + 16 lane)
   __shared__ uint4 stage[kPrefetch == 2 ? 2 : 1][kPrefetch == 2 ? kBlock / 64 : 1][4][64];
@@ -569,7 +612,7 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
   uint32_t it = 0;  // iteration count: the same for every lane of the wave (K entries each)
   for (uint64_t g = g0; g < g1; ++g, ++it) {
     const uint64_t e2 = (g + 2 < g1) ? ents[g + 2] : 0;
-    Affine<Bn254Fq> Pn;
+    Affine<Fq> Pn;
     if constexpr (kPrefetch == 1) {
       Pn = bases[entry_val(e1) & idx_mask];
     } else if constexpr (kPrefetch == 2) {
@@ -597,15 +640,15 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
       }
       if (!P.is_zero_canonical()) {
         P.y = P.y.cond_neg_canonical(v0 & kSignBit);
-        const F29 x2 = shl5_repack(P.x.v), y2 = shl5_repack(P.y.v);  // both paths
+        const F x2 = Pol::shift_repack(P.x.v), y2 = Pol::shift_repack(P.y.v);  // both paths
         if (acc_zero) {
-          acc = from_shifted(x2, y2);
+          acc = Pol::from_shifted(x2, y2);
           acc_zero = false;
         } else {
           int special = 0;
-          acc = madd(acc, x2, y2, &special);  // (unchanged when special)
+          acc = Pol::madd(acc, x2, y2, &special);  // (unchanged when special)
           if (special == 1) acc_zero = true;
-          else if (special == 2) acc = dbl_slow(acc);
+          else if (special == 2) acc = Pol::dbl_slow(acc);
         }
       }
     }
@@ -628,6 +671,32 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
   if (!(flags & kTail) || through) put(pieces, 2 * t + 1);
   tflags[t] = flags;
   tlast[t] = cur;
+}
+
+
+template <int kPrefetch, bool kRaw>
+__global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
+                                                           const uint64_t* __restrict__ ents, uint32_t c,
+                                                           uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
+                                                           uint32_t idx_mask, XYZZ<Bn254Fq>* __restrict__ bucket_sum,
+                                                           XYZZ<Bn254Fq>* __restrict__ pieces,
+                                                           uint32_t* __restrict__ tflags, uint32_t* __restrict__ tlast) {
+  seg_acc_limb_body<Pol29, kPrefetch, kRaw>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces, tflags,
+                                            tlast);
+}
+// BLS12-381 G1 over the 14 x 28-bit field: R-form stores (the FIPS chain join
+// and window reductions read them); 2 waves per SIMD (the 14-limb madd holds
+// ~4 x 14 accumulator + 2 x 14 base words)
+__global__ __launch_bounds__(kBlock, 2) void seg_acc28_kernel(const Affine<Bls381Fq>* __restrict__ bases,
+                                                              const uint64_t* __restrict__ ents, uint32_t c,
+                                                              uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
+                                                              uint32_t idx_mask,
+                                                              XYZZ<Bls381Fq>* __restrict__ bucket_sum,
+                                                              XYZZ<Bls381Fq>* __restrict__ pieces,
+                                                              uint32_t* __restrict__ tflags,
+                                                              uint32_t* __restrict__ tlast) {
+  seg_acc_limb_body<Pol28, 0, false>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces, tflags,
+                                     tlast);
 }
 
 // ---------------------------------------------------------------------------
@@ -1664,6 +1733,17 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
         hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                            tflags, tlast);
+    } else if constexpr (std::is_same_v<Curve, Bls381G1>) {
+      if (acc28_) {
+        last_schedule_ |= kSchedAcc28;
+        hipLaunchKernelGGL(seg_acc28_kernel, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+                           (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
+                           tflags, tlast);
+      } else {
+        hipLaunchKernelGGL(seg_acc_kernel<Curve>, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+                           (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
+                           tflags, tlast);
+      }
     } else if constexpr (std::is_same_v<Curve, Bn254G2> || std::is_same_v<Curve, Bls381G2>) {
       // a lane pair per virtual thread (set_variant bit 15, A/B; bit 16: inline 12-limb products)
       constexpr bool kCallDefault = Curve::F::Base::N == 12;
@@ -1901,6 +1981,9 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   const bool acc29_default = std::is_same_v<Curve, Bn254G1>;
   acc29_ = !(variant_ & 262144) && ((variant_ & (8192 | 16384 | 131072)) != 0 || acc29_default);
   acc29_mode_ = (variant_ & 131072) ? 2 : (variant_ & 8192) ? 1 : 0;
+  // BLS12-381 G1: the accumulation over 14 x 28-bit limbs (field/f28.h) by
+  // default; bit 20 restores the 12 x 32-bit FIPS field (A/B)
+  acc28_ = std::is_same_v<Curve, Bls381G1> && !(variant_ & (1 << 20));
   // G2: a lane pair per point with inline products by default (BLS12-381 G2
   // 2^24 accumulation 129 -> 113 ms, BN254 G2 2^22 16.3 -> 15.7 ms); bit 15
   // restores the one-lane kernel, bit 16 the pair with out-of-line 12-limb products

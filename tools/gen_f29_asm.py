@@ -26,9 +26,12 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tachyon_amd", "csrc", "field", "f29_asm.h")
 N = 9
+# the field's limb shape and names (tools/gen_f28.py reuses these generators
+# for BLS12-381 Fq in 14 x 28-bit limbs)
+SPEC29 = {"N": N, "W": 29, "T": "F29", "mask": "kM29", "pinv": "kPinv29", "p": "kP29"}
 
 
-def stmt(pairs, indent="  ", operand=None):
+def stmt(pairs, indent="  ", operand=None, spec=SPEC29):
     """One column: v_mad_u64_u32 acc += x * y for each (x, y) operand name
     (operand: name -> constraint text; default the Fq field's operands)."""
     if not pairs:
@@ -46,7 +49,7 @@ def stmt(pairs, indent="  ", operand=None):
         src = {"a": f"a.l[{idx}]", "b": f"b.l[{idx}]", "c": f"c.l[{idx}]", "d": f"d.l[{idx}]",
                "m": f"m[{idx}]", "t": f"dd[{idx}]"}
         if kind == "p":
-            return f'[{v}] "s"(kP29[{idx}])'
+            return f'[{v}] "s"({spec["p"]}[{idx}])'
         return f'[{v}] "v"({src[kind]})'
     operand = operand or default_operand
     ins = ", ".join(operand(v) for v in names)
@@ -56,7 +59,7 @@ def stmt(pairs, indent="  ", operand=None):
     return [f'{indent}asm("{text}" : [acc] "+&v"(acc), [sc] "=&s"(sc) : {ins});']
 
 
-def column_pairs(k, mode):
+def column_pairs(k, mode, N=N):
     """Products of column k (without the digit's m_k p_0)."""
     pairs = []
     if mode in ("mul", "mul2"):
@@ -83,29 +86,30 @@ def column_pairs(k, mode):
     return pairs
 
 
-def gen(name, mode, add):
-    args = {"mul": "const F29& a, const F29& b", "mul2": "const F29& a, const F29& b, const F29& c, const F29& d",
-            "sqr": "const F29& a"}[mode]
+def gen(name, mode, add, spec=SPEC29):
+    T, N, W = spec["T"], spec["N"], spec["W"]
+    args = {"mul": f"const {T}& a, const {T}& b", "mul2": f"const {T}& a, const {T}& b, const {T}& c, const {T}& d",
+            "sqr": f"const {T}& a"}[mode]
     if add:
-        args += ", const F29& e"
-    L = [f"__device__ __forceinline__ F29 {name}({args}) {{",
+        args += f", const {T}& e"
+    L = [f"__device__ __forceinline__ {T} {name}({args}) {{",
          "  uint64_t acc = 0, sc;",
          f"  uint32_t m[{N}];",
-         "  F29 r;"]
+         f"  {T} r;"]
     if mode == "sqr":
         L.append(f"  uint32_t dd[{N}];")
         L.append(f"  for (int i = 0; i < {N}; ++i) dd[i] = a.l[i] << 1;")
     for k in range(2 * N - 1):
         L.append(f"  // column {k}")
-        L += stmt(column_pairs(k, mode))
+        L += stmt(column_pairs(k, mode, N), spec=spec)
         if k < N:
-            L.append(f"  m[{k}] = ((uint32_t)acc * kPinv29) & kM29;")
-            L += stmt([(f"m{k}", "p0")])
+            L.append(f"  m[{k}] = ((uint32_t)acc * {spec['pinv']}) & {spec['mask']};")
+            L += stmt([(f"m{k}", "p0")], spec=spec)
         else:
             if add:
                 L.append(f"  acc += e.l[{k - N}];")
-            L.append(f"  r.l[{k - N}] = (uint32_t)acc & kM29;")
-        L.append("  acc >>= 29;")
+            L.append(f"  r.l[{k - N}] = (uint32_t)acc & {spec['mask']};")
+        L.append(f"  acc >>= {W};")
     if add:
         L.append(f"  acc += e.l[{N - 1}];")
     L.append(f"  r.l[{N - 1}] = (uint32_t)acc;")
