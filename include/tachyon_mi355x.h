@@ -443,6 +443,17 @@ TACHYON_C_EXPORT void tachyon_mi355x_groth16_prover_info(const tachyon_mi355x_gr
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                    size_t count, const void* r, const void* s, void* out_a,
                                                    void* out_b, void* out_c);
+/* One-process multi-device proofs (no reference counterpart; the reference's
+ * prover_main.cc:116-128 runs one process on one GPU): every later
+ * tachyon_mi355x_groth16_prove runs the multi-rank split on these devices --
+ * one host thread per entry runs the witness map and its 1/count chunk of
+ * every MSM (_prove_partials with rank = entry, world = count), and the
+ * partials are added on the host (_assemble); the proof equals the
+ * single-device one.  Ids may repeat (provers sharing a GPU on separate
+ * streams); count <= 1 returns to the single-device prover.  Returns 0 and
+ * changes nothing when an id is out of range. */
+TACHYON_C_EXPORT int tachyon_mi355x_groth16_set_devices(tachyon_mi355x_groth16_prover* prover, const int* device_ids,
+                                                        size_t count);
 TACHYON_C_EXPORT size_t tachyon_mi355x_groth16_partials_size(const tachyon_mi355x_groth16_prover* prover);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_partials(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                             size_t count, int with_b1, uint32_t rank,

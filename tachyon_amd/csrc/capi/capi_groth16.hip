@@ -9,6 +9,7 @@
 #include <cstring>
 #include <exception>
 #include <memory>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -79,12 +80,81 @@ void witness_map_into(P* p, const void* full, size_t count, void* out_h) {
   TA_HIP(hipStreamSynchronize(p->stream()));
 }
 
+// One-process multi-device proof: the multi-rank split of prove() (every
+// device runs the witness map and its contiguous 1/N chunk of every MSM,
+// Groth16Prover::partials) with one host thread per device instead of one
+// process per GPU, and the partials added on the host by assemble() -- so a
+// single-process caller (the reference's circom prover_main.cc:116-128 and
+// prove.h:64-147 run in one process) uses several MI355X.  Ids may repeat
+// (logical devices: provers sharing one GPU on separate streams).
+template <class P>
+void multi_prove_into(P* primary, std::vector<std::unique_ptr<P>>& provs, const std::vector<int>& devices,
+                      const void* full, size_t count, const void* r, const void* s, void* a, void* b, void* c) {
+  using Fr = typename P::Fr;
+  const size_t N = provs.size();
+  std::vector<PartialsOf<P*>> parts(N);
+  std::vector<std::exception_ptr> err(N);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < N; ++k) {
+    th.emplace_back([&, k] {
+      try {
+        TA_HIP(hipSetDevice(devices[k]));
+        parts[k] = provs[k]->partials(static_cast<const Fr*>(full), count, r != nullptr, (uint32_t)k, (uint32_t)N);
+      } catch (...) {
+        err[k] = std::current_exception();
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+  auto proof = primary->assemble(parts.data(), N, static_cast<const Fr*>(r), static_cast<const Fr*>(s));
+  memcpy(a, &proof.a, sizeof(proof.a));
+  memcpy(b, &proof.b, sizeof(proof.b));
+  memcpy(c, &proof.c, sizeof(proof.c));
+}
+
+template <class P>
+void make_device_provers(const P* primary, const std::vector<int>& devices, std::vector<std::unique_ptr<P>>& out) {
+  int prev = 0;
+  TA_HIP(hipGetDevice(&prev));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{prev};
+  out.clear();
+  for (int d : devices) {
+    TA_HIP(hipSetDevice(d));
+    out.push_back(std::make_unique<P>(primary->key()));  // the key's points and matrices on device d
+  }
+}
+
+template <class P>
+void free_device_provers(const std::vector<int>& devices, std::vector<std::unique_ptr<P>>& provs) {
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) prev = 0;
+  for (size_t k = 0; k < provs.size(); ++k) {
+    (void)hipSetDevice(devices[k]);
+    provs[k].reset();
+  }
+  provs.clear();
+  (void)hipSetDevice(prev);
+}
+
 }  // namespace
 
 struct tachyon_mi355x_groth16_prover {
   circom::CurveId curve;
   std::unique_ptr<BnProver> bn;
   std::unique_ptr<BlsProver> bls;
+  // tachyon_mi355x_groth16_set_devices: one prover per device entry (empty = bn / bls alone)
+  std::vector<int> devices;
+  std::vector<std::unique_ptr<BnProver>> bn_dev;
+  std::vector<std::unique_ptr<BlsProver>> bls_dev;
+  ~tachyon_mi355x_groth16_prover() {
+    free_device_provers(devices, bn_dev);
+    free_device_provers(devices, bls_dev);
+  }
 };
 
 #define PROVER_DISPATCH(p, ...)                         \
@@ -132,7 +202,35 @@ void tachyon_mi355x_groth16_prover_info(const tachyon_mi355x_groth16_prover* pro
 
 void tachyon_mi355x_groth16_prove(tachyon_mi355x_groth16_prover* prover, const void* full, size_t count,
                                   const void* r, const void* s, void* out_a, void* out_b, void* out_c) {
-  GUARD_BEGIN PROVER_DISPATCH(prover, prove_into(impl, full, count, r, s, out_a, out_b, out_c)); GUARD_END
+  GUARD_BEGIN
+  if (!prover->devices.empty()) {
+    if (prover->curve == circom::CurveId::kBn254)
+      multi_prove_into(prover->bn.get(), prover->bn_dev, prover->devices, full, count, r, s, out_a, out_b, out_c);
+    else
+      multi_prove_into(prover->bls.get(), prover->bls_dev, prover->devices, full, count, r, s, out_a, out_b, out_c);
+    return;
+  }
+  PROVER_DISPATCH(prover, prove_into(impl, full, count, r, s, out_a, out_b, out_c));
+  GUARD_END
+}
+
+int tachyon_mi355x_groth16_set_devices(tachyon_mi355x_groth16_prover* prover, const int* device_ids, size_t count) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  for (size_t i = 0; i < count; ++i)
+    if (device_ids[i] < 0 || device_ids[i] >= n) return 0;  // refused, nothing changed
+  GUARD_BEGIN
+  free_device_provers(prover->devices, prover->bn_dev);
+  free_device_provers(prover->devices, prover->bls_dev);
+  prover->devices.clear();
+  if (count > 1) {
+    prover->devices.assign(device_ids, device_ids + count);
+    if (prover->curve == circom::CurveId::kBn254) make_device_provers(prover->bn.get(), prover->devices, prover->bn_dev);
+    else make_device_provers(prover->bls.get(), prover->devices, prover->bls_dev);
+  }
+  return 1;
+  GUARD_END
+  return 0;
 }
 
 size_t tachyon_mi355x_groth16_partials_size(const tachyon_mi355x_groth16_prover* prover) {

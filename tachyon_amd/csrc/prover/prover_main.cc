@@ -2,7 +2,7 @@
 // backend, written against the public C-ABI only (include/tachyon_mi355x.h).
 //
 //   circom_prover --zkey circuit.zkey --wtns witness.wtns --proof proof.json \
-//                 --public public.json [--curve bn254|bls12_381] [--no_zk] [-n N]
+//                 --public public.json [--curve bn254|bls12_381] [--no_zk] [-n N] [--devices 0,1,..]
 //
 // Same flags, outputs and JSON layout as the reference (prover_main.cc:188-283;
 // proof JSON: circomlib/json/groth16_proof.h + points.h -- decimal canonical
@@ -144,7 +144,7 @@ std::string g2_json(const uint8_t* p, const CurveInfo& c) {
 
 int usage() {
   std::cerr << "usage: circom_prover --zkey F --wtns F --proof F --public F [--curve bn254|bls12_381] [--no_zk]\n"
-               "                     [-n|--num_runs N] [--no_use_mmap]\n";
+               "                     [-n|--num_runs N] [--no_use_mmap] [--devices 0,1,...]\n";
   return 1;
 }
 
@@ -154,6 +154,7 @@ int main(int argc, char** argv) {
   std::string zkey_path, wtns_path, proof_path, public_path, curve_name = "bn254";
   bool no_zk = false;
   size_t num_runs = 1;
+  std::vector<int> devices;  // --devices 0,1,...: one-process multi-device proofs
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -170,6 +171,16 @@ int main(int argc, char** argv) {
     else if (a == "-n" || a == "--num_runs") num_runs = std::stoul(next());
     else if (a == "--verify") { std::cerr << "--verify is not supported by this backend\n"; return 1; }
     else if (a == "--trace_path") next();
+    else if (a == "--devices") {
+      std::string list = next();
+      size_t pos = 0;
+      while (pos <= list.size()) {
+        size_t comma = list.find(',', pos);
+        if (comma == std::string::npos) comma = list.size();
+        devices.push_back(std::stoi(list.substr(pos, comma - pos)));
+        pos = comma + 1;
+      }
+    }
     else return usage();
   }
   if (zkey_path.empty() || wtns_path.empty() || proof_path.empty() || public_path.empty() || num_runs == 0)
@@ -192,6 +203,10 @@ int main(int argc, char** argv) {
   zkey.shrink_to_fit();
   uint32_t info[4];
   tachyon_mi355x_groth16_prover_info(prover, info);
+  if (devices.size() > 1 && !tachyon_mi355x_groth16_set_devices(prover, devices.data(), devices.size())) {
+    std::cerr << "--devices: a device id is out of range" << std::endl;
+    return 1;
+  }
   auto now = Clock::now();
   std::cout << "Time taken for parsing zkey (and uploading the proving key): "
             << std::chrono::duration<double>(now - start).count() << " s" << std::endl;

@@ -128,6 +128,15 @@ class Groth16Prover:
         part = self.prove_partials(full, rank, world, with_b1)
         return self.assemble(all_gather_bytes(part, group, device), r, s)
 
+    def set_devices(self, device_ids):
+        """One-process multi-device proofs: every later prove() runs the
+        multi-rank split with one host thread per device entry (ids may
+        repeat; [] or one id = single device) -- tachyon_mi355x_groth16_set_devices."""
+        ids = list(device_ids)
+        arr = (ctypes.c_int * max(1, len(ids)))(*ids)
+        if not lib().tachyon_mi355x_groth16_set_devices(self._h, arr, len(ids)):
+            raise ValueError(f"device ids out of range: {ids}")
+
     def set_profile(self, on: bool):
         lib().tachyon_mi355x_groth16_set_profile(self._h, 1 if on else 0)
 

@@ -188,3 +188,50 @@ def test_sharded_partials_assemble(curve, log_n, world):
     assert list(prover.assemble(blob)) == expect_nozk == list(prover.prove(fb))
     assert list(prover.assemble(shuffled, r, s)) == expect_zk
     prover.close()
+
+
+@pytest.mark.parametrize("curve,log_n,devices", [("bn254", 8, [0, 0]), ("bn254", 10, [0, 0, 0]),
+                                                  ("bls12_381", 6, [0, 0])])
+def test_multi_device_prover(curve, log_n, devices):
+    """One-process multi-device proofs (tachyon_mi355x_groth16_set_devices: a
+    prover and a host thread per device entry, partials added on the host) on
+    logical devices sharing the box's GPU: NoZK and ZK proofs equal the
+    oracle's; [] returns to the single-device prover; bad ids are refused."""
+    from tachyon_amd.groth16 import Groth16Prover
+    zbytes, full = synth_zkey(curve, log_n=log_n, num_public=2, seed=70 + log_n)
+    zk = CF.parse_zkey(zbytes)
+    prover = Groth16Prover(zbytes)
+    fb = fr_bytes(curve, full)
+    Fr = pyref.Field("bn254_fr" if curve == "bn254" else "bls12_381_fr")
+    r_int, s_int = 0x1234 + log_n, Fr.p - 5
+    prover.set_devices(devices)
+    assert list(prover.prove(fb)) == list(OG.prove(zk, full))
+    assert list(prover.prove(fb, Fr.to_bytes(r_int), Fr.to_bytes(s_int))) == list(OG.prove(zk, full, r_int, s_int))
+    with pytest.raises(ValueError):
+        prover.set_devices([0, 4096])
+    prover.set_devices([])
+    assert list(prover.prove(fb)) == list(OG.prove(zk, full))
+    prover.close()
+
+
+def test_circom_prover_cli_devices(tmp_path):
+    """bin/circom_prover --devices 0,0 (two logical devices on the box's GPU):
+    the NoZK proof equals the golden one."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tachyon_amd", "bin",
+                       "circom_prover")
+    g = json.load(open(os.path.join(GOLDEN, "groth16_multiplier_3.json")))
+    G1, G2 = pyref.Curve("bn254_g1"), pyref.Curve("bn254_g2")
+    proof_p, pub_p = tmp_path / "proof.json", tmp_path / "public.json"
+    cmd = [exe, "--zkey", os.path.join(GOLDEN, "multiplier_3.zkey"), "--wtns",
+           os.path.join(GOLDEN, "multiplier_3.wtns"), "--proof", str(proof_p), "--public", str(pub_p),
+           "--no_zk", "--devices", "0,0"]
+    subprocess.run(cmd, check=True, timeout=120, capture_output=True)
+    proof = json.load(open(proof_p))
+    A = tuple(int(x) for x in proof["pi_a"][:2])
+    B = tuple(tuple(int(x) for x in c) for c in proof["pi_b"][:2])
+    C = tuple(int(x) for x in proof["pi_c"][:2])
+    want = g["cases"][0]["proof"]
+    assert G1.to_bytes(A).hex() == want[0] and G2.to_bytes(B).hex() == want[1] and G1.to_bytes(C).hex() == want[2]
+    bad = subprocess.run(cmd[:-1] + ["0,4096"], timeout=120, capture_output=True)
+    assert bad.returncode != 0
