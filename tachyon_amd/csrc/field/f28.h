@@ -145,6 +145,21 @@ TA_HD F28 ksub2(const uint32_t (&k)[kN], const F28& a, const F28& b) {
   return r;
 }
 
+// carry propagation: limbs 0..12 < 2^28, the value unchanged (for limb-wise
+// sums whose limbs would overflow a product's columns)
+TA_HD F28 normalize(const F28& a) {
+  F28 r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < kN - 1; ++i) {
+    const uint32_t t = a.l[i] + c;
+    r.l[i] = t & kM28;
+    c = t >> 28;
+  }
+  r.l[kN - 1] = a.l[kN - 1] + c;
+  return r;
+}
+
 // x'' = x~ << 8 as 28-bit limbs, from the 12 x 32-bit R-form words w (x~ <
 // 2^384 - 2^? : lazy < 2p < 2^382, so the shifted value has < 390 bits)
 TA_HD F28 shl8_repack(const uint32_t* w) {

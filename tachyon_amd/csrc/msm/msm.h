@@ -28,13 +28,13 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0x1FFFBF;  // bits 0-20 except 6
+constexpr int kMsmVariantMask = 0x3FFFBF;  // bits 0-21 except 6 (21: a debug check, not a schedule)
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
 // G2 accumulation
 constexpr unsigned kSchedFusedRecode = 1, kSchedRecodeFedSort = 2, kSchedNarrowStaging = 4, kSchedAcc29 = 8,
-                   kSchedLanePair = 16, kSchedAcc28 = 32;
+                   kSchedLanePair = 16, kSchedAcc28 = 32, kSchedChainsChecked = 64;
 
 struct MsmPlan {
   unsigned c = 0;        // window bits
@@ -171,9 +171,10 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-20; see run_windows).  Every variant
+  // A/B tuning knobs (bits 0-5, 7-20; see run_windows) and bit 21, a debug
+  // check (the small-MSM chain flags vs the accumulation's).  Every variant
   // computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 20 are refused.
+  // experiment) and anything above bit 21 are refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;
@@ -209,7 +210,7 @@ class MsmGpu {
   unsigned force_c_ = 0;
   int variant_ = 0;
   MsmTimings timings_;
-  DeviceBuffer bases_, scalars_, ents_, ents2_, sort_tmp_, scan_tmp_;
+  DeviceBuffer bases_, scalars_, ents_, ents2_, sort_tmp_, scan_tmp_, check_;
   DeviceBuffer start_, end_, cnt_, off_a_, off_b_, part_a_, part_b_, seg_a_, seg_b_, windows_, buckets_;
   hipEvent_t ev_[8] = {};  // 0-5 phase marks, 7 chain count read back (early chain tables)
   hipStream_t sort_stream_ = nullptr;  // group sorts run here, overlapping the accumulation on stream_
@@ -223,6 +224,7 @@ class MsmGpu {
   int acc29_mode_ = 0;         // ... next base: 0 not prefetched, 1 in registers (bit 13), 2 via LDS-DMA (bit 17)
   bool pair_acc_ = false;      // G2 accumulation with a lane pair per point (bit 15)
   bool acc28_ = false;         // BLS12-381 G1 accumulation over 28-bit limbs (default; bit 20: FIPS 32-bit)
+  bool pair28_ = false;        // BLS12-381 G2 lane pair over 28-bit limbs (default; bit 20: FIPS pair)
   bool pair_inline_ = false;   // ... its 12-limb products inline (bit 16)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass

@@ -10,6 +10,7 @@
 #include "acc29.h"
 #include "acc28.h"
 #include "acc_pair.h"
+#include "pair28.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -803,6 +804,113 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typen
   }
 }
 
+// BLS12-381 G2 with a lane pair per point over the 14 x 28-bit Fq
+// (msm/pair28.h): seg_acc_pair_kernel's run logic; the stores convert this
+// lane's components to the R form the lane-pair FIPS reductions read.
+// set_variant bit 20 restores the FIPS pair (as for BLS12-381 G1).
+__global__ __launch_bounds__(kBlock) void seg_acc_pair28_kernel(const Affine<Bls381Fq2>* __restrict__ bases,
+                                                                const uint64_t* __restrict__ ents, uint32_t c,
+                                                                uint64_t gbeg, uint64_t gend, uint64_t tbase,
+                                                                uint32_t K, uint32_t idx_mask,
+                                                                XYZZ<Bls381Fq2>* __restrict__ bucket_sum,
+                                                                XYZZ<Bls381Fq2>* __restrict__ pieces,
+                                                                uint32_t* __restrict__ tflags,
+                                                                uint32_t* __restrict__ tlast) {
+  using Fb = Bls381Fq;
+  using namespace pair28;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint64_t tl = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 1;
+  const uint64_t g0 = gbeg + tl * K;
+  if (g0 >= gend) return;  // both lanes of the pair
+  const uint64_t g1 = min(g0 + K, gend);
+  const uint64_t t = tbase + tl;
+  const uint32_t dmask = (1u << c) - 1;
+  auto bucket_of_key = [&](uint32_t key) -> uint32_t {
+    uint32_t d = key & dmask;
+    return d ? ((key >> c) << (c - 1)) + (d - 1) : kNoBucket;
+  };
+  const uint32_t prev_b = g0 > gbeg ? bucket_of_key(entry_key(ents[g0 - 1])) : kNoBucket;
+  const uint32_t next_b = (g1 < gend) ? bucket_of_key(entry_key(ents[g1])) : kNoBucket;
+  const Fb* comp = reinterpret_cast<const Fb*>(bases);
+  Fb* bsum = reinterpret_cast<Fb*>(bucket_sum);
+  Fb* pcs = reinterpret_cast<Fb*>(pieces);
+  const Fb one_h = h ? Fb::zero() : Fb::one();
+  Acc acc;
+  bool acc_zero = true;
+  auto store = [&](Fb* dst, uint64_t idx) {  // this lane's components of the run sum (identity if none)
+    Fb* o = dst + 8 * idx;
+    if (acc_zero) {
+      o[h] = one_h;
+      o[2 + h] = one_h;
+      o[4 + h] = Fb::zero();
+      o[6 + h] = Fb::zero();
+    } else {
+      Fb v;
+      to32(acc.x, v.v);
+      o[h] = v;
+      to32(acc.y, v.v);
+      o[2 + h] = v;
+      to32(acc.zz, v.v);
+      o[4 + h] = v;
+      to32(acc.zzz, v.v);
+      o[6 + h] = v;
+    }
+  };
+  uint32_t flags = 0, runs = 0, cur = kNoBucket;
+  uint64_t e0 = ents[g0];
+  for (uint64_t g = g0; g < g1; ++g) {
+    const uint64_t e1 = (g + 1 < g1) ? ents[g + 1] : 0;
+    const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
+    const uint32_t b = bucket_of_key(k0);
+    if (b != kNoBucket) {
+      const Fb* pt = comp + 4 * (size_t)(v0 & idx_mask);
+      const Fb px = pt[h];
+      Fb py = pt[2 + h];
+      if (b != cur) {
+        if (cur != kNoBucket) {
+          if (runs == 1 && cur == prev_b) { store(pcs, 2 * t); flags |= kHead; }
+          else store(bsum, cur);
+        }
+        cur = b;
+        ++runs;
+        acc_zero = true;
+      }
+      const uint32_t pz = (px.is_zero_canonical() && py.is_zero_canonical()) ? 1u : 0u;
+      if (!(pz & dpp<kSwap>(pz))) {  // not the identity base (both components zero)
+        py = py.cond_neg_canonical(v0 & kSignBit);
+        const F28 x2 = shl8_repack(px.v), y2 = shl8_repack(py.v);
+        if (acc_zero) {
+          acc = from_shifted(x2, y2, h != 0);
+          acc_zero = false;
+        } else {
+          int special = 0;
+          acc = madd(acc, x2, y2, h != 0, &special);  // (unchanged when special)
+          if (special == 1) acc_zero = true;
+          else if (special == 2) acc = pair28::dbl(acc, h != 0);
+        }
+      }
+    }
+    e0 = e1;
+  }
+  if (cur != kNoBucket) {
+    const bool head = runs == 1 && cur == prev_b;
+    const bool tail = cur == next_b;
+    if (head) { store(pcs, 2 * t); flags |= kHead; }
+    if (tail) flags |= kTail;
+    if (tail && !head) store(pcs, 2 * t + 1);
+    if (!head && !tail) store(bsum, cur);
+  }
+  if (runs <= 1) flags |= kSingle;
+  acc_zero = true;  // absent pieces are the identity
+  if (!(flags & kHead)) store(pcs, 2 * t);
+  const bool through = (flags & kHead) && (flags & kTail) && (flags & kSingle);
+  if (!(flags & kTail) || through) store(pcs, 2 * t + 1);
+  if (h == 0) {
+    tflags[t] = flags;
+    tlast[t] = cur;
+  }
+}
+
 // A bucket that crosses thread boundaries forms a chain t0 < ... < t1: the
 // tail of t0, the whole-range heads of the "through" threads in between and
 // the head of t1 -- i.e. pieces[2*t0+1 .. 2*t1] (absent tails are identity).
@@ -825,6 +933,19 @@ __device__ __forceinline__ bool chain_end(uint32_t f) {
 // offsets were ~90 us on the critical path of a 0.7 ms 2^16 MSM).  Keys are
 // sorted, so equal first and last buckets mean one run; the loop runs only
 // when an end of the range holds digit-0 entries (no bucket).
+// Debug check (set_variant bit 21): the run flags chain_flags_kernel derived
+// from the sorted keys before the accumulation equal the ones the accumulation
+// wrote (the small-MSM chain tables are built from the former).
+__global__ __launch_bounds__(kBlock) void chain_flags_check_kernel(const uint32_t* __restrict__ tflags,
+                                                                   const uint32_t* __restrict__ tlast,
+                                                                   const uint32_t* __restrict__ cflags,
+                                                                   const uint32_t* __restrict__ clast, uint32_t T,
+                                                                   uint32_t* __restrict__ mismatches) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= T) return;
+  if (tflags[t] != cflags[t] || tlast[t] != clast[t]) atomicAdd(mismatches, 1u);
+}
+
 __global__ __launch_bounds__(kBlock) void chain_flags_kernel(const uint64_t* __restrict__ ents, uint32_t c,
                                                              uint64_t gbeg, uint64_t gend, uint32_t K, uint32_t T,
                                                              uint32_t* __restrict__ tflags,
@@ -1750,7 +1871,15 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       auto* pair_kernel = pair_inline_ ? &seg_acc_pair_kernel<Curve, false> : &seg_acc_pair_kernel<Curve, kCallDefault>;
       // (kCallDefault is false for 8-limb fields: both entries are the inline kernel there)
       if (pair_acc_) last_schedule_ |= kSchedLanePair;
-      if (pair_acc_)
+      bool pair28 = false;
+      if constexpr (std::is_same_v<Curve, Bls381G2>) pair28 = pair_acc_ && pair28_;
+      if (pair28) {
+        last_schedule_ |= kSchedAcc28;
+        if constexpr (std::is_same_v<Curve, Bls381G2>)
+          hipLaunchKernelGGL(seg_acc_pair28_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
+                             ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_,
+                             bucket_sum, pieces, tflags, tlast);
+      } else if (pair_acc_)
         hipLaunchKernelGGL(pair_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
                            ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum,
                            pieces, tflags, tlast);
@@ -1795,6 +1924,18 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // ---- join buckets that cross thread boundaries ----
   // (the chain count and the longest chain decide the levels: read back
   // while the accumulation runs when early_chains)
+  if (early_chains && (variant_ & (1 << 21))) {  // debug: pre-derived flags == the accumulation's
+    uint32_t* mism = static_cast<uint32_t*>(check_.ensure(sizeof(uint32_t)));
+    TA_HIP(hipMemsetAsync(mism, 0, sizeof(uint32_t), stream_));
+    hipLaunchKernelGGL(chain_flags_check_kernel, dim3(grid_for(T)), dim3(kBlock), 0, stream_, tflags, tlast, cflags,
+                       clast, (uint32_t)T, mism);
+    TA_HIP(hipGetLastError());
+    uint32_t h = 0;
+    TA_HIP(hipMemcpyAsync(&h, mism, sizeof(h), hipMemcpyDeviceToHost, stream_));
+    TA_HIP(hipStreamSynchronize(stream_));
+    if (h) throw std::runtime_error("tachyon_mi355x: chain flags derived before the accumulation differ from its own");
+    last_schedule_ |= kSchedChainsChecked;
+  }
   if (early_chains) {
     TA_HIP(hipEventSynchronize(ev_[7]));
   } else {
@@ -1984,6 +2125,9 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   // BLS12-381 G1: the accumulation over 14 x 28-bit limbs (field/f28.h) by
   // default; bit 20 restores the 12 x 32-bit FIPS field (A/B)
   acc28_ = std::is_same_v<Curve, Bls381G1> && !(variant_ & (1 << 20));
+  // BLS12-381 G2: the lane pair over the same 28-bit field (msm/pair28.h);
+  // bit 20 restores the FIPS pair, bit 15 the one-lane FIPS kernel
+  pair28_ = std::is_same_v<Curve, Bls381G2> && !(variant_ & (1 << 20));
   // G2: a lane pair per point with inline products by default (BLS12-381 G2
   // 2^24 accumulation 129 -> 113 ms, BN254 G2 2^22 16.3 -> 15.7 ms); bit 15
   // restores the one-lane kernel, bit 16 the pair with out-of-line 12-limb products

@@ -66,7 +66,8 @@ class NttDomain {
   const NttTimings& timings() const { return timings_; }
   // A/B kernel variants; bit 0: BN254 Fr on the 8 x 32-bit-limb passes
   // (dif_pass_kernel) instead of the 9 x 29-bit ones (dif29_pass_kernel, the
-  // default).  Unknown bits (or bit 0 on other fields): refused, returns false.
+  // default); bit 1: the 29-bit passes with XOR-swizzled LDS positions.
+  // Unknown bits (or any bit on other fields): refused, returns false.
   bool set_variant(int v);
   int variant() const { return variant_; }
 

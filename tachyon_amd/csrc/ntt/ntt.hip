@@ -243,18 +243,32 @@ struct Tw29Table {
   uint32_t off;
 };
 
+// kSwz: positions XOR-swizzled so that the 32-lane groups of a ds_read_b32 /
+// ds_write_b32 (bank = word mod 32) hit 32 distinct banks in every register
+// step of the 8-stage, 4-set passes (2^24: qlog = 6, 4, 2, 0): bit 2 ^= bit 5,
+// bits 3, 4 ^= bit 6.  Without it the qlog = 2 / 0 steps are 2- / 4-way
+// conflicted on all 72 LDS accesses of a group.
+template <bool kSwz>
+__device__ __forceinline__ uint32_t swz29(uint32_t p) {
+  if constexpr (kSwz) return p ^ ((p >> 3) & 4u) ^ (((p >> 6) & 1u) * 0x18u);
+  else return p;
+}
+template <bool kSwz>
 __device__ __forceinline__ F29 lds29_load(const uint32_t* __restrict__ lds, uint32_t pos) {
   F29 v;
+  pos = swz29<kSwz>(pos);
 #pragma unroll
   for (int i = 0; i < 9; ++i) v.l[i] = lds[i * kMaxLdsElems + pos];
   return v;
 }
+template <bool kSwz>
 __device__ __forceinline__ void lds29_store(uint32_t* __restrict__ lds, uint32_t pos, const F29& v) {
+  pos = swz29<kSwz>(pos);
 #pragma unroll
   for (int i = 0; i < 9; ++i) lds[i * kMaxLdsElems + pos] = v.l[i];
 }
 
-template <int R, bool kLast, class TwT, class IndexFn>
+template <int R, bool kLast, bool kSwz, class TwT, class IndexFn>
 __device__ __forceinline__ void radix29_step(uint32_t* __restrict__ lds, Tw29Table<TwT> tt,
                                              const PassArgs<Bn254Fr>& a, uint32_t t, IndexFn index) {
   constexpr int E = 1 << R;
@@ -285,28 +299,28 @@ __device__ __forceinline__ void radix29_step(uint32_t* __restrict__ lds, Tw29Tab
       }
       F29 x[4];
 #pragma unroll
-      for (int j = 0; j < E; ++j) x[j] = lds29_load(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m);
+      for (int j = 0; j < E; ++j) x[j] = lds29_load<kSwz>(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m);
       if constexpr (kLast) fr29::radix4_last(x, tA1);
       else fr29::radix4(x, tA0, tA1, tB0, tB1);
 #pragma unroll
-      for (int j = 0; j < E; ++j) lds29_store(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m, x[j]);
+      for (int j = 0; j < E; ++j) lds29_store<kSwz>(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m, x[j]);
     } else {
       TwT tA;
       if constexpr (!kLast) tA = twA[index(a0, m) & gapA];
       F29 x[2];
 #pragma unroll
-      for (int j = 0; j < E; ++j) x[j] = lds29_load(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m);
+      for (int j = 0; j < E; ++j) x[j] = lds29_load<kSwz>(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m);
       if constexpr (kLast) fr29::radix2_last(x);
       else fr29::radix2(x, tA);
 #pragma unroll
-      for (int j = 0; j < E; ++j) lds29_store(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m, x[j]);
+      for (int j = 0; j < E; ++j) lds29_store<kSwz>(lds, ((a0 + ((uint32_t)j << qlog)) << log_m) + m, x[j]);
     }
   }
 }
 
 // kFirst: the input is the 32-byte Montgomery array (the transform's first
 // pass, R'-form twiddles); otherwise 36-byte F29 from the previous pass.
-template <bool kFirst, class TwT>
+template <bool kFirst, bool kSwz, class TwT>
 __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restrict__ in_v, void* __restrict__ out_v,
                                                             Tw29Table<TwT> tt, PassArgs<Bn254Fr> a) {
   __shared__ uint32_t lds[9 * kMaxLdsElems];
@@ -343,7 +357,7 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
     } else {
       v = static_cast<const F29*>(in_v)[batch_off + i];
     }
-    lds29_store(lds, e, v);
+    lds29_store<kSwz>(lds, e, v);
   }
   __syncthreads();
 
@@ -351,11 +365,11 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
     const uint32_t R = min(2u, k - t);
     const bool last = a.final_pass && t + R == k;
     if (R == 2) {
-      if (last) radix29_step<2, true>(lds, tt, a, t, index);
-      else radix29_step<2, false>(lds, tt, a, t, index);
+      if (last) radix29_step<2, true, kSwz>(lds, tt, a, t, index);
+      else radix29_step<2, false, kSwz>(lds, tt, a, t, index);
     } else {
-      if (last) radix29_step<1, true>(lds, tt, a, t, index);
-      else radix29_step<1, false>(lds, tt, a, t, index);
+      if (last) radix29_step<1, true, kSwz>(lds, tt, a, t, index);
+      else radix29_step<1, false, kSwz>(lds, tt, a, t, index);
     }
     t += R;
     __syncthreads();
@@ -366,7 +380,7 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
     F29* out = static_cast<F29*>(out_v) + batch_off;
     for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
       const uint32_t mid = e >> log_m, m = e & (M - 1);
-      out[index(mid, m)] = lds29_load(lds, e);
+      out[index(mid, m)] = lds29_load<kSwz>(lds, e);
     }
   } else {
     Bn254Fr* out = static_cast<Bn254Fr*>(out_v) + batch_off;
@@ -374,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
       const uint32_t q = e >> log_m, m = e & (M - 1);
       const uint32_t mid = bitrev(q, k);
       Bn254Fr v;
-      fr29::to_canonical_words(lds29_load(lds, (mid << log_m) + m), v.v);
+      fr29::to_canonical_words(lds29_load<kSwz>(lds, (mid << log_m) + m), v.v);
       const uint32_t o = (q << (L - k)) + r0 + m;
       if (a.mode & kStoreCoset) v = (v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits])).canonical();
       else if (a.mode & kStoreScale) v = (v * a.scale).canonical();
@@ -689,8 +703,8 @@ void NttDomain<Fr>::ensure_tables32() {
 
 template <class Fr>
 bool NttDomain<Fr>::set_variant(int v) {
-  if (v < 0 || v > 1) return false;
-  if (v == 1 && !std::is_same_v<Fr, Bn254Fr>) return false;
+  if (v < 0 || v > 3) return false;
+  if (v != 0 && !std::is_same_v<Fr, Bn254Fr>) return false;
   variant_ = v;
   if (v & 1) ensure_tables32();
   return true;
@@ -851,12 +865,17 @@ void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch) {
       void* dst = ps.final_pass ? static_cast<void*>(d_data) : scratch;
       const uint32_t elems = (1u << ps.log_m) << ps.k;
       const uint32_t blocks = (uint32_t)(n_ / elems);
-      if (p == 0)
-        hipLaunchKernelGGL((dif29_pass_kernel<true, fr29::TwMont29>), dim3(blocks, (uint32_t)batch), dim3(kBlock), 0,
-                           stream_, src, dst, Tw29Table<fr29::TwMont29>{tm, 0u}, a);
-      else
-        hipLaunchKernelGGL((dif29_pass_kernel<false, fr29::TwShoup29>), dim3(blocks, (uint32_t)batch), dim3(kBlock), 0,
-                           stream_, src, dst, Tw29Table<fr29::TwShoup29>{ts, (uint32_t)split29_}, a);
+      const bool swz = (variant_ & 2) != 0;
+      if (p == 0) {
+        auto* k0 = swz ? &dif29_pass_kernel<true, true, fr29::TwMont29> : &dif29_pass_kernel<true, false, fr29::TwMont29>;
+        hipLaunchKernelGGL(k0, dim3(blocks, (uint32_t)batch), dim3(kBlock), 0, stream_, src, dst,
+                           Tw29Table<fr29::TwMont29>{tm, 0u}, a);
+      } else {
+        auto* k1 = swz ? &dif29_pass_kernel<false, true, fr29::TwShoup29>
+                       : &dif29_pass_kernel<false, false, fr29::TwShoup29>;
+        hipLaunchKernelGGL(k1, dim3(blocks, (uint32_t)batch), dim3(kBlock), 0, stream_, src, dst,
+                           Tw29Table<fr29::TwShoup29>{ts, (uint32_t)split29_}, a);
+      }
       TA_HIP(hipGetLastError());
       if (profile_) TA_HIP(hipEventRecord(ev_[p + 1], stream_));
     }

@@ -143,7 +143,8 @@ class VariableBaseMSMGpu:
         onesweep passes, 7-byte LDS staging (tachyon_mi355x_msm_gpu_last_schedule)."""
         b = lib().tachyon_mi355x_msm_gpu_last_schedule(self.curve_id, self._ctx)
         return {"fused_recode": bool(b & 1), "recode_fed_sort": bool(b & 2), "narrow_staging": bool(b & 4),
-                "acc29": bool(b & 8), "lane_pair": bool(b & 16), "acc28": bool(b & 32)}
+                "acc29": bool(b & 8), "lane_pair": bool(b & 16), "acc28": bool(b & 32),
+                "chains_checked": bool(b & 64)}
 
     def last_divisions(self) -> int:
         """Point chunks the last run was split into (device memory or host-upload pipeline)."""

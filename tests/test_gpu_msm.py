@@ -62,7 +62,8 @@ def test_msm_golden_bn254_g1_variants(variant):
 
 
 @pytest.mark.parametrize("curve,variant", [("bn254_g2", 0), ("bn254_g2", 32768), ("bls12_381_g2", 0),
-                                           ("bls12_381_g2", 32768), ("bls12_381_g2", 65536)])
+                                           ("bls12_381_g2", 32768), ("bls12_381_g2", 65536 | (1 << 20)),
+                                           ("bls12_381_g2", 1 << 20)])
 def test_msm_golden_g2_lane_pair(curve, variant):
     """The G2 accumulations: a lane pair per point with inline products (the
     default), the one-lane kernel (set_variant bit 15) and, for BLS12-381, the
@@ -351,7 +352,7 @@ def test_window_ranges_tile_the_msm(curve):
     m.close()
 
 
-@pytest.mark.parametrize("curve,logn", [("bn254_g1", 16), ("bn254_g1", 18), ("bls12_381_g2", 16)])
+@pytest.mark.parametrize("curve,logn", [("bn254_g1", 16), ("bn254_g1", 18), ("bls12_381_g1", 16), ("bls12_381_g2", 16)])
 def test_msm_schedule_variants_agree(curve, logn):
     """Every accepted set_variant schedule computes the same point: the separate
     recode + full sort (bit 7), rocPRIM's own digit-histogram pass instead of the
@@ -433,5 +434,32 @@ def test_msm_reduction_edge_cases(curve, variant):
         assert expect == bytes(pb)  # the identity, (0, 0)
         assert m.run(alt, one) == expect
         assert m.run(same, one) == O.msm(curve, same, one)[0]
+    finally:
+        m.set_variant(0)
+
+
+@pytest.mark.parametrize("curve", ["bn254_g1", "bls12_381_g1", "bn254_g2"])
+@pytest.mark.parametrize("logn", [14, 16, 17, 19])
+def test_chain_flags_pre_derived_match(curve, logn):
+    """below 2^21 accumulation threads the chain tables are built
+    from chain_flags_kernel's re-derivation of the run flags, not from the
+    flags the accumulation writes.  set_variant bit 21 compares the two on the
+    device after every accumulation (the run aborts on a mismatch): random,
+    NonUniform (one scalar) and digit-0-heavy (small) scalars, all equal to the
+    oracle."""
+    n = 1 << logn
+    pb, sf = O.CURVE_INFO[curve]
+    bases = O.gen_bases(curve, 51, n, 64).tobytes()
+    sets = {"random": O.gen_scalars(sf, 51, n).tobytes(),
+            "non_uniform": O.gen_scalars(sf, 52, 1).tobytes() * n,
+            "small": b"".join(O.field_op(sf, "to_mont", (i % 5).to_bytes(32, "little")) for i in range(64)) * (n // 64)}
+    m = ctx(curve)
+    m.set_variant(1 << 21)
+    try:
+        for name, sc in sets.items():
+            if logn > 16 and name == "small":
+                continue  # (the 64-scalar pattern is the same test at every size)
+            assert m.run(bases, sc) == O.msm(curve, bases, sc)[0], name
+            assert m.last_schedule()["chains_checked"], name
     finally:
         m.set_variant(0)
