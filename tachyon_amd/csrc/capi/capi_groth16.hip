@@ -118,6 +118,7 @@ template <class P>
 void make_device_provers(const P* primary, const std::vector<int>& devices, std::vector<std::unique_ptr<P>>& out) {
   int prev = 0;
   TA_HIP(hipGetDevice(&prev));
+  const int src_device = prev;  // the primary prover's device (created on the current one)
   struct Restore {
     int d;
     ~Restore() { (void)hipSetDevice(d); }
@@ -125,7 +126,7 @@ void make_device_provers(const P* primary, const std::vector<int>& devices, std:
   out.clear();
   for (int d : devices) {
     TA_HIP(hipSetDevice(d));
-    out.push_back(std::make_unique<P>(primary->key()));  // the key's points and matrices on device d
+    out.push_back(std::make_unique<P>(*primary, src_device));  // the key's points and matrices, peer copies
   }
 }
 

@@ -70,8 +70,11 @@ class Groth16Prover {
   using Key = circom::ZKey<G1, G2>;
 
   explicit Groth16Prover(const Key& key, hipStream_t stream = nullptr);
+  // a copy of src (whose buffers live on src_device) on the current device,
+  // the proving key copied peer to peer (one-process multi-device proofs)
+  Groth16Prover(const Groth16Prover& src, int src_device, hipStream_t stream = nullptr);
   ~Groth16Prover();
-  Groth16Prover(const Groth16Prover&) = delete;
+  Groth16Prover(const Groth16Prover&) = delete;  // (the device copy above takes a source device)
   Groth16Prover& operator=(const Groth16Prover&) = delete;
 
   // full: num_vars Montgomery-form assignments (full[0] = 1), host or device.
@@ -97,6 +100,7 @@ class Groth16Prover {
   hipStream_t stream() const { return stream_; }
 
  private:
+  void init_device_state();
   Key key_;  // host copy: verifying-key points and the query heads used on the host
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;

@@ -215,8 +215,9 @@ inline float ms_since(Clock::time_point t0) {
 
 }  // namespace
 
+// the stream, the two domains and the two MSM contexts, on the current device
 template <class G1, class G2>
-Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(key), stream_(stream) {
+void Groth16Prover<G1, G2>::init_device_state() {
   require_gpu();
   if (!stream_) {
     TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -231,6 +232,33 @@ Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(
   coset_->set_offset(ntt::root_of_unity<Fr>(log_n + 1));
   msm1_ = std::make_unique<msm::MsmGpu<G1>>(stream_);
   msm2_ = std::make_unique<msm::MsmGpu<G2>>(nullptr);  // own stream: runs beside the G1 MSMs
+}
+
+// A copy of `src` (on device src_device) on the current device: the device-
+// resident proving key (query points, the merged C1 | H1 array, the CSR
+// matrices) is copied peer to peer (xGMI between MI355X), the trimmed host key
+// shared; the one-process multi-device prover builds one per device.
+template <class G1, class G2>
+Groth16Prover<G1, G2>::Groth16Prover(const Groth16Prover& src, int src_device, hipStream_t stream)
+    : key_(src.key_), stream_(stream) {
+  init_device_state();
+  int dev = 0;
+  TA_HIP(hipGetDevice(&dev));
+  const std::pair<DeviceBuffer*, const DeviceBuffer*> bufs[] = {
+      {&a1_, &src.a1_}, {&b1_, &src.b1_}, {&lh1_, &src.lh1_}, {&b2_, &src.b2_},
+      {&row_a_, &src.row_a_}, {&row_b_, &src.row_b_}, {&col_, &src.col_}, {&val_, &src.val_}};
+  for (const auto& [dst, from] : bufs) {
+    void* d = dst->ensure(from->capacity());
+    TA_HIP(hipMemcpyPeer(d, dev, from->template as<void>(), src_device, from->capacity()));
+  }
+  lh_.ensure(src.lh_.capacity());
+  abc_.ensure(src.abc_.capacity());
+  full_.ensure(src.full_.capacity());
+}
+
+template <class G1, class G2>
+Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(key), stream_(stream) {
+  init_device_state();
 
   upload(a1_, key_.a1);
   upload(b1_, key_.b1);

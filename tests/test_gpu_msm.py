@@ -371,7 +371,7 @@ def test_msm_schedule_variants_agree(curve, logn):
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
         for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384,
-                  32768, 65536, 131072, 262144, 524288):
+                  32768, 65536, 131072, 262144, 524288, 1 << 20, (1 << 20) | 65536, 1 << 21):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
@@ -380,9 +380,13 @@ def test_msm_schedule_variants_agree(curve, logn):
             s = m.last_schedule()
             if curve == "bn254_g1":  # the 29-bit field by default; bit 18 the FIPS 32-bit field
                 assert s["acc29"] == (v != 262144), (hex(v), s)
+            elif curve == "bls12_381_g1":  # the 28-bit field by default; bit 20 the FIPS 32-bit field
+                assert s["acc28"] == (not v & (1 << 20)), (hex(v), s)
             else:  # G2: the lane pair by default; bit 15 the one-lane kernel
                 assert s["lane_pair"] == (v != 32768), (hex(v), s)
-        for bad in (64, 1 << 20):
+                if curve == "bls12_381_g2":  # the pair over 28-bit limbs; bit 20 the FIPS pair
+                    assert s["acc28"] == (v != 32768 and not v & (1 << 20)), (hex(v), s)
+        for bad in (64, 1 << 22):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
