@@ -249,9 +249,9 @@ TACHYON_C_EXPORT void* tachyon_mi355x_bn254_univariate_evaluation_domain_stream(
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(
     tachyon_bn254_univariate_evaluation_domain* domain, int on);
 /* A/B kernel variant of the domain's transforms (no reference counterpart):
- * 0 = the default 9 x 29-bit-limb passes, 1 = the 8 x 32-bit-limb passes.
- * Both compute the same canonical outputs.  Returns 0 (nothing changed) for
- * unknown values. */
+ * 0 = the default 8 x 32-bit-limb passes, 1 = the 9 x 29-bit-limb passes,
+ * 3 = the 29-bit passes with XOR-swizzled LDS positions.  All compute the same
+ * canonical outputs.  Returns 0 (nothing changed) for other values. */
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(
     tachyon_bn254_univariate_evaluation_domain* domain, int variant);
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(

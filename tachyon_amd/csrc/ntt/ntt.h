@@ -64,10 +64,11 @@ class NttDomain {
 
   void set_profile(bool on) { profile_ = on; }
   const NttTimings& timings() const { return timings_; }
-  // A/B kernel variants; bit 0: BN254 Fr on the 8 x 32-bit-limb passes
-  // (dif_pass_kernel) instead of the 9 x 29-bit ones (dif29_pass_kernel, the
-  // default); bit 1: the 29-bit passes with XOR-swizzled LDS positions.
-  // Unknown bits (or any bit on other fields): refused, returns false.
+  // A/B kernel variants (BN254 Fr): bit 0 = the 9 x 29-bit-limb passes
+  // (dif29_pass_kernel) instead of the default 8 x 32-bit ones (dif_pass_kernel;
+  // DESIGN.md NTT round 4: fewer instructions, the same time -- more
+  // multiplies per butterfly lower the clock); bit 1 (with bit 0) swizzles
+  // their LDS positions.  Unknown values (or any bit on other fields): refused.
   bool set_variant(int v);
   int variant() const { return variant_; }
 
@@ -102,7 +103,8 @@ class NttDomain {
   // BN254 Fr: the 29-bit-limb passes and their tables -- R'-form entries for
   // the first pass's stages [0, k0), Shoup entries for the later stages
   int variant_ = 0;
-  bool tables32_ = false;  // the 32-bit Shoup tables (built on first use of variant bit 0)
+  bool tables32_ = false;  // the 32-bit Shoup tables (built with the domain)
+  bool tables29_ = false;  // the 29-bit tables (built on first use of variant bit 0)
   size_t split29_ = 0;     // = n - (n >> k0): stage-table entries before the Shoup part
   DeviceBuffer t29m_fwd_, t29m_inv_, t29s_fwd_, t29s_inv_, scratch29_;
   DeviceBuffer coset_lo_, coset_hi_, icoset_lo_, icoset_hi_;

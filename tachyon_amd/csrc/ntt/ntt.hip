@@ -657,13 +657,15 @@ void NttDomain<Fr>::build_twiddles() {
     TA_HIP(hipGetLastError());
     TA_HIP(hipStreamSynchronize(stream_));  // host vectors go out of scope
   }
-  if constexpr (kShoup) build_tables29();
+  if constexpr (kShoup) ensure_tables32();  // (the 29-bit tables are built on first use of variant bit 0)
 }
 
 // BN254 Fr: the 29-bit tables from the Montgomery stage tables (tw29_table_kernel)
 template <class Fr>
 void NttDomain<Fr>::build_tables29() {
   if constexpr (std::is_same_v<Fr, Bn254Fr>) {
+    if (tables29_ || log_n_ == 0) return;
+    tables29_ = true;
     const uint32_t k0 = plan_.empty() ? log_n_ : plan_[0].k;
     const size_t count = n_ - 1;  // all stage tables
     split29_ = n_ - (n_ >> k0);
@@ -703,10 +705,10 @@ void NttDomain<Fr>::ensure_tables32() {
 
 template <class Fr>
 bool NttDomain<Fr>::set_variant(int v) {
-  if (v < 0 || v > 3) return false;
+  if (v < 0 || v > 3 || v == 2) return false;  // bit 1 (the LDS swizzle) modifies bit 0
   if (v != 0 && !std::is_same_v<Fr, Bn254Fr>) return false;
   variant_ = v;
-  if (v & 1) ensure_tables32();
+  if (v & 1) build_tables29();
   return true;
 }
 
@@ -746,7 +748,7 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
   }
   if (batch > 65535) throw std::runtime_error("tachyon_mi355x: NTT batch exceeds the grid limit");
   if constexpr (std::is_same_v<Fr, Bn254Fr>) {
-    if (!(variant_ & 1)) return run29(d_data, inverse, batch);
+    if (variant_ & 1) return run29(d_data, inverse, batch);
   }
   using Tw = typename NttTw<Fr>::type;
   constexpr bool kShoup = !std::is_same_v<Tw, Fr>;

@@ -20,7 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--log-n", type=int, default=24)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="0,1,3")
     ap.add_argument("--rounds", type=int, default=2)
     args = ap.parse_args()
     import torch
