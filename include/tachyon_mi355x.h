@@ -254,6 +254,21 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_prof
  * canonical outputs.  Returns 0 (nothing changed) for other values. */
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(
     tachyon_bn254_univariate_evaluation_domain* domain, int variant);
+/* One process, several GPUs: later transforms of the plain domain (offset 1;
+ * a coset keeps the single device) through the fft/ifft entry points above,
+ * transform_host and transform_device run the four-step NTT over `count`
+ * devices (ids may repeat: logical devices sharing a GPU) -- part g on ids[g],
+ * the all-to-all as peer copies over xGMI, input and output in natural order
+ * on the device the domain was created on (transform_device: a buffer there).
+ * count must be a power of two with 2^floor(log n / 2) >= count; count <= 1
+ * restores the single device.  Returns 1, or 0 (nothing changed) for a bad
+ * count or id, or when the generator set active now differs from the
+ * domain's (the plans would use another root).  Same results as one device. */
+TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices(
+    tachyon_bn254_univariate_evaluation_domain* domain, const int* ids, size_t count);
+/* the device list of set_devices (0 = single device); writes up to cap ids */
+TACHYON_C_EXPORT size_t tachyon_mi355x_bn254_univariate_evaluation_domain_devices(
+    const tachyon_bn254_univariate_evaluation_domain* domain, int* ids, size_t cap);
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(
     const tachyon_bn254_univariate_evaluation_domain* domain, float* total_ms, float* pass_ms, int max_passes);
 
@@ -335,7 +350,7 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ct
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule).
  * Every accepted variant computes the same MSM; returns 0 (nothing changed)
- * for bits outside 0xFBF. */
+ * for bits outside 0x3FFFBF (bits 0-21 but 6). */
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
  * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total,

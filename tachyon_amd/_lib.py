@@ -99,6 +99,8 @@ SIGNATURES = [
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_stream", vp, [vp]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile", None, [vp, i32]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant", i32, [vp, i32]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices", i32, [vp, vp, sz]),
+    ("tachyon_mi355x_bn254_univariate_evaluation_domain_devices", sz, [vp, vp, sz]),
     ("tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings", i32, [vp, fp, fp, i32]),
     ("tachyon_mi355x_bn254_ntt4_create", vp, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp]),
     ("tachyon_mi355x_bn254_ntt4_destroy", None, [vp]),

@@ -222,6 +222,13 @@ struct Vec {
 };
 struct Domain {
   std::unique_ptr<ntt::NttDomain<Bn254Fr>> impl;
+  int device = 0;  // the device the domain was created on (the multi-device primary)
+  // set_devices: the four-step over several devices for the plain domain
+  // (declared after impl: destroyed first, while impl's stream still exists)
+  std::unique_ptr<ntt::NttMultiDevice<Bn254Fr>> multi;
+  ntt::NttMultiDevice<Bn254Fr>* multi_for_plain() const {
+    return multi && impl->offset().is_one() ? multi.get() : nullptr;
+  }
 };
 // UnivariateEvaluations<RationalField<bn254::Fr>>: {numerator, denominator}
 // pairs; Zero() = 0 / 1 (math/base/rational_field.h:33,199-200)
@@ -509,6 +516,7 @@ tachyon_bn254_univariate_evaluation_domain* tachyon_bn254_univariate_evaluation_
   GUARD_BEGIN
   auto* d = new tachyon_bn254_univariate_evaluation_domain();
   d->impl.reset(new ntt::NttDomain<Bn254Fr>(num_coeffs));
+  TA_HIP(hipGetDevice(&d->device));
   return d;
   GUARD_END
 }
@@ -629,7 +637,10 @@ std::vector<FrC> do_fft(const Domain* d, std::vector<FrC>&& v) {
   if (v.empty()) return std::move(v);
   const size_t len = v.size(), n = d->impl->size();
   if (len < n) v.resize(n);  // zero padding
-  d->impl->forward_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
+  if (auto* m = d->multi_for_plain())
+    m->forward_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
+  else
+    d->impl->forward_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
   return std::move(v);
 }
 // IFFT + RemoveHighDegreeZeros (radix2_evaluation_domain.h:218-223)
@@ -637,7 +648,10 @@ std::vector<FrC> do_ifft(const Domain* d, std::vector<FrC>&& v) {
   if (v.empty()) return std::move(v);
   const size_t len = v.size(), n = d->impl->size();
   if (len < n) v.resize(n);
-  d->impl->inverse_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
+  if (auto* m = d->multi_for_plain())
+    m->inverse_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
+  else
+    d->impl->inverse_host(reinterpret_cast<const Bn254Fr*>(v.data()), len, reinterpret_cast<Bn254Fr*>(v.data()));
   size_t keep = v.size();
   while (keep > 0) {
     const FrC& x = v[keep - 1];
@@ -769,8 +783,15 @@ void tachyon_mi355x_bn254_univariate_evaluation_domain_set_offset(tachyon_bn254_
 void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_device(tachyon_bn254_univariate_evaluation_domain* d,
                                                                         tachyon_bn254_fr* d_data, int inverse) {
   GUARD_BEGIN
-  if (inverse) d->impl->inverse_device(reinterpret_cast<Bn254Fr*>(d_data));
-  else d->impl->forward_device(reinterpret_cast<Bn254Fr*>(d_data));
+  auto* x = reinterpret_cast<Bn254Fr*>(d_data);
+  if (auto* m = d->multi_for_plain()) {
+    if (inverse) m->inverse_device(x, x);
+    else m->forward_device(x, x);
+  } else if (inverse) {
+    d->impl->inverse_device(x);
+  } else {
+    d->impl->forward_device(x);
+  }
   GUARD_END
 }
 void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_host(tachyon_bn254_univariate_evaluation_domain* d,
@@ -781,8 +802,14 @@ void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_host(tachyon_bn
     throw std::runtime_error("transform_host: the vector must hold exactly size() elements (" + std::to_string(len) +
                              " != " + std::to_string(d->impl->size()) + ")");
   auto* v = reinterpret_cast<Bn254Fr*>(inout);
-  if (inverse) d->impl->inverse_host(v, len, v);
-  else d->impl->forward_host(v, len, v);
+  if (auto* m = d->multi_for_plain()) {
+    if (inverse) m->inverse_host(v, len, v);
+    else m->forward_host(v, len, v);
+  } else if (inverse) {
+    d->impl->inverse_host(v, len, v);
+  } else {
+    d->impl->forward_host(v, len, v);
+  }
   GUARD_END
 }
 void tachyon_mi355x_bn254_univariate_evaluation_domain_transform_batch_device(
@@ -803,6 +830,35 @@ int tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(tachyon_bn254_
                                                                   int variant) {
   GUARD_BEGIN return d->impl->set_variant(variant) ? 1 : 0; GUARD_END
   return 0;
+}
+int tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices(tachyon_bn254_univariate_evaluation_domain* d,
+                                                                   const int* ids, size_t count) {
+  GUARD_BEGIN
+  if (count <= 1) {
+    d->multi.reset();
+    return 1;
+  }
+  const size_t n = d->impl->size();
+  if (n < 4) return 0;
+  const std::vector<int> dev(ids, ids + count);
+  std::unique_ptr<ntt::NttMultiDevice<Bn254Fr>> m;
+  try {
+    m = std::make_unique<ntt::NttMultiDevice<Bn254Fr>>(d->impl->log_size(), dev, d->device, d->impl->stream());
+  } catch (const std::exception&) {  // not a power of two, too many for the size, or a bad id
+    return 0;
+  }
+  if (!(m->root() == d->impl->group_gen())) return 0;  // another generator set was active at create
+  d->multi = std::move(m);
+  return 1;
+  GUARD_END
+  return 0;
+}
+size_t tachyon_mi355x_bn254_univariate_evaluation_domain_devices(const tachyon_bn254_univariate_evaluation_domain* d,
+                                                                 int* ids, size_t cap) {
+  if (!d->multi) return 0;
+  const auto& v = d->multi->device_ids();
+  for (size_t i = 0; i < v.size() && i < cap; ++i) ids[i] = v[i];
+  return v.size();
 }
 int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(const tachyon_bn254_univariate_evaluation_domain* d,
                                                                    float* total_ms, float* pass_ms, int max_passes) {

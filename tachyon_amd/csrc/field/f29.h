@@ -49,6 +49,19 @@ constexpr uint32_t kK8[9] = {0x83e7ea38u, 0x882305b2u, 0x83951a74u, 0x96a91683u,
 // 16p, low limbs raised by 2^29
 constexpr uint32_t kK16[9] = {0x27cfd470u, 0x30460b6bu, 0x272a34efu, 0x2d522d0du, 0x385d9780u,
                               0x2db40c09u, 0x2a6e1410u, 0x25c2633fu, 0x030644e6u};
+// 33p, low limbs raised by 2^29 (minus a normalized value < 32p)
+constexpr uint32_t kK33[9] = {0x281ca627u, 0x2190778eu, 0x2ac70d2fu, 0x3d797cecu, 0x26410879u,
+                              0x3e4358d5u, 0x35830962u, 0x39e0ecb3u, 0x063cee1bu};
+// 16p, low limbs raised by 2^31 (minus PPP + 2Q, limbs < 3 2^29)
+constexpr uint32_t kK16r4[9] = {0x87cfd470u, 0x90460b68u, 0x872a34ecu, 0x8d522d0au, 0x985d977du,
+                                0x8db40c06u, 0x8a6e140du, 0x85c2633cu, 0x030644e3u};
+// 32p, low limbs raised by 2^29
+constexpr uint32_t kK32[9] = {0x2f9fa8e0u, 0x208c16d7u, 0x2e5469e0u, 0x3aa45a1bu, 0x30bb2f01u,
+                              0x3b681814u, 0x34dc2821u, 0x2b84c67fu, 0x060c89cdu};
+// 32p, low limbs raised by 3 2^29 (the lane-pair G2 products negate T = Q + 16p - X3,
+// limbs < 3 2^29 - 2, msm/pair29.h)
+constexpr uint32_t kK32r3[9] = {0x6f9fa8e0u, 0x608c16d5u, 0x6e5469deu, 0x7aa45a19u, 0x70bb2effu,
+                                0x7b681812u, 0x74dc281fu, 0x6b84c67du, 0x060c89cbu};
 // 1 in R' form (2^261 mod p)
 constexpr uint32_t kOne29[9] = {0x157ccc21u, 0x141c2758u, 0x185230d3u, 0x014c0419u, 0x0aa36fb9u,
                                 0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};
@@ -180,6 +193,20 @@ TA_HD F29 ksub2(const uint32_t (&k)[9], const F29& a, const F29& b) {
   return r;
 }
 
+// carries propagated: limbs 0..7 < 2^29 (a limb-wise sum of small multiples)
+TA_HD F29 normalize(const F29& a) {
+  F29 r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t t = a.l[i] + c;
+    r.l[i] = t & kM29;
+    c = t >> 29;
+  }
+  r.l[8] = a.l[8] + c;
+  return r;
+}
+
 // x' = x~ << 5 as 29-bit limbs, from the 8 x 32-bit R-form words w (x~ < 2^254
 // or lazy < 2p: the shifted value has < 261 bits, limbs exact)
 TA_HD F29 shl5_repack(const uint32_t* w) {
@@ -250,13 +277,13 @@ TA_HD void to32(const F29& x, uint32_t* w) {
   repack32<5>(v, w);
 }
 
-// x = 0 (mod p) for an N-form x < 32p: x = k p exactly for some k < 32, so
+// x = 0 (mod p) for an N-form x < 64p: x = k p exactly for some k < 64, so
 // (x mod 2^32) p^-1 mod 2^32 = k -- a one-multiply filter; the full limb
-// compare runs only when it passes (a true zero, or 32 in 2^32 others).
+// compare runs only when it passes (a true zero, or 64 in 2^32 others).
 TA_HD bool is_zero_mod_p(const F29& x) {
   const uint32_t lo = x.l[0] | (x.l[1] << 29);
   const uint32_t k = lo * kPinv32;
-  if (k >= 32) return false;
+  if (k >= 64) return false;
   uint64_t carry = 0;
   uint32_t diff = 0;
 #pragma unroll

@@ -224,7 +224,7 @@ class MsmGpu {
   int acc29_mode_ = 0;         // ... next base: 0 not prefetched, 1 in registers (bit 13), 2 via LDS-DMA (bit 17)
   bool pair_acc_ = false;      // G2 accumulation with a lane pair per point (bit 15)
   bool acc28_ = false;         // BLS12-381 G1 accumulation over 28-bit limbs (default; bit 20: FIPS 32-bit)
-  bool pair28_ = false;        // BLS12-381 G2 lane pair over 28-bit limbs (default; bit 20: FIPS pair)
+  bool pair_limb_ = false;     // G2 lane pair over 28-bit (BLS12-381) / 29-bit (BN254) limbs (default; bit 20: FIPS pair)
   bool pair_inline_ = false;   // ... its 12-limb products inline (bit 16)
   uint32_t idx_mask_ = 0x7FFFFFFFu;  // base-index mask of the accumulation gathers (strips the sign bit)
   bool fuse_recode_ = true;          // recode fused with the low-byte radix pass

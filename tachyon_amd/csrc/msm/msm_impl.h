@@ -11,6 +11,7 @@
 #include "acc28.h"
 #include "acc_pair.h"
 #include "pair28.h"
+#include "pair29.h"
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -486,8 +487,18 @@ __device__ __forceinline__ Raw raw_of(const Acc& a, bool zero) {
   if (zero) return Raw{};
   return {a.x, a.y, a.zz, a.zzz};
 }
+// an accumulation output (X, Y < 32p: madd's invariant) -> X, Y < 3p, the
+// reductions' invariant
 __device__ __forceinline__ Pt load_raw(const void* __restrict__ p, size_t i) {
   const Raw r = static_cast<const Raw*>(p)[i];
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) nz |= r.zz.l[k];
+  return {{reduce_shl5(r.x), reduce_shl5(r.y), r.zz, r.zzz}, nz == 0};
+}
+// a reduction's own intermediate (already under its invariant)
+__device__ __forceinline__ Pt load_sh(const Raw* __restrict__ p, size_t i) {
+  const Raw r = p[i];
   uint32_t nz = 0;
 #pragma unroll
   for (int k = 0; k < 9; ++k) nz |= r.zz.l[k];
@@ -804,20 +815,51 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_kernel(const Affine<typen
   }
 }
 
-// BLS12-381 G2 with a lane pair per point over the 14 x 28-bit Fq
-// (msm/pair28.h): seg_acc_pair_kernel's run logic; the stores convert this
-// lane's components to the R form the lane-pair FIPS reductions read.
-// set_variant bit 20 restores the FIPS pair (as for BLS12-381 G1).
-__global__ __launch_bounds__(kBlock) void seg_acc_pair28_kernel(const Affine<Bls381Fq2>* __restrict__ bases,
-                                                                const uint64_t* __restrict__ ents, uint32_t c,
-                                                                uint64_t gbeg, uint64_t gend, uint64_t tbase,
-                                                                uint32_t K, uint32_t idx_mask,
-                                                                XYZZ<Bls381Fq2>* __restrict__ bucket_sum,
-                                                                XYZZ<Bls381Fq2>* __restrict__ pieces,
-                                                                uint32_t* __restrict__ tflags,
-                                                                uint32_t* __restrict__ tlast) {
+// The limb-field lane pairs of G2 (field policies of seg_acc_pair_limb_kernel):
+// BLS12-381 over the 14 x 28-bit Fq (msm/pair28.h), BN254 over the 9 x 29-bit
+// Fq (msm/pair29.h).
+struct PairPol28 {
   using Fb = Bls381Fq;
-  using namespace pair28;
+  using F2 = Bls381Fq2;
+  using F = f28::F28;
+  using Acc = pair28::Acc;
+  static __device__ __forceinline__ F repack(const uint32_t* w) { return f28::shl8_repack(w); }
+  static __device__ __forceinline__ Acc start(const F& x, const F& y, bool h) { return pair28::from_shifted(x, y, h); }
+  static __device__ __forceinline__ Acc madd(const Acc& a, const F& x, const F& y, bool h, int* sp) {
+    return pair28::madd(a, x, y, h, sp);
+  }
+  static __device__ __forceinline__ Acc dbl(const Acc& a, bool h) { return pair28::dbl(a, h); }
+  static __device__ __forceinline__ void to32(const F& x, uint32_t* w) { f28::to32(x, w); }
+};
+struct PairPol29 {
+  using Fb = Bn254Fq;
+  using F2 = Bn254Fq2;
+  using F = f29::F29;
+  using Acc = pair29::Acc;
+  static __device__ __forceinline__ F repack(const uint32_t* w) { return f29::shl5_repack(w); }
+  static __device__ __forceinline__ Acc start(const F& x, const F& y, bool h) { return pair29::from_shifted(x, y, h); }
+  static __device__ __forceinline__ Acc madd(const Acc& a, const F& x, const F& y, bool h, int* sp) {
+    return pair29::madd(a, x, y, h, sp);
+  }
+  static __device__ __forceinline__ Acc dbl(const Acc& a, bool h) { return pair29::dbl(a, h); }
+  static __device__ __forceinline__ void to32(const F& x, uint32_t* w) { f29::to32(x, w); }
+};
+
+// G2 with a lane pair per point over a limb field: seg_acc_pair_kernel's run
+// logic; the stores convert this lane's components to the R form the
+// lane-pair FIPS reductions read.  set_variant bit 20 restores the FIPS pair.
+template <class Pol>
+__global__ __launch_bounds__(kBlock) void seg_acc_pair_limb_kernel(const Affine<typename Pol::F2>* __restrict__ bases,
+                                                                   const uint64_t* __restrict__ ents, uint32_t c,
+                                                                   uint64_t gbeg, uint64_t gend, uint64_t tbase,
+                                                                   uint32_t K, uint32_t idx_mask,
+                                                                   XYZZ<typename Pol::F2>* __restrict__ bucket_sum,
+                                                                   XYZZ<typename Pol::F2>* __restrict__ pieces,
+                                                                   uint32_t* __restrict__ tflags,
+                                                                   uint32_t* __restrict__ tlast) {
+  using Fb = typename Pol::Fb;
+  using F = typename Pol::F;
+  using Acc = typename Pol::Acc;
   const uint32_t h = threadIdx.x & 1u;
   const uint64_t tl = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 1;
   const uint64_t g0 = gbeg + tl * K;
@@ -846,13 +888,13 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair28_kernel(const Affine<Bls
       o[6 + h] = Fb::zero();
     } else {
       Fb v;
-      to32(acc.x, v.v);
+      Pol::to32(acc.x, v.v);
       o[h] = v;
-      to32(acc.y, v.v);
+      Pol::to32(acc.y, v.v);
       o[2 + h] = v;
-      to32(acc.zz, v.v);
+      Pol::to32(acc.zz, v.v);
       o[4 + h] = v;
-      to32(acc.zzz, v.v);
+      Pol::to32(acc.zzz, v.v);
       o[6 + h] = v;
     }
   };
@@ -876,17 +918,17 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair28_kernel(const Affine<Bls
         acc_zero = true;
       }
       const uint32_t pz = (px.is_zero_canonical() && py.is_zero_canonical()) ? 1u : 0u;
-      if (!(pz & dpp<kSwap>(pz))) {  // not the identity base (both components zero)
+      if (!(pz & pair::dpp<pair::kSwap>(pz))) {  // not the identity base (both components zero)
         py = py.cond_neg_canonical(v0 & kSignBit);
-        const F28 x2 = shl8_repack(px.v), y2 = shl8_repack(py.v);
+        const F x2 = Pol::repack(px.v), y2 = Pol::repack(py.v);
         if (acc_zero) {
-          acc = from_shifted(x2, y2, h != 0);
+          acc = Pol::start(x2, y2, h != 0);
           acc_zero = false;
         } else {
           int special = 0;
-          acc = madd(acc, x2, y2, h != 0, &special);  // (unchanged when special)
+          acc = Pol::madd(acc, x2, y2, h != 0, &special);  // (unchanged when special)
           if (special == 1) acc_zero = true;
-          else if (special == 2) acc = pair28::dbl(acc, h != 0);
+          else if (special == 2) acc = Pol::dbl(acc, h != 0);
         }
       }
     }
@@ -1323,7 +1365,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_tree29_kernel(const XYZZ<Bn2
   for (unsigned half = span >> 1; half >= 1; half >>= 1) {
     if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
     __syncthreads();
-    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
+    if (j < half) v = acc29::add(v, acc29::load_sh(sh, j));
     __syncthreads();
   }
   if (j == 0) acc29::store_pt(out, w, v);
@@ -1355,7 +1397,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_segtree29_kernel(const XYZZ<
   for (unsigned half = span >> 1; half >= 1; half >>= 1) {
     if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
     __syncthreads();
-    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
+    if (j < half) v = acc29::add(v, acc29::load_sh(sh, j));
     __syncthreads();
   }
   if (j == 0) acc29::store_pt(out, w, v);
@@ -1378,7 +1420,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_scan29_kernel(const XYZZ<Bn2
   for (unsigned d = 1; d < B; d <<= 1) {  // v = T_j
     acc29::store_raw(sh, j, v);
     __syncthreads();
-    if (j + d < B) v = acc29::add(v, acc29::load_raw(sh, j + d));
+    if (j + d < B) v = acc29::add(v, acc29::load_sh(sh, j + d));
     __syncthreads();
   }
   unsigned span = 1;
@@ -1386,7 +1428,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_scan29_kernel(const XYZZ<Bn2
   for (unsigned half = span >> 1; half >= 1; half >>= 1) {
     if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
     __syncthreads();
-    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
+    if (j < half) v = acc29::add(v, acc29::load_sh(sh, j));
     __syncthreads();
   }
   if (j == 0) acc29::store_pt(out, w, v);
@@ -1871,14 +1913,13 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       auto* pair_kernel = pair_inline_ ? &seg_acc_pair_kernel<Curve, false> : &seg_acc_pair_kernel<Curve, kCallDefault>;
       // (kCallDefault is false for 8-limb fields: both entries are the inline kernel there)
       if (pair_acc_) last_schedule_ |= kSchedLanePair;
-      bool pair28 = false;
-      if constexpr (std::is_same_v<Curve, Bls381G2>) pair28 = pair_acc_ && pair28_;
-      if (pair28) {
-        last_schedule_ |= kSchedAcc28;
-        if constexpr (std::is_same_v<Curve, Bls381G2>)
-          hipLaunchKernelGGL(seg_acc_pair28_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
-                             ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_,
-                             bucket_sum, pieces, tflags, tlast);
+      // the limb-field pairs (BLS12-381: 28-bit, BN254: 29-bit; bit 20 restores the FIPS pair)
+      using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
+      if (pair_acc_ && pair_limb_) {
+        last_schedule_ |= std::is_same_v<Curve, Bls381G2> ? kSchedAcc28 : kSchedAcc29;
+        hipLaunchKernelGGL(seg_acc_pair_limb_kernel<LimbPol>, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_,
+                           d_bases, ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_,
+                           bucket_sum, pieces, tflags, tlast);
       } else if (pair_acc_)
         hipLaunchKernelGGL(pair_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_, d_bases,
                            ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum,
@@ -2125,9 +2166,10 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   // BLS12-381 G1: the accumulation over 14 x 28-bit limbs (field/f28.h) by
   // default; bit 20 restores the 12 x 32-bit FIPS field (A/B)
   acc28_ = std::is_same_v<Curve, Bls381G1> && !(variant_ & (1 << 20));
-  // BLS12-381 G2: the lane pair over the same 28-bit field (msm/pair28.h);
-  // bit 20 restores the FIPS pair, bit 15 the one-lane FIPS kernel
-  pair28_ = std::is_same_v<Curve, Bls381G2> && !(variant_ & (1 << 20));
+  // G2: the lane pair over the 28-bit (BLS12-381, msm/pair28.h) / 29-bit
+  // (BN254, msm/pair29.h) field; bit 20 restores the FIPS pair, bit 15 the
+  // one-lane FIPS kernel
+  pair_limb_ = (std::is_same_v<Curve, Bls381G2> || std::is_same_v<Curve, Bn254G2>) && !(variant_ & (1 << 20));
   // G2: a lane pair per point with inline products by default (BLS12-381 G2
   // 2^24 accumulation 129 -> 113 ms, BN254 G2 2^22 16.3 -> 15.7 ms); bit 15
   // restores the one-lane kernel, bit 16 the pair with out-of-line 12-limb products

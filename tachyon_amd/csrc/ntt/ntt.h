@@ -19,6 +19,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 #include <vector>
 
 #include "../common/hip_util.h"
@@ -161,6 +162,7 @@ class Ntt4Step {
 
   size_t local_size() const { return n_ >> log_g_; }
   uint32_t log_rows() const { return log_r_; }
+  const Fr& root() const { return w_; }  // w_n of the plan (the generator set active at construction)
   hipStream_t stream() const { return stream_; }
 
   void forward_stage1(const Fr* in, Fr* send);
@@ -176,9 +178,60 @@ class Ntt4Step {
   NttDomain<Fr>* dom_r_ = nullptr;
   NttDomain<Fr>* dom_c_ = nullptr;
   uint32_t pow_bits_ = 0;
+  Fr w_;
   DeviceBuffer work_, w_lo_, w_hi_, wi_lo_, wi_hi_;
 };
 
 extern template class Ntt4Step<Bn254Fr>;
+
+// One process, several GPUs (round 4): the four-step plan above with one part
+// per entry of `devices` (ids may repeat -- logical devices sharing a GPU on
+// their own streams), the all-to-all as G x G peer copies (hipMemcpyPeerAsync:
+// xGMI between GPUs, a device copy within one), and the natural-order input
+// and output on the primary device: x is transposed there (R x C -> C x R) so
+// that part g's input columns are one contiguous chunk, and the parts' output
+// rows come back as one R x C matrix transposed to natural order.  Everything
+// is enqueued on the primary stream and the parts' streams (events between
+// them).  G = |devices| is a power of two with R = 2^floor(log_n / 2) >= G.
+template <class Fr>
+class NttMultiDevice {
+ public:
+  NttMultiDevice(uint32_t log_n, const std::vector<int>& devices, int primary, hipStream_t primary_stream);
+  ~NttMultiDevice();
+  NttMultiDevice(const NttMultiDevice&) = delete;
+  NttMultiDevice& operator=(const NttMultiDevice&) = delete;
+
+  size_t size() const { return n_; }
+  const std::vector<int>& device_ids() const { return ids_; }
+  const Fr& root() const { return parts_[0]->plan->root(); }
+  // x -> y, n elements each on the primary device (may alias); not synchronised
+  void forward_device(const Fr* x, Fr* y) { run(x, y, false); }
+  void inverse_device(const Fr* x, Fr* y) { run(x, y, true); }
+  // host vectors: len <= n inputs, zero-padded; n outputs (may alias); synchronises
+  void forward_host(const Fr* in, size_t len, Fr* out) { host(in, len, out, false); }
+  void inverse_host(const Fr* in, size_t len, Fr* out) { host(in, len, out, true); }
+
+ private:
+  struct Part {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::unique_ptr<Ntt4Step<Fr>> plan;
+    DeviceBuffer in, send, recv, out;
+    hipEvent_t ev1 = nullptr, ev2 = nullptr;
+  };
+  void run(const Fr* x, Fr* y, bool inverse);
+  void host(const Fr* in, size_t len, Fr* out, bool inverse);
+
+  uint32_t log_n_, log_g_, log_r_, log_c_;
+  size_t n_;
+  int primary_;
+  hipStream_t s0_;
+  hipEvent_t ev0_ = nullptr;
+  std::vector<int> ids_;
+  std::vector<std::unique_ptr<Part>> parts_;
+  DeviceBuffer stage_, io_;
+};
+
+extern template class NttMultiDevice<Bn254Fr>;
 
 }  // namespace tachyon_amd::ntt

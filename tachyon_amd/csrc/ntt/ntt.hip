@@ -935,6 +935,7 @@ Ntt4Step<Fr>::Ntt4Step(uint32_t log_n, uint32_t log_world, uint32_t rank, hipStr
   // w_n and its two-level power tables (w_n^e = lo[e & mask] * hi[e >> bits])
   Fr w = two_adic_root<Fr>();
   for (uint32_t i = log_n; i < (uint32_t)Fr::Config::kTwoAdicity; ++i) w = w.sqr();
+  w_ = w;
   pow_bits_ = (log_n + 1) / 2;
   const size_t lo_cnt = size_t(1) << pow_bits_, hi_cnt = size_t(1) << (log_n - pow_bits_);
   const Fr wi = w.inverse();
@@ -1006,6 +1007,153 @@ void Ntt4Step<Fr>::inverse_stage2(const Fr* recv, Fr* out) {
 }
 
 template <class Fr>
+NttMultiDevice<Fr>::NttMultiDevice(uint32_t log_n, const std::vector<int>& devices, int primary,
+                                   hipStream_t primary_stream)
+    : log_n_(log_n), n_(size_t(1) << log_n), primary_(primary), s0_(primary_stream), ids_(devices) {
+  const size_t G = devices.size();
+  if (G < 2 || (G & (G - 1))) throw std::runtime_error("tachyon_mi355x: multi-device NTT needs 2^k >= 2 devices");
+  log_g_ = (uint32_t)__builtin_ctzll(G);
+  log_r_ = log_n / 2;
+  log_c_ = log_n - log_r_;
+  if (log_g_ > log_r_) throw std::runtime_error("tachyon_mi355x: multi-device NTT needs R = 2^floor(L/2) >= devices");
+  int count = 0, prev = 0;
+  TA_HIP(hipGetDeviceCount(&count));
+  for (int d : devices)
+    if (d < 0 || d >= count) throw std::runtime_error("tachyon_mi355x: device id out of range");
+  TA_HIP(hipGetDevice(&prev));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{prev};
+  TA_HIP(hipSetDevice(primary_));
+  TA_HIP(hipEventCreateWithFlags(&ev0_, hipEventDisableTiming));
+  for (int d : devices)  // xGMI peer access where the pair supports it (copies work without it)
+    if (d != primary_) {
+      int ok = 0;
+      if (hipDeviceCanAccessPeer(&ok, primary_, d) == hipSuccess && ok) (void)hipDeviceEnablePeerAccess(d, 0);
+      (void)hipGetLastError();
+    }
+  for (size_t g = 0; g < G; ++g) {
+    TA_HIP(hipSetDevice(devices[g]));
+    auto p = std::make_unique<Part>();
+    p->device = devices[g];
+    TA_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    TA_HIP(hipEventCreateWithFlags(&p->ev1, hipEventDisableTiming));
+    TA_HIP(hipEventCreateWithFlags(&p->ev2, hipEventDisableTiming));
+    p->plan = std::make_unique<Ntt4Step<Fr>>(log_n, log_g_, (uint32_t)g, p->stream);
+    const size_t m = n_ >> log_g_;
+    p->in.ensure(m * sizeof(Fr));
+    p->send.ensure(m * sizeof(Fr));
+    p->recv.ensure(m * sizeof(Fr));
+    p->out.ensure(m * sizeof(Fr));
+    for (int e : devices)
+      if (e != devices[g]) {
+        int ok = 0;
+        if (hipDeviceCanAccessPeer(&ok, devices[g], e) == hipSuccess && ok) (void)hipDeviceEnablePeerAccess(e, 0);
+        (void)hipGetLastError();
+      }
+    parts_.push_back(std::move(p));
+  }
+  TA_HIP(hipSetDevice(primary_));
+  stage_.ensure(n_ * sizeof(Fr));
+}
+
+template <class Fr>
+NttMultiDevice<Fr>::~NttMultiDevice() {
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) prev = 0;
+  for (auto& p : parts_) {  // each part's stream, events and buffers on its own device
+    (void)hipSetDevice(p->device);
+    (void)hipStreamSynchronize(p->stream);
+    p->plan.reset();
+    p->in.release();
+    p->send.release();
+    p->recv.release();
+    p->out.release();
+    (void)hipEventDestroy(p->ev1);
+    (void)hipEventDestroy(p->ev2);
+    (void)hipStreamDestroy(p->stream);
+  }
+  (void)hipSetDevice(primary_);
+  (void)hipStreamSynchronize(s0_);
+  stage_.release();
+  io_.release();
+  if (ev0_) (void)hipEventDestroy(ev0_);
+  (void)hipSetDevice(prev);
+}
+
+// forward: stage = x^T (C x R), part g's input = stage chunk g (its columns,
+//   column-major); stage 1; all-to-all; stage 2 -> rows [g R/G, (g+1) R/G) of
+//   Z[k1][k2] = X[k1 + R k2]; the parts' rows = Z (R x C) in stage; y = Z^T.
+// inverse: stage = Z = y^T as (R x C) from y (C x R), part g's input = rows
+//   chunk g; inverse stages 1, 2 -> columns; the parts' columns = x^T; x = transpose.
+template <class Fr>
+void NttMultiDevice<Fr>::run(const Fr* x, Fr* y, bool inverse) {
+  const size_t G = parts_.size(), m = n_ >> log_g_, chunk = m >> log_g_;
+  const uint32_t R = 1u << log_r_, C = 1u << log_c_;
+  const uint32_t rows_in = inverse ? C : R, cols_in = inverse ? R : C;
+  int prev = 0;
+  TA_HIP(hipGetDevice(&prev));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{prev};
+  TA_HIP(hipSetDevice(primary_));
+  Fr* stage = stage_.as<Fr>();
+  hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(cols_in, 32), ceil_div(rows_in, 32)), dim3(kBlock), 0, s0_,
+                     x, stage, rows_in, cols_in);
+  TA_HIP(hipGetLastError());
+  TA_HIP(hipEventRecord(ev0_, s0_));
+  for (size_t g = 0; g < G; ++g) {  // scatter + stage 1
+    Part& p = *parts_[g];
+    TA_HIP(hipSetDevice(p.device));
+    TA_HIP(hipStreamWaitEvent(p.stream, ev0_, 0));
+    TA_HIP(hipMemcpyPeerAsync(p.in.template as<void>(), p.device, stage + g * m, primary_, m * sizeof(Fr), p.stream));
+    if (inverse) p.plan->inverse_stage1(p.in.template as<Fr>(), p.send.template as<Fr>());
+    else p.plan->forward_stage1(p.in.template as<Fr>(), p.send.template as<Fr>());
+    TA_HIP(hipEventRecord(p.ev1, p.stream));
+  }
+  for (size_t h = 0; h < G; ++h) {  // all-to-all: chunk h of every part's send -> part h's recv + stage 2
+    Part& q = *parts_[h];
+    TA_HIP(hipSetDevice(q.device));
+    for (size_t g = 0; g < G; ++g) TA_HIP(hipStreamWaitEvent(q.stream, parts_[g]->ev1, 0));
+    for (size_t g = 0; g < G; ++g)
+      TA_HIP(hipMemcpyPeerAsync(q.recv.template as<Fr>() + g * chunk, q.device, parts_[g]->send.template as<Fr>() + h * chunk,
+                                parts_[g]->device, chunk * sizeof(Fr), q.stream));
+    if (inverse) q.plan->inverse_stage2(q.recv.template as<Fr>(), q.out.template as<Fr>());
+    else q.plan->forward_stage2(q.recv.template as<Fr>(), q.out.template as<Fr>());
+    TA_HIP(hipEventRecord(q.ev2, q.stream));
+  }
+  TA_HIP(hipSetDevice(primary_));
+  for (size_t g = 0; g < G; ++g) {  // gather on the primary stream
+    Part& p = *parts_[g];
+    TA_HIP(hipStreamWaitEvent(s0_, p.ev2, 0));
+    TA_HIP(hipMemcpyPeerAsync(stage + g * m, primary_, p.out.template as<void>(), p.device, m * sizeof(Fr), s0_));
+  }
+  hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(rows_in, 32), ceil_div(cols_in, 32)), dim3(kBlock), 0, s0_,
+                     stage, y, cols_in, rows_in);
+  TA_HIP(hipGetLastError());
+}
+
+template <class Fr>
+void NttMultiDevice<Fr>::host(const Fr* in, size_t len, Fr* out, bool inverse) {
+  if (len > n_) throw std::runtime_error("tachyon_mi355x: more inputs than the domain size");
+  int prev = 0;
+  TA_HIP(hipGetDevice(&prev));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{prev};
+  TA_HIP(hipSetDevice(primary_));
+  Fr* d = static_cast<Fr*>(io_.ensure(n_ * sizeof(Fr)));
+  TA_HIP(hipMemcpyAsync(d, in, len * sizeof(Fr), hipMemcpyHostToDevice, s0_));
+  if (len < n_) TA_HIP(hipMemsetAsync(d + len, 0, (n_ - len) * sizeof(Fr), s0_));
+  run(d, d, inverse);
+  TA_HIP(hipMemcpyAsync(out, d, n_ * sizeof(Fr), hipMemcpyDeviceToHost, s0_));
+  TA_HIP(hipStreamSynchronize(s0_));
+}
+
+template <class Fr>
 Fr root_of_unity(uint32_t log_n) {
   if (log_n > (uint32_t)Fr::Config::kTwoAdicity)
     throw std::runtime_error("tachyon_mi355x: no root of unity of that order in the field");
@@ -1028,5 +1176,6 @@ template Bls381Fr root_of_unity<Bls381Fr>(uint32_t);
 template Bn254Fr field_from_u64<Bn254Fr>(uint64_t);
 template Bls381Fr field_from_u64<Bls381Fr>(uint64_t);
 template class Ntt4Step<Bn254Fr>;
+template class NttMultiDevice<Bn254Fr>;
 
 }  // namespace tachyon_amd::ntt

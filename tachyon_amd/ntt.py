@@ -151,6 +151,20 @@ class Radix2EvaluationDomain:
         if not lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(self._d, variant):
             raise ValueError(f"unknown NTT variant {variant}")
 
+    def set_devices(self, device_ids):
+        """Run later transforms of the plain domain as a four-step NTT over these
+        devices, one process (ids may repeat; a power of two of them; [] or one
+        id = single device) -- tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices."""
+        ids = list(device_ids)
+        arr = (ctypes.c_int * max(1, len(ids)))(*ids)
+        if not lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices(self._d, arr, len(ids)):
+            raise ValueError(f"device list refused for a 2^{self.size.bit_length() - 1} domain: {ids}")
+
+    def devices(self) -> list:
+        arr = (ctypes.c_int * 64)()
+        k = lib().tachyon_mi355x_bn254_univariate_evaluation_domain_devices(self._d, arr, 64)
+        return list(arr)[:min(k, 64)]
+
     def last_timings(self):
         total = ctypes.c_float()
         passes = (ctypes.c_float * 16)()

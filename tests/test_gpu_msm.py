@@ -61,13 +61,15 @@ def test_msm_golden_bn254_g1_variants(variant):
     m.close()
 
 
-@pytest.mark.parametrize("curve,variant", [("bn254_g2", 0), ("bn254_g2", 32768), ("bls12_381_g2", 0),
+@pytest.mark.parametrize("curve,variant", [("bn254_g2", 0), ("bn254_g2", 32768), ("bn254_g2", 1 << 20),
+                                           ("bls12_381_g2", 0),
                                            ("bls12_381_g2", 32768), ("bls12_381_g2", 65536 | (1 << 20)),
                                            ("bls12_381_g2", 1 << 20)])
 def test_msm_golden_g2_lane_pair(curve, variant):
-    """The G2 accumulations: a lane pair per point with inline products (the
-    default), the one-lane kernel (set_variant bit 15) and, for BLS12-381, the
-    pair with out-of-line 12-limb products (bit 16) -- golden edge cases, a
+    """The G2 accumulations: a lane pair per point over the limb fields (the
+    default: BN254 9 x 29-bit, BLS12-381 14 x 28-bit), the FIPS pair (bit 20),
+    the one-lane kernel (set_variant bit 15) and, for BLS12-381, the FIPS pair
+    with out-of-line 12-limb products (bit 16) -- golden edge cases, a
     random set, a repeated base (doublings inside one bucket) and P, -P
     alternating (cancellations)."""
     from tachyon_amd.msm import VariableBaseMSMGpu
@@ -384,8 +386,11 @@ def test_msm_schedule_variants_agree(curve, logn):
                 assert s["acc28"] == (not v & (1 << 20)), (hex(v), s)
             else:  # G2: the lane pair by default; bit 15 the one-lane kernel
                 assert s["lane_pair"] == (v != 32768), (hex(v), s)
+                limb = v != 32768 and not v & (1 << 20)
                 if curve == "bls12_381_g2":  # the pair over 28-bit limbs; bit 20 the FIPS pair
-                    assert s["acc28"] == (v != 32768 and not v & (1 << 20)), (hex(v), s)
+                    assert s["acc28"] == limb, (hex(v), s)
+                else:  # BN254 G2: the pair over 29-bit limbs; bit 20 the FIPS pair
+                    assert s["acc29"] == limb, (hex(v), s)
         for bad in (64, 1 << 22):
             with pytest.raises(ValueError):
                 m.set_variant(bad)

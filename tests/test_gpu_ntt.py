@@ -215,3 +215,56 @@ def test_field29_extreme_inputs():
             assert d.fft(v) == want, variant
             assert d.ifft(want) == O.ifft(want, n), variant
             d.close()
+
+
+@pytest.mark.parametrize("log_n,devices", [(4, [0, 0]), (10, [0, 0]), (13, [0, 0, 0, 0]), (16, [0] * 8),
+                                           (20, [0, 0])])
+def test_multi_device_domain_logical(log_n, devices):
+    """One process, several devices (set_devices): the plain domain's fft / ifft,
+    transform_host and transform_device run the four-step over `devices`
+    (logical devices sharing the box's one GPU: the peer copies are device
+    copies) -- bytewise equal to the oracle and to the single-device domain;
+    a coset keeps the single device; [] restores it."""
+    torch = pytest.importorskip("torch")
+    n = 1 << log_n
+    coeffs = O.gen_scalars("bn254_fr", 3000 + log_n, n).tobytes()
+    d = domain(n)
+    d.set_devices(devices)
+    assert d.devices() == devices
+    ev = d.fft(coeffs)
+    assert ev == O.fft(coeffs, n)
+    assert d.ifft(ev) == O.ifft(ev, n)
+    short = coeffs[:32 * (n // 3 + 1)]  # zero padding
+    assert d.fft(short) == O.fft(short, n)
+    buf = np.frombuffer(bytearray(coeffs), dtype=np.uint8).copy()
+    d.transform_host(buf)
+    assert buf.tobytes() == ev
+    x = torch.frombuffer(bytearray(coeffs), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    d.transform_device(x.data_ptr())
+    torch.cuda.synchronize()
+    assert x.cpu().numpy().tobytes() == ev
+    d.transform_device(x.data_ptr(), inverse=True)
+    torch.cuda.synchronize()
+    assert x.cpu().numpy().tobytes() == coeffs
+    five = O.field_op("bn254_fr", "to_mont", (5).to_bytes(32, "little"))
+    d.set_offset(five)
+    assert d.fft(coeffs) == O.fft(coeffs, n, five)
+    d.set_offset(O.field_op("bn254_fr", "to_mont", (1).to_bytes(32, "little")))
+    d.set_devices([])
+    assert d.devices() == []
+    assert d.fft(coeffs) == ev
+    d.close()
+
+
+def test_multi_device_domain_refused():
+    """Device lists the four-step cannot take leave the domain unchanged: not a
+    power of two, more devices than R = 2^floor(log n / 2), a bad id."""
+    d = domain(1 << 10)
+    for bad in ([0, 0, 0], [0] * 64, [0, 99], [-1, 0]):
+        with pytest.raises(ValueError):
+            d.set_devices(bad)
+        assert d.devices() == []
+    coeffs = O.gen_scalars("bn254_fr", 77, 1 << 10).tobytes()
+    assert d.fft(coeffs) == O.fft(coeffs, 1 << 10)
+    d.close()
