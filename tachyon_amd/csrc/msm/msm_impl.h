@@ -476,16 +476,22 @@ __device__ __forceinline__ Pt add(const Pt& a, const Pt& b) {
   return {special == 2 ? dbl(a.a) : s, false};
 }
 // A bucket or piece as the 29-bit accumulation leaves it (R' form, 4 x 9
-// limbs, 144 B; all-zero limbs = the identity): the accumulation's run-end
+// limbs, 144 B; zz = 0 is the identity): the accumulation's run-end
 // stores skip the four R-form conversions (they run in the loop's divergent
 // branch whenever any lane of the wave changes bucket) and the 29-bit
 // reductions read it without converting.
 struct alignas(16) Raw {
   F29 x, y, zz, zzz;
 };
+// the identity is zz = 0 (load_raw / load_sh test zz only; the other limbs
+// are not read then): one masked coordinate instead of four in the
+// accumulation's divergent store branch
 __device__ __forceinline__ Raw raw_of(const Acc& a, bool zero) {
-  if (zero) return Raw{};
-  return {a.x, a.y, a.zz, a.zzz};
+  const uint32_t keep = zero ? 0u : ~0u;
+  Raw r{a.x, a.y, a.zz, a.zzz};
+#pragma unroll
+  for (int k = 0; k < 9; ++k) r.zz.l[k] &= keep;
+  return r;
 }
 // an accumulation output (X, Y < 32p: madd's invariant) -> X, Y < 3p, the
 // reductions' invariant

@@ -1082,11 +1082,13 @@ NttMultiDevice<Fr>::~NttMultiDevice() {
   (void)hipSetDevice(prev);
 }
 
-// forward: stage = x^T (C x R), part g's input = stage chunk g (its columns,
-//   column-major); stage 1; all-to-all; stage 2 -> rows [g R/G, (g+1) R/G) of
-//   Z[k1][k2] = X[k1 + R k2]; the parts' rows = Z (R x C) in stage; y = Z^T.
-// inverse: stage = Z = y^T as (R x C) from y (C x R), part g's input = rows
-//   chunk g; inverse stages 1, 2 -> columns; the parts' columns = x^T; x = transpose.
+// forward: stage = x^T (x as R x C), part g's input = stage chunk g (its
+//   columns, column-major); stage 1; all-to-all; stage 2 -> rows [g R/G,
+//   (g+1) R/G) of Z[k1][k2] = X[k1 + R k2]; the parts' rows = Z (R x C) in
+//   stage; y = Z^T.  Both transposes take an R x C matrix.
+// inverse: stage = Z = y^T (y as C x R), part g's input = rows chunk g;
+//   inverse stages 1, 2 -> columns; the parts' columns = x^T (C x R); x = its
+//   transpose.  Both transposes take a C x R matrix.
 template <class Fr>
 void NttMultiDevice<Fr>::run(const Fr* x, Fr* y, bool inverse) {
   const size_t G = parts_.size(), m = n_ >> log_g_, chunk = m >> log_g_;
@@ -1130,8 +1132,8 @@ void NttMultiDevice<Fr>::run(const Fr* x, Fr* y, bool inverse) {
     TA_HIP(hipStreamWaitEvent(s0_, p.ev2, 0));
     TA_HIP(hipMemcpyPeerAsync(stage + g * m, primary_, p.out.template as<void>(), p.device, m * sizeof(Fr), s0_));
   }
-  hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(rows_in, 32), ceil_div(cols_in, 32)), dim3(kBlock), 0, s0_,
-                     stage, y, cols_in, rows_in);
+  hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(cols_in, 32), ceil_div(rows_in, 32)), dim3(kBlock), 0, s0_,
+                     stage, y, rows_in, cols_in);
   TA_HIP(hipGetLastError());
 }
 

@@ -57,7 +57,7 @@ def main():
     if show_blocks:
         for lab, c in blocks:
             n = sum(c.values())
-            if n > 50:
+            if n > int(__import__("os").environ.get("MINB", "50")):
                 print(f"block {lab}: {n} instrs; " + ", ".join(f"{k}:{v}" for k, v in c.most_common(8)))
 
 
