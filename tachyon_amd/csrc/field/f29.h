@@ -49,15 +49,9 @@ constexpr uint32_t kK8[9] = {0x83e7ea38u, 0x882305b2u, 0x83951a74u, 0x96a91683u,
 // 16p, low limbs raised by 2^29
 constexpr uint32_t kK16[9] = {0x27cfd470u, 0x30460b6bu, 0x272a34efu, 0x2d522d0du, 0x385d9780u,
                               0x2db40c09u, 0x2a6e1410u, 0x25c2633fu, 0x030644e6u};
-// 33p, low limbs raised by 2^29 (minus a normalized value < 32p)
+// 33p, low limbs raised by 2^29 (minus a normalized value < 32p: msm/pair29.h)
 constexpr uint32_t kK33[9] = {0x281ca627u, 0x2190778eu, 0x2ac70d2fu, 0x3d797cecu, 0x26410879u,
                               0x3e4358d5u, 0x35830962u, 0x39e0ecb3u, 0x063cee1bu};
-// 16p, low limbs raised by 2^31 (minus PPP + 2Q, limbs < 3 2^29)
-constexpr uint32_t kK16r4[9] = {0x87cfd470u, 0x90460b68u, 0x872a34ecu, 0x8d522d0au, 0x985d977du,
-                                0x8db40c06u, 0x8a6e140du, 0x85c2633cu, 0x030644e3u};
-// 32p, low limbs raised by 2^29
-constexpr uint32_t kK32[9] = {0x2f9fa8e0u, 0x208c16d7u, 0x2e5469e0u, 0x3aa45a1bu, 0x30bb2f01u,
-                              0x3b681814u, 0x34dc2821u, 0x2b84c67fu, 0x060c89cdu};
 // 32p, low limbs raised by 3 2^29 (the lane-pair G2 products negate T = Q + 16p - X3,
 // limbs < 3 2^29 - 2, msm/pair29.h)
 constexpr uint32_t kK32r3[9] = {0x6f9fa8e0u, 0x608c16d5u, 0x6e5469deu, 0x7aa45a19u, 0x70bb2effu,

@@ -12,30 +12,29 @@ struct Acc {
   F29 x, y, zz, zzz;
 };
 
-// the first point of a run: its shifted coordinates as they are (X, Y < 32p;
-// the madd below takes them without a reduction)
-TA_HD Acc from_shifted(const F29& x2, const F29& y2) { return {x2, y2, konst(kOne29), konst(kOne29)}; }
+// the first point of a run, from its coordinates already shifted for madd
+TA_HD Acc from_shifted(const F29& x2, const F29& y2) {
+  return {reduce_shl5(x2), reduce_shl5(y2), konst(kOne29), konst(kOne29)};
+}
 
 // acc + (x2, y2): madd-2008-s (point_xyzz_impl.h:129-176) with every
 // subtraction folded into a product's output columns (limb-wise K - x, K a
 // raised multiple of p) and Y3 = R (Q - X3) - Y1 PPP as one reduction of
-// R T + (33p - Y1) PPP.  Value bounds (in units of p; a product of A and B
-// leaves < A B / 128 + 1 + addend), invariant of the accumulator X, Y < 32,
-// ZZ, ZZZ < 3 -- wide enough for a run's first point as it comes
-// (from_shifted: x~ << 5 < 32p, no reduction) and the doubling's output
-// (from32, < 3p); base coordinates x~ << 5 < 32:
-//   P   = x2 ZZ1 + (33p - X1)  < 34.75    R  = y2 ZZZ1 + (33p - Y1) < 34.75
-//   PP  = P^2 < 10.44  PPP = P PP < 3.84  Q  = X1 PP < 3.61
-//   X3  = R^2 + (16p - PPP - 2Q) < 26.44  T  = Q + (32p - X3) < 35.61
-//   Y3  = R T + (33p - Y1) PPP < 11.66    ZZ3, ZZZ3 < 1.25
-// Column sums stay below 2^64: the widest, R T + (33p - Y1) PPP + m p, is
-// < 13.5 2^60 (T's limbs < 1.5 2^30, 33p - Y1's < 2^30).  The reductions
-// take these points through load_raw, which brings X and Y under 3p.
+// R T + (4p - Y1) PPP.  Value bounds (in units of p; a product of A and B
+// leaves < A B / 128 + 1 + addend), invariant acc X < 10, Y, ZZ, ZZZ < 3 (a
+// run's first point and the doubling's output come in through from32, < 3p);
+// base coordinates x~ << 5 < 32:
+//   P   = x2 ZZ1 + (16p - X1)  < 17.75    R  = y2 ZZZ1 + (4p - Y1) < 5.75
+//   PP  = P^2 < 3.47  PPP = P PP < 1.49   Q  = X1 PP < 1.28
+//   X3  = R^2 + (8p - PPP - 2Q) < 9.26    T  = Q + (16p - X3) < 17.3
+//   Y3  = R T + (4p - Y1) PPP < 1.83      ZZ3, ZZZ3 < 1.09
+// Column sums stay below 2^64: the widest, R T + (4p - Y1) PPP + m p, is
+// < 13.5 2^60 (T's limbs < 1.41 2^30, 4p - Y1's < 2^30).
 // *special = 1: the sum is the identity (P = -acc), 2: P = acc (the caller
 // doubles); acc is returned unchanged then.
 TA_HD Acc madd(const Acc& A, const F29& x2, const F29& y2, int* special) {
-  const F29 P = mul_add(x2, A.zz, ksub(kK33, A.x));
-  const F29 R = mul_add(y2, A.zzz, ksub(kK33, A.y));
+  const F29 P = mul_add(x2, A.zz, ksub(kK16, A.x));
+  const F29 R = mul_add(y2, A.zzz, ksub(kK4, A.y));
   if (is_zero_mod_p(P)) {
     *special = is_zero_mod_p(R) ? 2 : 1;
     return A;
@@ -44,9 +43,9 @@ TA_HD Acc madd(const Acc& A, const F29& x2, const F29& y2, int* special) {
   const F29 PPP = mul(P, PP);
   const F29 Q = mul(A.x, PP);
   Acc C;
-  C.x = sqr_add(R, ksub2(kK16r4, PPP, Q));
-  const F29 T = add_ksub(Q, kK32, C.x);
-  C.y = mul2_add(R, T, ksub(kK33, A.y), PPP);
+  C.x = sqr_add(R, ksub2(kK8, PPP, Q));
+  const F29 T = add_ksub(Q, kK16, C.x);
+  C.y = mul2_add(R, T, ksub(kK4, A.y), PPP);
   C.zz = mul(A.zz, PP);
   C.zzz = mul(A.zzz, PPP);
   return C;

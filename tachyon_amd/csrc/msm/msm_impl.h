@@ -476,35 +476,19 @@ __device__ __forceinline__ Pt add(const Pt& a, const Pt& b) {
   return {special == 2 ? dbl(a.a) : s, false};
 }
 // A bucket or piece as the 29-bit accumulation leaves it (R' form, 4 x 9
-// limbs, 144 B; zz = 0 is the identity): the accumulation's run-end
+// limbs, 144 B; all-zero limbs = the identity): the accumulation's run-end
 // stores skip the four R-form conversions (they run in the loop's divergent
 // branch whenever any lane of the wave changes bucket) and the 29-bit
 // reductions read it without converting.
 struct alignas(16) Raw {
   F29 x, y, zz, zzz;
 };
-// the identity is zz = 0 (load_raw / load_sh test zz only; the other limbs
-// are not read then): one masked coordinate instead of four in the
-// accumulation's divergent store branch
 __device__ __forceinline__ Raw raw_of(const Acc& a, bool zero) {
-  const uint32_t keep = zero ? 0u : ~0u;
-  Raw r{a.x, a.y, a.zz, a.zzz};
-#pragma unroll
-  for (int k = 0; k < 9; ++k) r.zz.l[k] &= keep;
-  return r;
+  if (zero) return Raw{};
+  return {a.x, a.y, a.zz, a.zzz};
 }
-// an accumulation output (X, Y < 32p: madd's invariant) -> X, Y < 3p, the
-// reductions' invariant
 __device__ __forceinline__ Pt load_raw(const void* __restrict__ p, size_t i) {
   const Raw r = static_cast<const Raw*>(p)[i];
-  uint32_t nz = 0;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) nz |= r.zz.l[k];
-  return {{reduce_shl5(r.x), reduce_shl5(r.y), r.zz, r.zzz}, nz == 0};
-}
-// a reduction's own intermediate (already under its invariant)
-__device__ __forceinline__ Pt load_sh(const Raw* __restrict__ p, size_t i) {
-  const Raw r = p[i];
   uint32_t nz = 0;
 #pragma unroll
   for (int k = 0; k < 9; ++k) nz |= r.zz.l[k];
@@ -835,7 +819,11 @@ struct PairPol28 {
     return pair28::madd(a, x, y, h, sp);
   }
   static __device__ __forceinline__ Acc dbl(const Acc& a, bool h) { return pair28::dbl(a, h); }
+  static __device__ __forceinline__ Acc add(const Acc& a, const Acc& b, bool h, int* sp) {
+    return pair28::add(a, b, h, sp);
+  }
   static __device__ __forceinline__ void to32(const F& x, uint32_t* w) { f28::to32(x, w); }
+  static __device__ __forceinline__ F from32(const uint32_t* w) { return f28::from32(w); }
 };
 struct PairPol29 {
   using Fb = Bn254Fq;
@@ -848,7 +836,11 @@ struct PairPol29 {
     return pair29::madd(a, x, y, h, sp);
   }
   static __device__ __forceinline__ Acc dbl(const Acc& a, bool h) { return pair29::dbl(a, h); }
+  static __device__ __forceinline__ Acc add(const Acc& a, const Acc& b, bool h, int* sp) {
+    return pair29::add(a, b, h, sp);
+  }
   static __device__ __forceinline__ void to32(const F& x, uint32_t* w) { f29::to32(x, w); }
+  static __device__ __forceinline__ F from32(const uint32_t* w) { return f29::from32(w); }
 };
 
 // G2 with a lane pair per point over a limb field: seg_acc_pair_kernel's run
@@ -1236,14 +1228,77 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_segment
 // XYZZ<Fq2> additions hold two points and their temporaries (BLS12-381:
 // 220-460 spilled VGPRs per kernel, 21 ms of a 2^24 MSM); split by component
 // they stay in registers.  Same schedules as the one-lane kernels above.
+// The arithmetic of the pair reductions: the FIPS lane pair (acc_pair.h) or a
+// limb-field pair (msm/pair28.h, pair29.h) that converts the R-form arrays on
+// load (from32, < 3p) and store (to32), keeping identities as flags.
 template <class Curve>
-struct PairTypes {
+struct FipsPairArith {
   using Fb = typename Curve::F::Base;
   using H = pair::Half<HotFp<Fb>, Fb::N == 12>;
   using A = pair::Acc<H>;
+  static __device__ __forceinline__ A load(const Fb* p, size_t i, uint32_t h) { return pair::load<H>(p, i, h); }
+  static __device__ __forceinline__ void store(Fb* p, size_t i, uint32_t h, const A& a) { pair::store(p, i, h, a); }
+  static __device__ __forceinline__ A add(const A& a, const A& b, bool h) { return pair::add(a, b, h); }
+  static __device__ __forceinline__ A zero(bool h) { return pair::zero<H>(h); }
+  static __device__ __forceinline__ A small_mul(const A& P, uint32_t m, bool h) { return pair::small_mul(P, m, h); }
+};
+template <class Pol>
+struct LimbPairArith {
+  using Fb = typename Pol::Fb;
+  struct A {
+    typename Pol::Acc a;
+    bool zero;
+  };
+  static __device__ __forceinline__ A load(const Fb* p, size_t i, uint32_t h) {
+    const Fb* o = p + 8 * i;
+    const Fb x = o[h], y = o[2 + h], zz = o[4 + h], zzz = o[6 + h];
+    uint32_t nz = 0;
+#pragma unroll
+    for (int k = 0; k < Fb::N; ++k) nz |= zz.v[k];
+    nz |= pair::dpp<pair::kSwap>(nz);  // the identity: zz = 0 in both components
+    return {{Pol::from32(x.v), Pol::from32(y.v), Pol::from32(zz.v), Pol::from32(zzz.v)}, nz == 0};
+  }
+  static __device__ __forceinline__ void store(Fb* p, size_t i, uint32_t h, const A& a) {
+    Fb* o = p + 8 * i;
+    if (a.zero) {
+      const Fb one_h = h ? Fb::zero() : Fb::one();
+      o[h] = one_h;
+      o[2 + h] = one_h;
+      o[4 + h] = Fb::zero();
+      o[6 + h] = Fb::zero();
+      return;
+    }
+    Fb v;
+    Pol::to32(a.a.x, v.v);
+    o[h] = v;
+    Pol::to32(a.a.y, v.v);
+    o[2 + h] = v;
+    Pol::to32(a.a.zz, v.v);
+    o[4 + h] = v;
+    Pol::to32(a.a.zzz, v.v);
+    o[6 + h] = v;
+  }
+  static __device__ __forceinline__ A add(const A& a, const A& b, bool h) {
+    if (a.zero) return b;
+    if (b.zero) return a;
+    int special = 0;
+    const typename Pol::Acc s = Pol::add(a.a, b.a, h, &special);
+    if (special == 1) return {a.a, true};
+    return {special == 2 ? Pol::dbl(a.a, h) : s, false};
+  }
+  static __device__ __forceinline__ A zero(bool) { return {typename Pol::Acc{}, true}; }
+  static __device__ __forceinline__ A small_mul(const A& P, uint32_t m, bool h) {
+    if (m == 0 || P.zero) return zero(h);
+    A r = P;
+    for (int bit = 30 - __builtin_clz(m); bit >= 0; --bit) {
+      r.a = Pol::dbl(r.a, h);  // (no point of this prime-order group doubles to the identity)
+      if ((m >> bit) & 1) r = add(r, P, h);
+    }
+    return r;
+  }
 };
 
-template <class Curve>
+template <class Curve, class Ar = FipsPairArith<Curve>>
 __global__ __launch_bounds__(kBlock, 2) void seg_reduce_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                                  const uint32_t* __restrict__ beg,
                                                                  const uint32_t* __restrict__ end,
@@ -1251,9 +1306,7 @@ __global__ __launch_bounds__(kBlock, 2) void seg_reduce_pair_kernel(const XYZZ<t
                                                                  unsigned K2, XYZZ<typename Curve::F>* __restrict__ out,
                                                                  const uint32_t* __restrict__ bucket,
                                                                  XYZZ<typename Curve::F>* __restrict__ bucket_sum) {
-  using T = PairTypes<Curve>;
-  using Fb = typename T::Fb;
-  using H = typename T::H;
+  using Fb = typename Ar::Fb;
   const uint32_t h = threadIdx.x & 1u;
   const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
   if (t >= out_off[nseg]) return;  // both lanes of the pair
@@ -1261,19 +1314,17 @@ __global__ __launch_bounds__(kBlock, 2) void seg_reduce_pair_kernel(const XYZZ<t
   const uint32_t e0 = beg[s] + (t - out_off[s]) * K2;
   const uint32_t e1 = min(end[s], e0 + K2);
   const Fb* src = reinterpret_cast<const Fb*>(in);
-  pair::Acc<H> acc = pair::load<H>(src, e0, h);
-  for (uint32_t e = e0 + 1; e < e1; ++e) acc = pair::add(acc, pair::load<H>(src, e, h), h != 0);
-  if (bucket) pair::store(reinterpret_cast<Fb*>(bucket_sum), bucket[s], h, acc);
-  else pair::store(reinterpret_cast<Fb*>(out), t, h, acc);
+  typename Ar::A acc = Ar::load(src, e0, h);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = Ar::add(acc, Ar::load(src, e, h), h != 0);
+  if (bucket) Ar::store(reinterpret_cast<Fb*>(bucket_sum), bucket[s], h, acc);
+  else Ar::store(reinterpret_cast<Fb*>(out), t, h, acc);
 }
 
-template <class Curve>
+template <class Curve, class Ar = FipsPairArith<Curve>>
 __global__ __launch_bounds__(kBlock, 2) void window_segment_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                                      unsigned W, unsigned B, unsigned L,
                                                                      XYZZ<typename Curve::F>* __restrict__ out) {
-  using T = PairTypes<Curve>;
-  using Fb = typename T::Fb;
-  using H = typename T::H;
+  using Fb = typename Ar::Fb;
   const uint32_t h = threadIdx.x & 1u;
   const uint32_t S = B / L;
   const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
@@ -1281,22 +1332,20 @@ __global__ __launch_bounds__(kBlock, 2) void window_segment_pair_kernel(const XY
   const uint32_t w = t / S, j = t - w * S;
   const Fb* bs = reinterpret_cast<const Fb*>(bucket_sum);
   const size_t b0 = (size_t)w * B + (size_t)j * L;
-  pair::Acc<H> R = pair::zero<H>(h != 0), acc = R;
+  typename Ar::A R = Ar::zero(h != 0), acc = R;
   for (int k = (int)L - 1; k >= 0; --k) {
-    R = pair::add(R, pair::load<H>(bs, b0 + k, h), h != 0);
-    acc = pair::add(acc, R, h != 0);
+    R = Ar::add(R, Ar::load(bs, b0 + k, h), h != 0);
+    acc = Ar::add(acc, R, h != 0);
   }
-  acc = pair::add(acc, pair::small_mul(R, j * L, h != 0), h != 0);
-  pair::store(reinterpret_cast<Fb*>(out), t, h, acc);
+  acc = Ar::add(acc, Ar::small_mul(R, j * L, h != 0), h != 0);
+  Ar::store(reinterpret_cast<Fb*>(out), t, h, acc);
 }
 
-template <class Curve>
+template <class Curve, class Ar = FipsPairArith<Curve>>
 __global__ __launch_bounds__(kBlock, 2) void reduce_uniform_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                                      unsigned W, unsigned S_in, unsigned K2,
                                                                      XYZZ<typename Curve::F>* __restrict__ out) {
-  using T = PairTypes<Curve>;
-  using Fb = typename T::Fb;
-  using H = typename T::H;
+  using Fb = typename Ar::Fb;
   const uint32_t h = threadIdx.x & 1u;
   const uint32_t S_out = (S_in + K2 - 1) / K2;
   const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
@@ -1304,9 +1353,9 @@ __global__ __launch_bounds__(kBlock, 2) void reduce_uniform_pair_kernel(const XY
   const uint32_t w = t / S_out, q = t - w * S_out;
   const uint32_t e0 = q * K2, e1 = min(S_in, e0 + K2);
   const Fb* src = reinterpret_cast<const Fb*>(in) + (size_t)8 * w * S_in;
-  pair::Acc<H> acc = pair::load<H>(src, e0, h);
-  for (uint32_t e = e0 + 1; e < e1; ++e) acc = pair::add(acc, pair::load<H>(src, e, h), h != 0);
-  pair::store(reinterpret_cast<Fb*>(out), t, h, acc);
+  typename Ar::A acc = Ar::load(src, e0, h);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = Ar::add(acc, Ar::load(src, e, h), h != 0);
+  Ar::store(reinterpret_cast<Fb*>(out), t, h, acc);
 }
 
 // The BN254 G1 reductions over the 29-bit field (acc29::add / dbl; R-form
@@ -1371,7 +1420,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_tree29_kernel(const XYZZ<Bn2
   for (unsigned half = span >> 1; half >= 1; half >>= 1) {
     if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
     __syncthreads();
-    if (j < half) v = acc29::add(v, acc29::load_sh(sh, j));
+    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
     __syncthreads();
   }
   if (j == 0) acc29::store_pt(out, w, v);
@@ -1403,7 +1452,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_segtree29_kernel(const XYZZ<
   for (unsigned half = span >> 1; half >= 1; half >>= 1) {
     if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
     __syncthreads();
-    if (j < half) v = acc29::add(v, acc29::load_sh(sh, j));
+    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
     __syncthreads();
   }
   if (j == 0) acc29::store_pt(out, w, v);
@@ -1426,7 +1475,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_scan29_kernel(const XYZZ<Bn2
   for (unsigned d = 1; d < B; d <<= 1) {  // v = T_j
     acc29::store_raw(sh, j, v);
     __syncthreads();
-    if (j + d < B) v = acc29::add(v, acc29::load_sh(sh, j + d));
+    if (j + d < B) v = acc29::add(v, acc29::load_raw(sh, j + d));
     __syncthreads();
   }
   unsigned span = 1;
@@ -1434,7 +1483,7 @@ __global__ __launch_bounds__(kBlock, 2) void window_scan29_kernel(const XYZZ<Bn2
   for (unsigned half = span >> 1; half >= 1; half >>= 1) {
     if (j >= half && j < 2 * half) acc29::store_raw(sh, j - half, v);
     __syncthreads();
-    if (j < half) v = acc29::add(v, acc29::load_sh(sh, j));
+    if (j < half) v = acc29::add(v, acc29::load_raw(sh, j));
     __syncthreads();
   }
   if (j == 0) acc29::store_pt(out, w, v);
@@ -1954,9 +2003,16 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   auto* win_reduce = &reduce_uniform_kernel<Curve>;
   if constexpr (kG2) {
     if (pair_reduce) {
-      seg_reduce = &seg_reduce_pair_kernel<Curve>;
-      win_segment = &window_segment_pair_kernel<Curve>;
-      win_reduce = &reduce_uniform_pair_kernel<Curve>;
+      using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
+      if (pair_limb_ && !(variant_ & (1 << 22))) {  // the limb-field pair additions (bit 22: the FIPS pair)
+        seg_reduce = &seg_reduce_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        win_segment = &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        win_reduce = &reduce_uniform_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+      } else {
+        seg_reduce = &seg_reduce_pair_kernel<Curve>;
+        win_segment = &window_segment_pair_kernel<Curve>;
+        win_reduce = &reduce_uniform_pair_kernel<Curve>;
+      }
     }
   }
   // BN254 G1: the reductions over the 29-bit field with the 29-bit accumulation

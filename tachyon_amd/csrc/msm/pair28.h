@@ -144,4 +144,29 @@ __device__ __forceinline__ Acc dbl(const Acc& A, bool h) {
   return C;
 }
 
+// add-2008-s (point_xyzz_impl.h:45-97) for the G2 reductions, both operands
+// not the identity (the caller keeps identity flags); inputs and outputs
+// X < 10p, Y < 6p, ZZ, ZZZ < 3p (from32 loads give < 3p); *special as madd's
+// (tests/test_pair28_model.py point_add)
+__device__ __forceinline__ Acc add(const Acc& A, const Acc& B, bool h, int* special) {
+  const F28 U1 = pmul<kK4>(A.x, B.zz, h), S1 = pmul<kK4>(A.y, B.zzz, h);
+  const F28 P = pmul_add<kK4>(B.x, A.zz, ksub(kK4, U1), h);
+  const F28 R = pmul_add<kK4>(B.y, A.zzz, ksub(kK4, S1), h);
+  if (pzero(P)) {
+    *special = pzero(R) ? 2 : 1;
+    return A;
+  }
+  const F28 PP = psqr<kK16>(P, h);
+  const F28 PPP = pmul<kK4>(P, PP, h);
+  const F28 Q = pmul<kK4>(U1, PP, h);
+  const F28 W = pmul<kK4>(S1, PPP, h);
+  Acc C;
+  C.x = psqr_add<kK16>(R, ksub2(kK8, PPP, Q), h);
+  const F28 T = add_ksub(Q, kK16, C.x);
+  C.y = pmul_add<kK32r3>(R, T, ksub(kK4, W), h);
+  C.zz = pmul<kK4>(pmul<kK4>(A.zz, B.zz, h), PP, h);
+  C.zzz = pmul<kK4>(pmul<kK4>(A.zzz, B.zzz, h), PPP, h);
+  return C;
+}
+
 }  // namespace tachyon_amd::msm::pair28

@@ -231,3 +231,48 @@ def test_run_start_bounds():
         for c, want in ((x2[0], xv[0]), (x2[1], xv[1]), (y2[0], yv[0]), (y2[1], yv[1])):
             r = reduce(c)
             assert value(r) < 3 * P and value(r) * INV % P == want and all(x <= M28 for x in r[:N - 1])
+
+
+def point_add(A, B):
+    """add-2008-s for the G2 reductions (pair28.h add): inputs and outputs X <
+    10p, Y < 6p, ZZ, ZZZ < 3p (from32 loads give < 3p)"""
+    X1, Y1, ZZ1, ZZZ1 = A
+    X2, Y2, ZZ2, ZZZ2 = B
+    U1 = pmul(X1, ZZ2, G.K4)
+    S1 = pmul(Y1, ZZZ2, G.K4)
+    Pv = pmul(X2, ZZ1, G.K4, pksub(G.K4, U1))
+    R = pmul(Y2, ZZZ1, G.K4, pksub(G.K4, S1))
+    if is_zero(Pv[0]) and is_zero(Pv[1]):
+        return (2 if is_zero(R[0]) and is_zero(R[1]) else 1), A
+    PP = psqr(Pv, G.K16)
+    PPP = pmul(Pv, PP, G.K4)
+    Q = pmul(U1, PP, G.K4)
+    Wv = pmul(S1, PPP, G.K4)
+    X3 = psqr(R, G.K16, pksub2(G.K8, PPP, Q))
+    T = padd_ksub(Q, G.K16, X3)
+    Y3 = pmul(R, T, G.K32R3, pksub(G.K4, Wv))
+    return 0, (X3, Y3, pmul(pmul(ZZ1, ZZ2, G.K4), PP, G.K4), pmul(pmul(ZZZ1, ZZZ2, G.K4), PPP, G.K4))
+
+
+def add_ref(A, B):
+    X1, Y1, ZZ1, ZZZ1 = A
+    X2, Y2, ZZ2, ZZZ2 = B
+    U1, S1 = fm(X1, ZZ2), fm(Y1, ZZZ2)
+    Pv = fs(fm(X2, ZZ1), U1)
+    R = fs(fm(Y2, ZZZ1), S1)
+    PP = fm(Pv, Pv)
+    PPP = fm(Pv, PP)
+    Q = fm(U1, PP)
+    X3 = fs(fs(fm(R, R), PPP), fa(Q, Q))
+    Y3 = fs(fm(R, fs(Q, X3)), fm(S1, PPP))
+    return X3, Y3, fm(fm(ZZ1, ZZ2), PP), fm(fm(ZZZ1, ZZZ2), PPP)
+
+
+def test_pair28_add_at_bounds():
+    """the reductions' addition at the top of the invariant"""
+    rng = random.Random(14)
+    for _ in range(60):
+        A, B = rand_acc(rng), rand_acc(rng)
+        sp, out = point_add(A, B)
+        assert sp == 0
+        check_out(out, add_ref(tuple(f2(c) for c in A), tuple(f2(c) for c in B)))

@@ -305,3 +305,49 @@ def test_pair29_mutant_detected():
         assert failed
     finally:
         K33 = keep
+
+
+def point_add(A, B):
+    """add-2008-s for the G2 reductions (pair29.h add): inputs and outputs X <
+    10p, Y < 6p, ZZ, ZZZ < 3p (from32 loads give < 3p); R reduced before its
+    square, P squared as it is (5.4p, the 8p negation constant)"""
+    X1, Y1, ZZ1, ZZZ1 = A
+    X2, Y2, ZZ2, ZZZ2 = B
+    U1 = pmul(X1, ZZ2, K4)
+    S1 = pmul(Y1, ZZZ2, K4)
+    Pv = pmul(X2, ZZ1, K4, pksub(K4, U1))
+    R = pred(pmul(Y2, ZZZ1, K4, pksub(K4, S1)))
+    if is_zero(Pv[0]) and is_zero(Pv[1]):
+        return (2 if is_zero(R[0]) and is_zero(R[1]) else 1), A
+    PP = psqr(Pv, K8)
+    PPP = pmul(Pv, PP, K4)
+    Q = pmul(U1, PP, K4)
+    Wv = pmul(S1, PPP, K4)
+    X3 = psqr(R, K4, pksub2(K8, PPP, Q))
+    T = padd_ksub(Q, K16, X3)
+    Y3 = pmul(R, T, K32R3, pksub(K4, Wv))
+    return 0, (X3, Y3, pmul(pmul(ZZ1, ZZ2, K4), PP, K4), pmul(pmul(ZZZ1, ZZZ2, K4), PPP, K4))
+
+
+def add_ref(A, B):
+    X1, Y1, ZZ1, ZZZ1 = A
+    X2, Y2, ZZ2, ZZZ2 = B
+    U1, S1 = fm(X1, ZZ2), fm(Y1, ZZZ2)
+    Pv = fs(fm(X2, ZZ1), U1)
+    R = fs(fm(Y2, ZZZ1), S1)
+    PP = fm(Pv, Pv)
+    PPP = fm(Pv, PP)
+    Q = fm(U1, PP)
+    X3 = fs(fs(fm(R, R), PPP), fa(Q, Q))
+    Y3 = fs(fm(R, fs(Q, X3)), fm(S1, PPP))
+    return X3, Y3, fm(fm(ZZ1, ZZ2), PP), fm(fm(ZZZ1, ZZZ2), PPP)
+
+
+def test_pair29_add_at_bounds():
+    """the reductions' addition at the top of X < 10p, Y < 6p, ZZ, ZZZ < 3p"""
+    rng = random.Random(25)
+    for _ in range(60):
+        A, B = rand_acc(rng, OUT_BOUNDS), rand_acc(rng, OUT_BOUNDS)
+        sp, out = point_add(A, B)
+        assert sp == 0
+        check_out(out, add_ref(tuple(f2(c) for c in A), tuple(f2(c) for c in B)))

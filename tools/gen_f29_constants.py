@@ -31,8 +31,6 @@ def main():
     print(fmt("kK8", raised(8, 4), "8p, low limbs raised by 2^31 (>= 2^31 - 4)"))
     print(fmt("kK16", raised(16, 1), "16p, low limbs raised by 2^29"))
     print(fmt("kK33", raised(33, 1), "33p, low limbs raised by 2^29 (minus a normalized value < 32p)"))
-    print(fmt("kK16r4", raised(16, 4), "16p, low limbs raised by 2^31 (minus PPP + 2Q, limbs < 3 2^29)"))
-    print(fmt("kK32", raised(32, 1), "32p, low limbs raised by 2^29"))
     print(fmt("kK32r3", raised(32, 3), "32p, low limbs raised by 3 2^29"))
     one = (1 << 261) % P
     print(fmt("kOne29", limbs(one), "1 in R' = 2^261 form"))
