@@ -260,10 +260,12 @@ TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_set_varia
  * devices (ids may repeat: logical devices sharing a GPU) -- part g on ids[g],
  * the all-to-all as peer copies over xGMI, input and output in natural order
  * on the device the domain was created on (transform_device: a buffer there).
- * count must be a power of two with 2^floor(log n / 2) >= count; count <= 1
- * restores the single device.  Returns 1, or 0 (nothing changed) for a bad
- * count or id, or when the generator set active now differs from the
- * domain's (the plans would use another root).  Same results as one device. */
+ * The four-step splits by a power of two: the first 2^k ids are used, the
+ * largest 2^k <= count with 2^k <= 2^floor(log n / 2) (_devices reports
+ * them); count <= 1 restores the single device.  Returns 1, or 0 (nothing
+ * changed) for a bad id, a domain too small for two parts, or when the
+ * generator set active now differs from the domain's (the plans would use
+ * another root).  Same results as one device. */
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices(
     tachyon_bn254_univariate_evaluation_domain* domain, const int* ids, size_t count);
 /* the device list of set_devices (0 = single device); writes up to cap ids */

@@ -840,7 +840,16 @@ int tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices(tachyon_bn254_
   }
   const size_t n = d->impl->size();
   if (n < 4) return 0;
-  const std::vector<int> dev(ids, ids + count);
+  int avail = 0;
+  TA_HIP(hipGetDeviceCount(&avail));
+  for (size_t i = 0; i < count; ++i)
+    if (ids[i] < 0 || ids[i] >= avail) return 0;
+  // the four-step splits R and C by a power of two: the first 2^k of the ids,
+  // 2^k <= count and <= R = 2^floor(log n / 2) (devices() reports them)
+  size_t use = 1;
+  while (use * 2 <= count && use * 2 <= (size_t(1) << (d->impl->log_size() / 2))) use *= 2;
+  if (use < 2) return 0;
+  const std::vector<int> dev(ids, ids + use);
   std::unique_ptr<ntt::NttMultiDevice<Bn254Fr>> m;
   try {
     m = std::make_unique<ntt::NttMultiDevice<Bn254Fr>>(d->impl->log_size(), dev, d->device, d->impl->stream());

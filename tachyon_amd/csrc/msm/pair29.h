@@ -153,7 +153,9 @@ __device__ __forceinline__ Acc dbl(const Acc& A, bool h) {
 // square, P squared as it is with the 8p negation constant; *special as madd's
 // (tests/test_pair29_model.py point_add)
 __device__ __forceinline__ Acc add(const Acc& A, const Acc& B, bool h, int* special) {
+  // ZZ1 ZZ2 and ZZZ1 ZZZ2 first: the operands' Z coordinates die early (register pressure)
   const F29 U1 = pmul<kK4>(A.x, B.zz, h), S1 = pmul<kK4>(A.y, B.zzz, h);
+  const F29 ZZ12 = pmul<kK4>(A.zz, B.zz, h), ZZZ12 = pmul<kK4>(A.zzz, B.zzz, h);
   const F29 P = pmul_add<kK4>(B.x, A.zz, ksub(kK4, U1), h);
   const F29 R = reduce_shl5(pmul_add<kK4>(B.y, A.zzz, ksub(kK4, S1), h));
   if (pzero(P)) {
@@ -168,8 +170,8 @@ __device__ __forceinline__ Acc add(const Acc& A, const Acc& B, bool h, int* spec
   C.x = psqr_add<kK4>(R, ksub2(kK8, PPP, Q), h);
   const F29 T = add_ksub(Q, kK16, C.x);
   C.y = pmul_add<kK32r3>(R, T, ksub(kK4, W), h);
-  C.zz = pmul<kK4>(pmul<kK4>(A.zz, B.zz, h), PP, h);
-  C.zzz = pmul<kK4>(pmul<kK4>(A.zzz, B.zzz, h), PPP, h);
+  C.zz = pmul<kK4>(ZZ12, PP, h);
+  C.zzz = pmul<kK4>(ZZZ12, PPP, h);
   return C;
 }
 

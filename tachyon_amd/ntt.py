@@ -153,8 +153,9 @@ class Radix2EvaluationDomain:
 
     def set_devices(self, device_ids):
         """Run later transforms of the plain domain as a four-step NTT over these
-        devices, one process (ids may repeat; a power of two of them; [] or one
-        id = single device) -- tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices."""
+        devices, one process (ids may repeat; the first 2^k of them are used,
+        see devices(); [] or one id = single device) --
+        tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices."""
         ids = list(device_ids)
         arr = (ctypes.c_int * max(1, len(ids)))(*ids)
         if not lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices(self._d, arr, len(ids)):

@@ -218,7 +218,7 @@ def test_field29_extreme_inputs():
 
 
 @pytest.mark.parametrize("log_n,devices", [(4, [0, 0]), (10, [0, 0]), (13, [0, 0, 0, 0]), (16, [0] * 8),
-                                           (20, [0, 0])])
+                                           (20, [0, 0]), (11, [0, 0, 0])])
 def test_multi_device_domain_logical(log_n, devices):
     """One process, several devices (set_devices): the plain domain's fft / ifft,
     transform_host and transform_device run the four-step over `devices`
@@ -230,7 +230,8 @@ def test_multi_device_domain_logical(log_n, devices):
     coeffs = O.gen_scalars("bn254_fr", 3000 + log_n, n).tobytes()
     d = domain(n)
     d.set_devices(devices)
-    assert d.devices() == devices
+    used = 1 << (len(devices).bit_length() - 1)  # the first 2^k ids
+    assert d.devices() == devices[:used]
     ev = d.fft(coeffs)
     assert ev == O.fft(coeffs, n)
     assert d.ifft(ev) == O.ifft(ev, n)
@@ -258,13 +259,21 @@ def test_multi_device_domain_logical(log_n, devices):
 
 
 def test_multi_device_domain_refused():
-    """Device lists the four-step cannot take leave the domain unchanged: not a
-    power of two, more devices than R = 2^floor(log n / 2), a bad id."""
+    """Device lists the four-step cannot take leave the domain unchanged (a bad
+    id, a domain too small for two parts); more devices than R = 2^floor(log n
+    / 2) use the first R of them."""
     d = domain(1 << 10)
-    for bad in ([0, 0, 0], [0] * 64, [0, 99], [-1, 0]):
+    for bad in ([0, 99], [-1, 0]):
         with pytest.raises(ValueError):
             d.set_devices(bad)
         assert d.devices() == []
+    d.set_devices([0] * 64)
+    assert d.devices() == [0] * 32
+    d.set_devices([])
+    tiny = domain(2)
+    with pytest.raises(ValueError):
+        tiny.set_devices([0, 0])
+    tiny.close()
     coeffs = O.gen_scalars("bn254_fr", 77, 1 << 10).tobytes()
     assert d.fft(coeffs) == O.fft(coeffs, 1 << 10)
     d.close()
