@@ -109,7 +109,6 @@ class Groth16Prover {
   std::unique_ptr<ntt::NttDomain<Fr>> dom_, coset_;
   std::unique_ptr<msm::MsmGpu<G1>> msm1_;
   std::unique_ptr<msm::MsmGpu<G2>> msm2_;
-  std::unique_ptr<msm::MsmGpu<G1>> msm1b_;  // TACHYON_G16_LH_STREAM: the l + h MSM on its own stream
   DeviceBuffer a1_, b1_, lh1_, b2_;              // query points (lh1 = C1 | H1)
   DeviceBuffer lh_;                              // scalars of the merged MSM: witness | h
   DeviceBuffer row_a_, row_b_, col_, val_;       // CSR of the A and B matrices

@@ -4,7 +4,6 @@
 
 #include <algorithm>
 #include <chrono>
-#include <cstdlib>
 #include <exception>
 #include <thread>
 
@@ -233,10 +232,6 @@ void Groth16Prover<G1, G2>::init_device_state() {
   coset_->set_offset(ntt::root_of_unity<Fr>(log_n + 1));
   msm1_ = std::make_unique<msm::MsmGpu<G1>>(stream_);
   msm2_ = std::make_unique<msm::MsmGpu<G2>>(nullptr);  // own stream: runs beside the G1 MSMs
-  // TACHYON_G16_LH_STREAM=1: the merged witness + h MSM on a third stream and
-  // host thread beside the A MSM (A/B knob; DESIGN.md Groth16)
-  const char* e = getenv("TACHYON_G16_LH_STREAM");
-  if (e && e[0] == '1') msm1b_ = std::make_unique<msm::MsmGpu<G1>>(nullptr);
 }
 
 // A copy of `src` (on device src_device) on the current device: the device-
@@ -321,7 +316,6 @@ Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(
 template <class G1, class G2>
 Groth16Prover<G1, G2>::~Groth16Prover() {
   msm1_.reset();
-  msm1b_.reset();
   msm2_.reset();
   dom_.reset();
   coset_.reset();
@@ -412,28 +406,13 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   if (nw)
     TA_HIP(hipMemcpyAsync(d_lh, d_full + key_.num_instance(), nw * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
   witness_map(d_full, d_lh + nw);
-  if (profile_ || msm1b_) {
+  if (profile_) {
     TA_HIP(hipStreamSynchronize(stream_));
     timings_.qap = ms_since(t1);
   }
-  size_t lh_lo = 0;
-  const size_t lh_len = shard(nw + n_, &lh_lo);
-  // the merged witness (l) + h MSM on its own stream and thread when msm1b_ exists
-  std::exception_ptr lh_error;
-  std::thread lh_thread;
-  if (msm1b_) {
-    lh_thread = std::thread([&] {
-      try {
-        TA_HIP(hipSetDevice(device));
-        auto tl = Clock::now();
-        out.lh = lh_len ? msm1b_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
-        timings_.msm_l = ms_since(tl);
-      } catch (...) {
-        lh_error = std::current_exception();
-      }
-    });
-  }
-  Joiner lh_joiner{lh_thread};
+  // (The l + h MSM on a third stream and host thread beside the A MSM was
+  // measured: 12.23-12.37 vs 11.95-12.20 ms per 2^20 proof -- the GPU is
+  // already full with the G2 MSM beside the G1 ones.)
   auto t2 = Clock::now();
   out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
   timings_.msm_a = ms_since(t2);
@@ -443,16 +422,13 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   t2 = Clock::now();
   // witness (l) and h MSMs merged; h_coefficients.size() == h_g1_query.size()
   // == domain size: the else branch of prove.h:103-112
-  if (!msm1b_) {
-    out.lh = lh_len ? msm1_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
-    timings_.msm_l = ms_since(t2);
-  } else {
-    lh_thread.join();
-  }
+  size_t lh_lo = 0;
+  const size_t lh_len = shard(nw + n_, &lh_lo);
+  out.lh = lh_len ? msm1_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
+  timings_.msm_l = ms_since(t2);
   timings_.msm_h = 0;
   g2_thread.join();
   if (g2_error) std::rethrow_exception(g2_error);
-  if (lh_error) std::rethrow_exception(lh_error);
   out.b2 = acc_b2;
   timings_.total = ms_since(t0);
   return out;
