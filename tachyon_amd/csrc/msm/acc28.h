@@ -49,6 +49,34 @@ TA_HD Acc madd(const Acc& A, const F28& x2, const F28& y2, int* special) {
   return C;
 }
 
+// The bucket-sum reductions over the same field: add-2008-s
+// (point_xyzz_impl.h:45-97), both operands not the identity, invariant X <
+// 10p, Y, ZZ, ZZZ < 3p (from32 gives < 3p); *special as madd's:
+//   U1 = X1 ZZ2, S1 = Y1 ZZZ2 < 1.02   P = X2 ZZ1 + (4p - U1) < 5.02
+//   R = Y2 ZZZ1 + (4p - S1) < 5.01     PP < 1.02  PPP, Q < 1.003
+//   X3 = R^2 + (8p - PPP - 2Q) < 9.02  Y3 = R T + (4p - S1) PPP < 1.04
+//   ZZ3 = (ZZ1 ZZ2) PP, ZZZ3 < 1.002
+TA_HD Acc add(const Acc& A, const Acc& B, int* special) {
+  const F28 U1 = mul(A.x, B.zz), S1 = mul(A.y, B.zzz);
+  const F28 ZZ12 = mul(A.zz, B.zz), ZZZ12 = mul(A.zzz, B.zzz);
+  const F28 P = mul_add(B.x, A.zz, ksub(kK4, U1));
+  const F28 R = mul_add(B.y, A.zzz, ksub(kK4, S1));
+  if (is_zero_mod_p(P)) {
+    *special = is_zero_mod_p(R) ? 2 : 1;
+    return A;
+  }
+  const F28 PP = sqr(P);
+  const F28 PPP = mul(P, PP);
+  const F28 Q = mul(U1, PP);
+  Acc C;
+  C.x = sqr_add(R, ksub2(kK8, PPP, Q));
+  const F28 T = add_ksub(Q, kK16, C.x);
+  C.y = mul2_add(R, T, ksub(kK4, S1), PPP);
+  C.zz = mul(ZZ12, PP);
+  C.zzz = mul(ZZZ12, PPP);
+  return C;
+}
+
 // dbl-2008-s-1 (a = 0; point_xyzz_impl.h:199-236) under the same invariant:
 //   U = 2 Y1 < 6   V = U^2 < 1.02   W = U V < 1.003   S = X1 V < 1.005
 //   M = X1 (3 X1) < 1.12

@@ -1161,10 +1161,67 @@ __device__ __forceinline__ uint32_t find_segment(const uint32_t* __restrict__ of
   return lo;
 }
 
+// The arithmetic of the one-lane reductions: the FIPS field (XYZZ<HotFp>, the
+// arrays as they are) or a limb field (BLS12-381 G1 over 14 x 28-bit limbs,
+// msm/acc28.h) that converts the R-form arrays on load (from32, < 3p) and
+// store (to32), identities as flags.
+template <class Curve>
+struct FipsArith {
+  using F = typename HotOf<typename Curve::F>::type;  // inline products (same layout)
+  using A = XYZZ<F>;
+  static __device__ __forceinline__ A load(const XYZZ<typename Curve::F>* p, size_t i) {
+    return reinterpret_cast<const XYZZ<F>*>(p)[i];
+  }
+  static __device__ __forceinline__ void store(XYZZ<typename Curve::F>* p, size_t i, const A& a) {
+    reinterpret_cast<XYZZ<F>*>(p)[i] = a;
+  }
+  static __device__ __forceinline__ A add(const A& a, const A& b) { return a + b; }
+  static __device__ __forceinline__ A zero() { return A::zero(); }
+  static __device__ __forceinline__ A dbl(const A& a) { return a.dbl(); }
+  static __device__ __forceinline__ bool is_zero(const A& a) { return a.is_zero(); }
+};
+struct Limb28Arith {
+  using Fq = Bls381Fq;
+  struct A {
+    acc28_core::Acc a;
+    bool zero;
+  };
+  static __device__ __forceinline__ A load(const XYZZ<Fq>* p, size_t i) {
+    const XYZZ<Fq> q = p[i];
+    if (q.is_zero()) return {acc28_core::Acc{}, true};
+    return {{f28::from32(q.x.v), f28::from32(q.y.v), f28::from32(q.zz.v), f28::from32(q.zzz.v)}, false};
+  }
+  static __device__ __forceinline__ void store(XYZZ<Fq>* p, size_t i, const A& a) {
+    if (a.zero) {
+      p[i] = XYZZ<Fq>::zero();
+      return;
+    }
+    XYZZ<Fq> r;
+    f28::to32(a.a.x, r.x.v);
+    f28::to32(a.a.y, r.y.v);
+    f28::to32(a.a.zz, r.zz.v);
+    f28::to32(a.a.zzz, r.zzz.v);
+    p[i] = r;
+  }
+  static __device__ __forceinline__ A add(const A& a, const A& b) {
+    if (a.zero) return b;
+    if (b.zero) return a;
+    int special = 0;
+    const acc28_core::Acc s = acc28_core::add(a.a, b.a, &special);
+    if (special == 1) return {a.a, true};
+    return {special == 2 ? acc28_core::dbl(a.a) : s, false};
+  }
+  static __device__ __forceinline__ A zero() { return {acc28_core::Acc{}, true}; }
+  static __device__ __forceinline__ A dbl(const A& a) {  // (no point of this prime-order group doubles to the identity)
+    return a.zero ? a : A{acc28_core::dbl(a.a), false};
+  }
+  static __device__ __forceinline__ bool is_zero(const A& a) { return a.zero; }
+};
+
 // One K2-ary level of the segmented tree: output q of segment s is the sum of
 // in[beg[s] + q*K2 .. min(end[s], +K2)).  On the last level every segment has
 // one output, which goes to bucket_sum[bucket[s]].
-template <class Curve>
+template <class Curve, class Ar = FipsArith<Curve>>
 __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_reduce_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                             const uint32_t* __restrict__ beg,
                                                             const uint32_t* __restrict__ end,
@@ -1172,18 +1229,16 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void seg_reduce_ker
                                                             unsigned K2, XYZZ<typename Curve::F>* __restrict__ out,
                                                             const uint32_t* __restrict__ bucket,
                                                             XYZZ<typename Curve::F>* __restrict__ bucket_sum) {
-  using F = typename HotOf<typename Curve::F>::type;  // inline products (same layout)
-  const XYZZ<F>* hin = reinterpret_cast<const XYZZ<F>*>(in);
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= out_off[nseg]) return;
   uint32_t s = find_segment(out_off, nseg, t);
   uint32_t q = t - out_off[s];
   uint32_t e0 = beg[s] + q * K2;
   uint32_t e1 = min(end[s], e0 + K2);
-  XYZZ<F> acc = hin[e0];
-  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc + hin[e];
-  if (bucket) reinterpret_cast<XYZZ<F>*>(bucket_sum)[bucket[s]] = acc;
-  else reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
+  typename Ar::A acc = Ar::load(in, e0);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = Ar::add(acc, Ar::load(in, e));
+  if (bucket) Ar::store(bucket_sum, bucket[s], acc);
+  else Ar::store(out, t, acc);
 }
 
 // m * P for a small non-negative integer m (double-and-add, high bit first)
@@ -1199,29 +1254,38 @@ __device__ XYZZ<F> small_mul(const XYZZ<F>& P, uint32_t m) {
   }
   return r;
 }
+template <class Ar>
+__device__ typename Ar::A small_mul_ar(const typename Ar::A& P, uint32_t m) {
+  if (m == 0 || Ar::is_zero(P)) return Ar::zero();
+  typename Ar::A r = P;
+  for (int bit = 30 - __builtin_clz(m); bit >= 0; --bit) {
+    r = Ar::dbl(r);
+    if ((m >> bit) & 1) r = Ar::add(r, P);
+  }
+  return r;
+}
 
 // Window reduction, stage 1: segment j of window w covers buckets
 // [j*L, (j+1)*L) (bucket b holds |digit| = b+1).  Running sums from the top
 // give S = sum (b - jL + 1) B_b and R = sum B_b; the segment's share of
 // sum_b (b+1) B_b is S + jL * R  (PippengerBase::AccumulateBuckets,
 // pippenger_base.h:36-57, split across threads).
-template <class Curve>
+template <class Curve, class Ar = FipsArith<Curve>>
 __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_segment_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                                 unsigned W, unsigned B, unsigned L,
                                                                 XYZZ<typename Curve::F>* __restrict__ out) {
-  using F = typename HotOf<typename Curve::F>::type;
   uint32_t S = B / L;
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= W * S) return;
   uint32_t w = t / S, j = t - w * S;
-  const XYZZ<F>* bs = reinterpret_cast<const XYZZ<F>*>(bucket_sum) + (size_t)w * B + (size_t)j * L;
-  XYZZ<F> R = XYZZ<F>::zero(), acc = XYZZ<F>::zero();
+  const size_t b0 = (size_t)w * B + (size_t)j * L;
+  typename Ar::A R = Ar::zero(), acc = Ar::zero();
   for (int k = (int)L - 1; k >= 0; --k) {
-    R = R + bs[k];
-    acc = acc + R;
+    R = Ar::add(R, Ar::load(bucket_sum, b0 + k));
+    acc = Ar::add(acc, R);
   }
-  acc = acc + small_mul(R, j * L);
-  reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
+  acc = Ar::add(acc, small_mul_ar<Ar>(R, j * L));
+  Ar::store(out, t, acc);
 }
 
 // The G2 reductions with a lane pair per point (acc_pair.h): the one-lane
@@ -1504,20 +1568,19 @@ __global__ __launch_bounds__(kBlock, 2) void reduce_uniform29_kernel(const XYZZ<
 }
 
 // Window reduction, stage 2: sum K2 consecutive segment sums per window.
-template <class Curve>
+template <class Curve, class Ar = FipsArith<Curve>>
 __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void reduce_uniform_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                                 unsigned W, unsigned S_in, unsigned K2,
                                                                 XYZZ<typename Curve::F>* __restrict__ out) {
-  using F = typename HotOf<typename Curve::F>::type;
   uint32_t S_out = (S_in + K2 - 1) / K2;
   uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   if (t >= W * S_out) return;
   uint32_t w = t / S_out, q = t - w * S_out;
   uint32_t e0 = q * K2, e1 = min(S_in, e0 + K2);
-  const XYZZ<F>* src = reinterpret_cast<const XYZZ<F>*>(in) + (size_t)w * S_in;
-  XYZZ<F> acc = src[e0];
-  for (uint32_t e = e0 + 1; e < e1; ++e) acc = acc + src[e];
-  reinterpret_cast<XYZZ<F>*>(out)[t] = acc;
+  const XYZZ<typename Curve::F>* src = in + (size_t)w * S_in;
+  typename Ar::A acc = Ar::load(src, e0);
+  for (uint32_t e = e0 + 1; e < e1; ++e) acc = Ar::add(acc, Ar::load(src, e));
+  Ar::store(out, t, acc);
 }
 
 // Window reduction by workgroup trees (no per-segment (jL)*R fix-up, two
@@ -2013,6 +2076,15 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
         win_segment = &window_segment_pair_kernel<Curve>;
         win_reduce = &reduce_uniform_pair_kernel<Curve>;
       }
+    }
+  }
+  // BLS12-381 G1: the reductions over the 28-bit field with the 28-bit accumulation
+  // (set_variant bit 22: the FIPS reductions)
+  if constexpr (std::is_same_v<Curve, Bls381G1>) {
+    if (acc28_ && !(variant_ & (1 << 22))) {
+      seg_reduce = &seg_reduce_kernel<Curve, Limb28Arith>;
+      win_segment = &window_segment_kernel<Curve, Limb28Arith>;
+      win_reduce = &reduce_uniform_kernel<Curve, Limb28Arith>;
     }
   }
   // BN254 G1: the reductions over the 29-bit field with the 29-bit accumulation

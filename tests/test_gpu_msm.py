@@ -421,15 +421,18 @@ def _neg_point(curve, p: bytes) -> bytes:
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("curve,variant", [("bn254_g1", 0), ("bn254_g1", 262144), ("bn254_g2", 0),
-                                           ("bls12_381_g1", 0), ("bls12_381_g2", 0), ("bls12_381_g2", 32768)])
+                                           ("bn254_g2", 1 << 22), ("bls12_381_g1", 0), ("bls12_381_g1", 1 << 22),
+                                           ("bls12_381_g2", 0), ("bls12_381_g2", 1 << 22),
+                                           ("bls12_381_g2", 32768)])
 def test_msm_reduction_edge_cases(curve, variant):
     """Inputs that drive the chain join and the window sums through their
     special cases: every base the same point (equal bucket pieces and equal
     running sums -> the doubling branch of the reduction additions), bases
     alternating P, -P under one repeated scalar (pieces and bucket sums that
     cancel -> the identity branch), and one repeated base and scalar.
-    Default schedule (29-bit reductions on BN254 G1, lane-pair reductions on
-    G2) and the FIPS / one-lane ones (bits 18 / 15)."""
+    Default schedule (29-bit reductions on BN254 G1, 28-bit on BLS12-381 G1,
+    limb-field lane-pair reductions on G2) and the FIPS / FIPS-pair /
+    one-lane ones (bits 18 / 22 / 15)."""
     pb, fr = O.CURVE_INFO[curve]
     n = 1 << 13
     g = O.gen_bases(curve, 31, 1, 1).tobytes()
