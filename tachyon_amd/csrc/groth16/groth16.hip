@@ -410,8 +410,9 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     TA_HIP(hipStreamSynchronize(stream_));
     timings_.qap = ms_since(t1);
   }
-  // (The l + h MSM on a third stream and host thread beside the A MSM was
-  // measured: 12.23-12.37 vs 11.95-12.20 ms per 2^20 proof -- the GPU is
+  // (Measured and dropped: the l + h MSM on a third stream and host thread
+  // beside the A MSM, 12.23-12.37 vs 11.95-12.20 ms per 2^20 proof, and the A
+  // MSM after B2 on the G2 stream, 12.34-13.13 vs 11.81-12.09 -- the GPU is
   // already full with the G2 MSM beside the G1 ones.)
   auto t2 = Clock::now();
   out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();

@@ -60,18 +60,24 @@ struct MsmPlan {
 // latency of the bucket/window reduction sets a ~1 ms floor, which favours
 // few windows.  Table = fastest c of the BN254 G1 sweeps on MI355X
 // (tools/tune_msm.py); only c with a distinct window count
-// (W = ceil(255/c)) are candidates.
-inline unsigned default_window_bits(unsigned lg) {
+// (W = ceil(255/c)) are candidates.  For another scalar width a c whose
+// window count c - 1 also gives is one bit of buckets too many: BLS12-381's
+// 255-bit Fr has W = 16 at c = 16 and at c = 17, and c = 16 measured faster at
+// 2^22 / 2^23 (G1 12.8 vs 14.1 / 23.4 vs 25.5 ms, G2 31.7 vs 34.5 / 60.3 vs
+// 64.1; profiles/r04b/tune_bls_*.log).
+inline unsigned default_window_bits(unsigned lg, unsigned scalar_bits = 254) {
   static constexpr unsigned kBest[] = {8, 10, 13, 15, 16, 16, 17, 17, 20, 20, 20};  // lg = 16 .. 26
-  if (lg < 16) return (unsigned)std::max<int>(4, (int)lg - 7);
-  return kBest[std::min<unsigned>(lg, 26) - 16];
+  unsigned c = lg < 16 ? (unsigned)std::max<int>(4, (int)lg - 7) : kBest[std::min<unsigned>(lg, 26) - 16];
+  const unsigned d = scalar_bits + 1;  // signed digits: W c >= bits + 1
+  while (c > 4 && (d + c - 2) / (c - 1) == (d + c - 1) / c) --c;
+  return c;
 }
 
 inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, unsigned w_begin, unsigned w_end) {
   MsmPlan p;
   unsigned lg = 1;
   while ((size_t(1) << lg) < n) ++lg;
-  unsigned c = force_c ? force_c : default_window_bits(lg);
+  unsigned c = force_c ? force_c : default_window_bits(lg, scalar_bits);
   p.c = c;
   p.windows = (scalar_bits + 1 + c - 1) / c;  // W*c >= bits+1
   p.buckets = 1u << (c - 1);
