@@ -365,8 +365,10 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_last_timings(int curve, const void*
 TACHYON_C_EXPORT size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const void* ctx);
 /* Schedule of the last run (of its last point chunk): bit 0 the recode fused
  * with the first radix pass, bit 1 onesweep passes fed by the recode's digit
- * counts, bit 2 7-byte LDS staging in the recode scatter, bit 3 the BN254 G1
- * accumulation over the 29-bit-limb field, bit 4 the lane-pair G2 accumulation. */
+ * counts, bit 2 7-byte LDS staging in the recode scatter, bit 3 an
+ * accumulation over the 29-bit-limb field (BN254 G1; BN254 G2's lane pair),
+ * bit 4 the lane-pair G2 accumulation, bit 5 over the 28-bit-limb field
+ * (BLS12-381 G1 / G2), bit 6 the chain-flag debug check ran. */
 TACHYON_C_EXPORT unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx);
 /* Diagnostic: mixed additions per second (G/s) of the curve's bucket
  * accumulation field code in registers on the current device (no gathers, no

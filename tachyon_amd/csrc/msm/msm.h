@@ -98,8 +98,13 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, u
   // 2^21 4.72/4.71/4.66, 2^22 8.14/8.10/8.24; one box, K = 128 vs 64: 2^20
   // 2.88 (K 64) vs 2.94 (K 32), 2^22 8.87 vs 8.57, 2^23 15.56 vs 15.77;
   // 2^26: K = 128/256/512/1024 -> 99.9/98.9/99.1/99.3)
+  // Round 4 (29-bit and limb-pair reductions): twice that K for 2^22 < entries
+  // <= 2^25 -- 2^18 1.19 -> 1.17, 2^19 1.53 -> 1.48, 2^21 3.82 -> 3.62 ms, 2^20
+  // even, 2^22 and up slower (profiles/r04b/tune_k_bn254_g1_2_18_25.log)
   size_t k = entries >= (size_t(1) << 29)   ? 256
              : entries >= (size_t(1) << 26) ? 128
+             : entries > (size_t(1) << 25)  ? std::clamp<size_t>(entries >> 18, 16, 64)
+             : entries > (size_t(1) << 22)  ? std::clamp<size_t>(entries >> 17, 32, 128)
                                             : std::clamp<size_t>(entries >> 18, 16, 64);
   if (p.group == 1) k = n >> 18;  // ~1024 workgroups per window launch
   p.K = (unsigned)std::clamp<size_t>(k, 8, 256);
