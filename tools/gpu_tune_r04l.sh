@@ -8,5 +8,5 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 timeout -k 10 300 python tools/tune_msm.py --curve bn254_g1 --log-n 16 17 18 19 20 21 22 --rounds 2 > gpurun_out/krule_g1.log 2>&1 &&
 timeout -k 10 300 python tools/tune_msm.py --curve bn254_g2 --log-n 20 21 --rounds 2 > gpurun_out/krule_g2.log 2>&1 &&
 timeout -k 10 300 python tools/tune_msm.py --curve bls12_381_g1 --log-n 20 21 --rounds 2 > gpurun_out/krule_bls.log 2>&1 &&
-timeout -k 10 500 python tools/tune_msm.py --curve bn254_g1 --log-n 24 26 --variants 0 16 32 48 256 512 768 --rounds 2 \
+timeout -k 10 500 python tools/tune_msm.py --curve bn254_g1 --log-n 24 26 --variants 0 16 32 48 256 512 768 8388608 --rounds 2 \
   > gpurun_out/tune_sort_recode.log 2>&1
