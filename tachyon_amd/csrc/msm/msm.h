@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0xFFFFBF;  // bits 0-23 except 6 (21: a debug check, not a schedule)
+constexpr int kMsmVariantMask = 0x7FFFBF;  // bits 0-22 except 6 (21: a debug check, not a schedule)
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
@@ -182,12 +182,11 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-20, 22 -- the FIPS reductions instead of the
-  // limb-field ones -- and 23 -- BN254 G1's accumulation at 4 waves per SIMD;
-  // see run_windows) and bit 21, a debug
+  // A/B tuning knobs (bits 0-5, 7-20 and 22 -- the FIPS reductions instead of
+  // the limb-field ones; see run_windows) and bit 21, a debug
   // check (the small-MSM chain flags vs the accumulation's).  Every variant
   // computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 23 are refused.
+  // experiment) and anything above bit 22 are refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;
@@ -234,7 +233,7 @@ class MsmGpu {
   bool wide_stage_ = false;    // 8-byte entries in the recode scatter's LDS staging (bit 11)
   bool tree_reduce_ = false;   // window sums by workgroup trees (bit 12)
   bool acc29_ = false;         // BN254 G1 accumulation over 29-bit limbs (default; bit 18: FIPS 32-bit)
-  int acc29_mode_ = 0;         // ... next base: 0 not prefetched, 1 in registers (bit 13), 2 via LDS-DMA (bit 17), 3 as 0 at 4 waves (bit 23)
+  int acc29_mode_ = 0;         // ... next base: 0 not prefetched, 1 in registers (bit 13), 2 via LDS-DMA (bit 17)
   bool pair_acc_ = false;      // G2 accumulation with a lane pair per point (bit 15)
   bool acc28_ = false;         // BLS12-381 G1 accumulation over 28-bit limbs (default; bit 20: FIPS 32-bit)
   bool pair_limb_ = false;     // G2 lane pair over 28-bit (BLS12-381) / 29-bit (BN254) limbs (default; bit 20: FIPS pair)

@@ -676,9 +676,10 @@ __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>
 }
 
 
-// kPrefetch 3: as 0 at 4 waves per SIMD (<= 128 VGPRs; set_variant bit 23, A/B)
+// (4 waves per SIMD -- <= 128 VGPRs, 14 spilled -- measured slower at 2^26:
+// 76.1-76.4 vs 75.0-75.5 ms, profiles/r04b/tune_sort_tiles_recode_spt_4waves_2_24_26.log)
 template <int kPrefetch, bool kRaw>
-__global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : kPrefetch == 3 ? 4 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
+__global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
                                                            const uint64_t* __restrict__ ents, uint32_t c,
                                                            uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
                                                            uint32_t idx_mask, XYZZ<Bn254Fq>* __restrict__ bucket_sum,
@@ -2004,8 +2005,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
       if (acc29_) last_schedule_ |= kSchedAcc29;
       if (acc29_)  // 29-bit-limb accumulation (BN254 G1 default; set_variant bits 13 / 17: base prefetch A/B)
-        hipLaunchKernelGGL(acc29_mode_ == 3   ? (raw ? seg_acc29_kernel<3, true> : seg_acc29_kernel<3, false>)
-                           : acc29_mode_ == 2 ? (raw ? seg_acc29_kernel<2, true> : seg_acc29_kernel<2, false>)
+        hipLaunchKernelGGL(acc29_mode_ == 2 ? (raw ? seg_acc29_kernel<2, true> : seg_acc29_kernel<2, false>)
                            : acc29_mode_ == 1 ? (raw ? seg_acc29_kernel<1, true> : seg_acc29_kernel<1, false>)
                                               : (raw ? seg_acc29_kernel<0, true> : seg_acc29_kernel<0, false>),
                            dim3(grid_for(Tg)),
@@ -2298,7 +2298,7 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   // (2 waves) / through LDS by LDS-DMA (A/B); bit 14 is the default
   const bool acc29_default = std::is_same_v<Curve, Bn254G1>;
   acc29_ = !(variant_ & 262144) && ((variant_ & (8192 | 16384 | 131072)) != 0 || acc29_default);
-  acc29_mode_ = (variant_ & (1 << 23)) ? 3 : (variant_ & 131072) ? 2 : (variant_ & 8192) ? 1 : 0;
+  acc29_mode_ = (variant_ & 131072) ? 2 : (variant_ & 8192) ? 1 : 0;
   // BLS12-381 G1: the accumulation over 14 x 28-bit limbs (field/f28.h) by
   // default; bit 20 restores the 12 x 32-bit FIPS field (A/B)
   acc28_ = std::is_same_v<Curve, Bls381G1> && !(variant_ & (1 << 20));
