@@ -248,10 +248,11 @@ TACHYON_C_EXPORT void* tachyon_mi355x_bn254_univariate_evaluation_domain_stream(
  * returns the number of passes written. */
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(
     tachyon_bn254_univariate_evaluation_domain* domain, int on);
-/* A/B kernel variant of the domain's transforms (no reference counterpart):
- * 0 = the default 8 x 32-bit-limb passes, 1 = the 9 x 29-bit-limb passes,
- * 3 = the 29-bit passes with XOR-swizzled LDS positions.  All compute the same
- * canonical outputs.  Returns 0 (nothing changed) for other values. */
+/* Kernel variant of the domain's transforms (no reference counterpart):
+ * 0 = the 8 x 32-bit-limb passes, 1 = the 9 x 29-bit-limb passes, 3 = the
+ * 29-bit passes with XOR-swizzled LDS positions; a new domain uses 1 up to
+ * 2^20 elements and 0 above (the faster of the two at each size).  All compute
+ * the same canonical outputs.  Returns 0 (nothing changed) for other values. */
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(
     tachyon_bn254_univariate_evaluation_domain* domain, int variant);
 /* One process, several GPUs: later transforms of the plain domain (offset 1;

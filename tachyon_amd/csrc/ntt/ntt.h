@@ -65,11 +65,12 @@ class NttDomain {
 
   void set_profile(bool on) { profile_ = on; }
   const NttTimings& timings() const { return timings_; }
-  // A/B kernel variants (BN254 Fr): bit 0 = the 9 x 29-bit-limb passes
-  // (dif29_pass_kernel) instead of the default 8 x 32-bit ones (dif_pass_kernel;
-  // DESIGN.md NTT round 4: fewer instructions, the same time -- more
-  // multiplies per butterfly lower the clock); bit 1 (with bit 0) swizzles
-  // their LDS positions.  Unknown values (or any bit on other fields): refused.
+  // Kernel variants (BN254 Fr): bit 0 = the 9 x 29-bit-limb passes
+  // (dif29_pass_kernel), 0 = the 8 x 32-bit ones (dif_pass_kernel); the
+  // default is 1 up to 2^20 and 0 above (DESIGN.md NTT round 4: fewer
+  // instructions win while the clock holds, more multiplies per butterfly
+  // lower it at 2^22+); bit 1 (with bit 0) swizzles their LDS positions.
+  // Unknown values (or any bit on other fields): refused.
   bool set_variant(int v);
   int variant() const { return variant_; }
 
@@ -105,7 +106,7 @@ class NttDomain {
   // the first pass's stages [0, k0), Shoup entries for the later stages
   int variant_ = 0;
   bool tables32_ = false;  // the 32-bit Shoup tables (built with the domain)
-  bool tables29_ = false;  // the 29-bit tables (built on first use of variant bit 0)
+  bool tables29_ = false;  // the 29-bit tables (built with the domain up to 2^20, else on first use of bit 0)
   size_t split29_ = 0;     // = n - (n >> k0): stage-table entries before the Shoup part
   DeviceBuffer t29m_fwd_, t29m_inv_, t29s_fwd_, t29s_inv_, scratch29_;
   DeviceBuffer coset_lo_, coset_hi_, icoset_lo_, icoset_hi_;

@@ -610,6 +610,17 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
   ev_.resize(plan_.size() + 1);
   for (auto& e : ev_) TA_HIP(hipEventCreate(&e));
   build_twiddles();
+  // BN254 Fr up to 2^20: the 29-bit passes by default -- fewer instructions
+  // win while the clock holds (2^20 forward 0.126 -> 0.118 ms, inverse 0.133 ->
+  // 0.127); from 2^22 the 32-bit ones are faster (2^24 1.78 vs 1.88 ms
+  // forward; profiles/r04b/ntt_ab_32_vs_29_2_20_24.log).  set_variant(0)
+  // forces the 32-bit passes.
+  if constexpr (std::is_same_v<Fr, Bn254Fr>) {
+    if (log_n_ >= 1 && log_n_ <= 20) {
+      variant_ = 1;
+      build_tables29();
+    }
+  }
 }
 
 template <class Fr>

@@ -145,9 +145,10 @@ class Radix2EvaluationDomain:
         lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_profile(self._d, 1 if on else 0)
 
     def set_variant(self, variant: int):
-        """A/B kernel variant: 0 = the 8 x 32-bit-limb passes (default), 1 = the
-        9 x 29-bit-limb passes, 3 = the 29-bit passes with swizzled LDS
-        positions; all give the same canonical outputs."""
+        """Kernel variant: 0 = the 8 x 32-bit-limb passes, 1 = the 9 x 29-bit-limb
+        passes, 3 = the 29-bit passes with swizzled LDS positions (a new domain
+        uses 1 up to 2^20 elements, 0 above); all give the same canonical
+        outputs."""
         if not lib().tachyon_mi355x_bn254_univariate_evaluation_domain_set_variant(self._d, variant):
             raise ValueError(f"unknown NTT variant {variant}")
 
