@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0xFFFFBF;  // bits 0-23 except 6 (21: a debug check, not a schedule)
+constexpr int kMsmVariantMask = 0x7FFFBF;  // bits 0-22 except 6 (21: a debug check, not a schedule)
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
@@ -182,12 +182,11 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-20, 22 -- the FIPS reductions instead of
-  // the limb-field ones -- and 23 -- the G2 limb-pair window segments at one
-  // wave per SIMD; see run_windows) and bit 21, a debug
+  // A/B tuning knobs (bits 0-5, 7-20 and 22 -- the FIPS reductions instead of
+  // the limb-field ones; see run_windows) and bit 21, a debug
   // check (the small-MSM chain flags vs the accumulation's).  Every variant
   // computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 23 are refused.
+  // experiment) and anything above bit 22 are refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;

@@ -1386,8 +1386,11 @@ __global__ __launch_bounds__(kBlock, 2) void seg_reduce_pair_kernel(const XYZZ<t
   else Ar::store(reinterpret_cast<Fb*>(out), t, h, acc);
 }
 
-template <class Curve, class Ar = FipsPairArith<Curve>, int kWaves = 2>
-__global__ __launch_bounds__(kBlock, kWaves) void window_segment_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+// (BLS12-381's limb pair spills here at the two-wave cap; one wave per SIMD
+// without spills measured slower: reduction 14.1 -> 14.7 ms at 2^24,
+// profiles/r04b/ab_window_segment_one_wave_rejected.log)
+template <class Curve, class Ar = FipsPairArith<Curve>>
+__global__ __launch_bounds__(kBlock, 2) void window_segment_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                                      unsigned W, unsigned B, unsigned L,
                                                                      XYZZ<typename Curve::F>* __restrict__ out) {
   using Fb = typename Ar::Fb;
@@ -2071,10 +2074,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
       if (pair_limb_ && !(variant_ & (1 << 22))) {  // the limb-field pair additions (bit 22: the FIPS pair)
         seg_reduce = &seg_reduce_pair_kernel<Curve, LimbPairArith<LimbPol>>;
-        // (bit 23: the window segments at one wave per SIMD -- BLS12-381's
-        // limb pair spills at the two-wave cap of 256 VGPRs)
-        win_segment = (variant_ & (1 << 23)) ? &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol>, 1>
-                                             : &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        win_segment = &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol>>;
         win_reduce = &reduce_uniform_pair_kernel<Curve, LimbPairArith<LimbPol>>;
       } else {
         seg_reduce = &seg_reduce_pair_kernel<Curve>;

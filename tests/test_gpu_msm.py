@@ -63,7 +63,6 @@ def test_msm_golden_bn254_g1_variants(variant):
 
 @pytest.mark.parametrize("curve,variant", [("bn254_g2", 0), ("bn254_g2", 32768), ("bn254_g2", 1 << 20),
                                            ("bn254_g2", 1 << 22), ("bls12_381_g2", 1 << 22),
-                                           ("bn254_g2", 1 << 23), ("bls12_381_g2", 1 << 23),
                                            ("bls12_381_g2", 0),
                                            ("bls12_381_g2", 32768), ("bls12_381_g2", 65536 | (1 << 20)),
                                            ("bls12_381_g2", 1 << 20)])
@@ -376,7 +375,7 @@ def test_msm_schedule_variants_agree(curve, logn):
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
         for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384,
-                  32768, 65536, 131072, 262144, 524288, 1 << 20, (1 << 20) | 65536, 1 << 21, 1 << 22, 1 << 23):
+                  32768, 65536, 131072, 262144, 524288, 1 << 20, (1 << 20) | 65536, 1 << 21, 1 << 22):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
@@ -394,7 +393,7 @@ def test_msm_schedule_variants_agree(curve, logn):
                     assert s["acc28"] == limb, (hex(v), s)
                 else:  # BN254 G2: the pair over 29-bit limbs; bit 20 the FIPS pair
                     assert s["acc29"] == limb, (hex(v), s)
-        for bad in (64, 1 << 24):
+        for bad in (64, 1 << 23):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
