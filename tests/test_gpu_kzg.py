@@ -63,10 +63,18 @@ def test_batch_and_downsize():
     polys = [O.gen_scalars("bn254_fr", 900 + i, n).tobytes() for i in range(10)]
     batch = kzg.commit_batch(polys)
     lag = kzg.commit_batch([O.fft(p, n) for p in polys], lagrange=True)
+    # against the oracle's MSM over the SRS the device built (itself checked
+    # against the oracle's SRS in test_setup_and_commit), not only the
+    # single-polynomial path
+    powers, lag_srs = kzg.g1_powers_of_tau(), kzg.g1_powers_of_tau_lagrange()
+    assert batch == [O.msm("bn254_g1", powers, p)[0] for p in polys]
+    assert lag == [O.msm("bn254_g1", lag_srs, O.fft(p, n))[0] for p in polys]
     assert batch == lag == [kzg.commit(p) for p in polys]
     # ragged batch incl. an empty polynomial and a zero polynomial (identity
     # commitments stay (0, 0) through the one-inversion normalisation)
     ragged = [polys[0][:32 * 3], b"", bytes(32 * n), polys[1]]
+    assert kzg.commit_batch(ragged) == [O.msm("bn254_g1", powers[:len(p) * 2], p)[0] if p else bytes(64)
+                                        for p in ragged]
     assert kzg.commit_batch(ragged) == [kzg.commit(p) if p else bytes(64) for p in ragged]
     assert kzg.commit_batch(ragged)[1] == bytes(64) and kzg.commit_batch(ragged)[2] == bytes(64)
     assert kzg.commit_batch([polys[0] + polys[0][:32]]) is None  # more than N: nothing written
