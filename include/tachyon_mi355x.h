@@ -336,6 +336,13 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_window_range_affine(int curve, void
                                                                  const void* scalars, size_t size,
                                                                  unsigned w_begin, unsigned w_end,
                                                                  void* out_affine);
+/* `count` MSMs over the same `len` bases (device memory of the current
+ * device, e.g. a KZG SRS) in one recode / sort / accumulation / reduction:
+ * MSM g takes scalars[g len, (g+1) len) (host or device; zero scalars pad
+ * shorter ones) and writes its affine result to out_affine[g].  Returns 1, or
+ * 0 (nothing written) when the bases are not device memory. */
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_batch_affine(int curve, void* ctx, const void* bases, size_t len,
+                                                        const void* scalars, size_t count, void* out_affine);
 /* Contexts for the C++ plugin boundary (include/tachyon_mi355x_msm.h):
  * VariableBaseMSMGpu<Point>(mem_pool, stream) (variable_base_msm_gpu.h:16-18)
  * over any of the four groups, its work on `stream` (hipStream_t; NULL = a

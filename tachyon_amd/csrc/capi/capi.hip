@@ -163,6 +163,17 @@ void msm_window_range_out(void* ctx, const void* bases, const void* scalars, siz
   memcpy(out, &a, sizeof(a));
 }
 
+// `count` MSMs over the same device-resident bases in one launch sequence
+// (MsmGpu::run_batch): count affine results ((0, 0) = identity)
+template <class Curve>
+void msm_batch_out(void* ctx, const void* bases, size_t len, const void* scalars, size_t count, void* out) {
+  using F = typename Curve::F;
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  const auto pts = c->impl.run_batch(bases, scalars, len, count);
+  auto* o = static_cast<Affine<F>*>(out);
+  for (size_t g = 0; g < count; ++g) o[g] = pts[g].to_affine();
+}
+
 // The MSM in the point form a C++ caller asks for (include/tachyon_mi355x_msm.h):
 // 0 affine {x, y} ((0, 0) = identity); 1 projective / 2 Jacobian {x, y, z}
 // (identity (1, 1, 0), projective_point.h:34-36, jacobian_point.h; otherwise
@@ -367,6 +378,12 @@ void tachyon_mi355x_msm_gpu_window_range_affine(int curve, void* ctx, const void
                                                 size_t size, unsigned w_begin, unsigned w_end, void* out_affine) {
   GUARD_BEGIN CURVE_DISPATCH(curve, msm_window_range_out<C>(ctx, bases, scalars, size, w_begin, w_end, out_affine))
   GUARD_END
+}
+int tachyon_mi355x_msm_gpu_batch_affine(int curve, void* ctx, const void* bases, size_t len, const void* scalars,
+                                        size_t count, void* out_affine) {
+  if (!is_device_pointer(bases)) return 0;
+  GUARD_BEGIN CURVE_DISPATCH(curve, msm_batch_out<C>(ctx, bases, len, scalars, count, out_affine)) GUARD_END
+  return 1;
 }
 void* tachyon_mi355x_msm_gpu_create(int curve, void* stream) {
   GUARD_BEGIN CURVE_DISPATCH(curve, return new MsmCtx<C>(static_cast<hipStream_t>(stream))) GUARD_END

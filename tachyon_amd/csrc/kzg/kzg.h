@@ -59,6 +59,7 @@ class Kzg {
   bool own_stream_ = false;
   size_t n_ = 0;
   DeviceBuffer powers_, lagrange_, scratch_;
+  DeviceBuffer batch_;  // commit_batch: the zero-padded count x len scalars
   std::unique_ptr<msm::MsmGpu<Curve>> msm_;
 };
 

@@ -172,8 +172,20 @@ template <class Curve>
 bool Kzg<Curve>::commit_batch(const Fr* const* scalars, const size_t* lens, size_t count, bool lagrange, Aff* out) {
   for (size_t i = 0; i < count; ++i)
     if (lens[i] > n_) return false;
-  std::vector<XYZZ<F>> pts(count);
-  for (size_t i = 0; i < count; ++i) pts[i] = msm_->run(d_srs(lagrange), scalars[i], lens[i]);
+  // one batched MSM (MsmGpu::run_batch: a block of windows per polynomial,
+  // one recode / sort / accumulation / reduction) over the SRS prefix of the
+  // longest polynomial, the others zero-padded
+  size_t len = 0;
+  for (size_t i = 0; i < count; ++i) len = std::max(len, lens[i]);
+  std::vector<XYZZ<F>> pts(count, XYZZ<F>::zero());
+  if (len > 0) {
+    Fr* padded = static_cast<Fr*>(batch_.ensure(count * len * sizeof(Fr)));
+    TA_HIP(hipMemsetAsync(padded, 0, count * len * sizeof(Fr), msm_->stream()));
+    for (size_t i = 0; i < count; ++i)  // host or device polynomials
+      if (lens[i])
+        TA_HIP(hipMemcpyAsync(padded + i * len, scalars[i], lens[i] * sizeof(Fr), hipMemcpyDefault, msm_->stream()));
+    pts = msm_->run_batch(d_srs(lagrange), padded, len, count);
+  }
   batch_to_affine(pts, out);
   return true;
 }

@@ -168,6 +168,11 @@ class MsmGpu {
   void run_windows(const void* bases, const void* scalars, size_t n, std::vector<Point>* out,
                    MsmPlan* plan_out);
 
+  // `count` MSMs over the same `len` device-resident bases (scalars: count x
+  // len, host or device, zero-padded) as one recode / sort / accumulation /
+  // reduction with a block of windows per MSM; returns the count results.
+  std::vector<Point> run_batch(const void* bases, const void* scalars, size_t len, size_t count);
+
   // The windows [w_begin, w_end) of the MSM only: sum_w 2^(c w) S_w over
   // them (c = the forced window bits or the size's default).  Summing the
   // results of ranges that tile [0, W) gives run(); multi-GPU window split.
@@ -253,6 +258,7 @@ class MsmGpu {
   size_t last_divisions_ = 1;
   unsigned last_schedule_ = 0;
   unsigned range_begin_ = 0, range_end_ = ~0u;  // window range of the next run_windows
+  unsigned batch_ = 1;                           // MSMs in the next run_windows (run_batch)
 };
 
 extern template class MsmGpu<Bn254G1>;

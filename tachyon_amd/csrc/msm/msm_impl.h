@@ -48,8 +48,11 @@ enum : uint32_t { kHead = 1, kTail = 2, kSingle = 4 };
 // Windows [w0, w0 + wr) of W are emitted, as local windows 0 .. wr-1 (the
 // lower windows still run for their carries).
 template <class Fr, class Emit>
+// glen > 0 (a batch of MSMs over shared bases, run_batch): scalar i belongs to
+// MSM g = i / glen, its windows are g * wr .. g * wr + wr - 1 of the key space
+// and its base index is i - g * glen
 __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsigned c, unsigned W, unsigned w0,
-                                              unsigned wr, Emit emit) {
+                                              unsigned wr, Emit emit, uint32_t glen = 0) {
   constexpr int N = Fr::N;
   Fr s = scalar.from_mont();
   uint32_t limbs[N];
@@ -57,6 +60,12 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
   for (int k = 0; k < N; ++k) limbs[k] = s.v[k];
   const uint32_t mask = (1u << c) - 1;
   const uint32_t half = 1u << (c - 1);
+  uint32_t gw = 0, vi = i;
+  if (glen) {
+    const uint32_t g = i / glen;
+    gw = g * wr;
+    vi = i - g * glen;
+  }
   uint32_t carry = 0;
   for (unsigned w = 0; w < w0 + wr; ++w) {
     uint32_t coeff = (limbs[0] & mask) + carry;
@@ -75,7 +84,7 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
       key = coeff;  // top digit, carry folded in, non-negative
       sign = 0;
     }
-    if (w >= w0) emit(w - w0, ((w - w0) << c) | key, i | sign);
+    if (w >= w0) emit(w - w0, ((gw + w - w0) << c) | key, vi | sign);
   }
 }
 
@@ -86,12 +95,12 @@ __device__ __forceinline__ uint32_t entry_val(uint64_t e) { return (uint32_t)e; 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
                                                         unsigned c, unsigned W, unsigned w0, unsigned wr,
-                                                        uint64_t* __restrict__ ents) {
+                                                        uint64_t* __restrict__ ents, uint32_t glen) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  recode_scalar(scalars[i], i, c, W, w0, wr, [&](unsigned w, uint32_t key, uint32_t val) {
-    ents[(size_t)w * n + i] = make_entry(key, val);
-  });
+  recode_scalar(
+      scalars[i], i, c, W, w0, wr,
+      [&](unsigned w, uint32_t key, uint32_t val) { ents[(size_t)w * n + i] = make_entry(key, val); }, glen);
 }
 
 // Recode fused with the first radix pass (key bits 0..7), in two launches:
@@ -137,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
                                                              uint32_t nblocks, uint32_t spt, uint32_t places,
                                                              uint32_t* __restrict__ hist,
                                                              uint32_t* __restrict__ later,
-                                                             uint4* __restrict__ zero, size_t zero_n) {
+                                                             uint4* __restrict__ zero, size_t zero_n, uint32_t glen) {
   __shared__ uint32_t cnt[3][256];
   const uint32_t t = threadIdx.x;
   // the bucket sums start as the identity (all-zero words): cleared here, not by a memset launch
@@ -166,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
           if (places > 0) atomicAdd(&cnt[1][(key >> 8) & 255], 1u);
           if (places > 1) atomicAdd(&cnt[2][(key >> 16) & 255], 1u);
         }
-      });
+      }, glen);
   }
   __syncthreads();
   hist[(size_t)t * nblocks + blockIdx.x] = cnt[0][t];
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
                                                                 uint32_t nblocks, uint32_t spt,
                                                                 const uint32_t* __restrict__ hist,
                                                                 const uint32_t* __restrict__ off,
-                                                                uint64_t* __restrict__ ents) {
+                                                                uint64_t* __restrict__ ents, uint32_t glen) {
   // the block's entries are binned in LDS first, then written out bin run by
   // bin run, so consecutive lanes store to consecutive addresses
   extern __shared__ uint64_t lds_u64[];
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
         } else {
           lents[p] = make_entry(key, val);
         }
-      });
+      }, glen);
   }
   __syncthreads();
   const uint32_t total = loff[255] + cur[255];
@@ -1794,10 +1803,15 @@ void MsmGpu<Curve>::build_chains(const uint32_t* flags, const uint32_t* last, si
 template <class Curve>
 void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan,
                             Point* d_windows) {
-  // W = the windows this run computes (plan.active()); Wt = all windows of
-  // the scalar (the recode's carry chain), the range starting at window w0
-  const unsigned W = plan.active(), Wt = plan.windows, wr0 = plan.w_begin, B = plan.buckets, c = plan.c;
-  const size_t entries = n * W;
+  // Ws = the windows each scalar emits (plan.active()); Wt = all windows of
+  // the scalar (the recode's carry chain), the range starting at window w0;
+  // W = the window sums this run computes: Ws, or Ws per MSM of a batch over
+  // shared bases (run_batch: batch_ MSMs of n / batch_ points each, MSM g's
+  // windows g Ws .. g Ws + Ws - 1 in the key space)
+  const unsigned Ws = plan.active(), Wt = plan.windows, wr0 = plan.w_begin, B = plan.buckets, c = plan.c;
+  const unsigned W = Ws * batch_;
+  const uint32_t glen = batch_ > 1 ? (uint32_t)(n / batch_) : 0u;
+  const size_t entries = n * Ws;
   const size_t nb = (size_t)W * B;
   if (n >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM size must be < 2^31 per device");
   const uint32_t K = plan.K;
@@ -1805,12 +1819,15 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // contiguous entry range [w0*n, w1*n); its sort (sort stream) overlaps the
   // accumulation of the previous group (MSM stream) -- the sort is HBM-bound,
   // the accumulation VALU-bound, so they share the CUs well
-  const unsigned G = std::max(1u, std::min(plan.group, W));
+  // (a batch sorts all its windows together: the recode writes the entries
+  // by scalar window, not by key window)
+  const unsigned G = batch_ > 1 ? W : std::max(1u, std::min(plan.group, W));
   const unsigned ngroups = (W + G - 1) / G;
+  const size_t epw = entries / W;  // entries per key window's share of the array (n without a batch)
   size_t T = 0;  // accumulation threads over all groups
   for (unsigned g = 0; g < ngroups; ++g) {
     const unsigned w0 = g * G, w1 = std::min(W, w0 + G);
-    T += ((size_t)(w1 - w0) * n + K - 1) / K;
+    T += ((size_t)(w1 - w0) * epw + K - 1) / K;
   }
   if (T >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM too large for the chunking");
   ensure_group_events(ngroups);
@@ -1877,7 +1894,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // (the scatter stages a block's spt x 256 x W entries in LDS, <= 128 KiB)
   const uint32_t spt = recode_spt_;
   const bool narrow = key_bits <= 24 && !wide_stage_;  // 7-byte LDS staging in the scatter
-  const size_t scatter_lds = (size_t)spt * kBlock * W * (narrow ? 7 : sizeof(uint64_t));
+  const size_t scatter_lds = (size_t)spt * kBlock * Ws * (narrow ? 7 : sizeof(uint64_t));
   const bool fused = fuse_recode_ && G == W && scatter_lds <= 128 * 1024;
   const unsigned sort_begin = fused ? std::min(8u, key_bits) : 0u;
   // onesweep passes fed with digit counts from the recode (places = the
@@ -1899,8 +1916,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     uint32_t* later = hist + 2 * hn;
     uint32_t* digit_cnt = later + later_places * hn;  // 2 x 256 counts, 2 x 256 offsets, 256 spare
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       Wt, wr0, W, nblocks, spt, later_places, hist, later, reinterpret_cast<uint4*>(bucket_sum),
-                       nb * slot / 16);
+                       Wt, wr0, Ws, nblocks, spt, later_places, hist, later, reinterpret_cast<uint4*>(bucket_sum),
+                       nb * slot / 16, glen);
     TA_HIP(hipGetLastError());
     if (later_places > 0) {
       digit_off = digit_cnt + 2 * 256;
@@ -1927,10 +1944,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       scatter_lds_set_[narrow ? 1 : 0] = true;
     }
     hipLaunchKernelGGL(scatter, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars, (uint32_t)n, c, Wt, wr0,
-                       W, nblocks, spt, hist, hoff, dst);
+                       Ws, nblocks, spt, hist, hoff, dst, glen);
   } else {
     hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       Wt, wr0, W, ents);
+                       Wt, wr0, Ws, ents, glen);
   }
   TA_HIP(hipGetLastError());
   // every bucket without an entry stays the identity (the fused recode clears them)
@@ -1939,7 +1956,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   if (sort_stream != stream_) TA_HIP(hipStreamWaitEvent(sort_stream, ev_[2], 0));
 
   // ---- per group: radix sort of its (window, bucket, point) entries, then accumulation ----
-  const size_t max_group_entries = (size_t)G * n;
+  const size_t max_group_entries = (size_t)G * epw;
   size_t sort_bytes = 0;
   void* sort_tmp = nullptr;
   uint8_t* os_tmp = nullptr;  // own passes: lookback states, block id, spare offsets
@@ -1954,7 +1971,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   acc_launches_ = ngroups;
   for (unsigned g = 0; g < ngroups; ++g) {
     const unsigned w0 = g * G, w1 = std::min(W, w0 + G);
-    const size_t e0 = (size_t)w0 * n, ecount = (size_t)(w1 - w0) * n;
+    const size_t e0 = (size_t)w0 * epw, ecount = (size_t)(w1 - w0) * epw;
     size_t bytes = sort_bytes;
     if (own_sort) {
       const size_t lookback_bytes = (size_t)256 * ((entries + kOnesweepMinTile - 1) / kOnesweepMinTile) * 4;
@@ -2315,7 +2332,8 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   pair_acc_ = !(variant_ & 32768);
   pair_inline_ = !(variant_ & 65536);
   if (plan_out) *plan_out = plan;
-  out->assign(plan.active(), Point::zero());
+  const unsigned nwin = plan.active() * batch_;  // window sums (per MSM of a batch, run_batch)
+  out->assign(nwin, Point::zero());
   if (n == 0 || plan.active() == 0) return;
   if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
   const Aff* d_bases = static_cast<const Aff*>(bases);
@@ -2330,9 +2348,9 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
     TA_HIP(hipMemcpyAsync(p, scalars, n * sizeof(Fr), hipMemcpyHostToDevice, stream_));
     d_scalars = static_cast<const Fr*>(p);
   }
-  Point* d_windows = static_cast<Point*>(windows_.ensure(std::max(1u, plan.active()) * sizeof(Point)));
+  Point* d_windows = static_cast<Point*>(windows_.ensure(std::max(1u, nwin) * sizeof(Point)));
   enqueue(d_bases, d_scalars, n, plan, d_windows);
-  TA_HIP(hipMemcpyAsync(out->data(), d_windows, plan.active() * sizeof(Point), hipMemcpyDeviceToHost, stream_));
+  TA_HIP(hipMemcpyAsync(out->data(), d_windows, nwin * sizeof(Point), hipMemcpyDeviceToHost, stream_));
   TA_HIP(hipStreamSynchronize(stream_));
   for (auto& p : *out) p = p.canonical();  // device values live in [0, 2p)
   if (profile_) {
@@ -2621,6 +2639,42 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* 
     total = total + combine_windows(ws, plan.c);
   }
   return total;
+}
+
+// `count` MSMs over the same `len` device-resident bases in one recode, sort,
+// accumulation and reduction: MSM g's scalars are scalars[g len, (g+1) len)
+// (device or host; zero scalars pad shorter ones), its windows a block of
+// the key space (recode_scalar's glen), its result the Horner combination of
+// its own window sums.  One launch sequence instead of `count` -- the small
+// MSMs of a KZG batch commitment are latency-bound one by one.
+template <class Curve>
+std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* bases, const void* scalars,
+                                                                    size_t len, size_t count) {
+  std::vector<Point> res(count, Point::zero());
+  if (count == 0 || len == 0) return res;
+  if (count == 1) {
+    res[0] = run(bases, scalars, len);
+    return res;
+  }
+  if (!is_device_pointer(bases)) throw std::runtime_error("tachyon_mi355x: run_batch needs device-resident bases");
+  const size_t total = len * count;
+  if (total >= (size_t(1) << 31) || count > 4096)
+    throw std::runtime_error("tachyon_mi355x: MSM batch too large (< 2^31 scalars, <= 4096 MSMs)");
+  struct Reset {
+    MsmGpu* m;
+    ~Reset() { m->batch_ = 1; }
+  } reset{this};
+  batch_ = (unsigned)count;
+  last_divisions_ = 1;
+  std::vector<Point> ws;
+  MsmPlan plan;
+  run_windows(bases, scalars, total, &ws, &plan);
+  const unsigned Ws = plan.active();
+  for (size_t g = 0; g < count; ++g) {
+    std::vector<Point> one(ws.begin() + g * Ws, ws.begin() + (g + 1) * Ws);
+    res[g] = combine_windows(one, plan.c);
+  }
+  return res;
 }
 
 // The windows [w_begin, w_end) alone (PippengerBase::AccumulateWindowSums

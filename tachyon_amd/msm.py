@@ -83,6 +83,21 @@ class VariableBaseMSMGpu:
         del keep
         return out.raw
 
+    def run_batch(self, d_bases, scalars, length: int, count: int) -> list:
+        """`count` MSMs over the same `length` device-resident bases (a CUDA
+        tensor or device pointer) in one launch sequence: MSM g takes
+        scalars[g length .. (g+1) length) (host or device; zero-padded);
+        returns count affine results -- tachyon_mi355x_msm_gpu_batch_affine."""
+        pb = d_bases if isinstance(d_bases, int) else d_bases.data_ptr()
+        ps, sn, ks = _ptr(scalars)
+        if sn < length * count * self.scalar_bytes:
+            raise ValueError("scalars shorter than count x length")
+        out = ctypes.create_string_buffer(self.point_bytes * max(1, count))
+        if not lib().tachyon_mi355x_msm_gpu_batch_affine(self.curve_id, self._ctx, pb, length, ps, count, out):
+            raise ValueError("run_batch needs device-resident bases")
+        del ks
+        return [out.raw[g * self.point_bytes:(g + 1) * self.point_bytes] for g in range(count)]
+
     def run_window_range(self, bases, scalars, w_begin: int, w_end: int, n=None) -> bytes:
         """The windows [w_begin, w_end) of the MSM only: sum_w 2^(c w) S_w
         (affine).  Ranges tiling [0, W) add up to run(); see

@@ -477,3 +477,43 @@ def test_chain_flags_pre_derived_match(curve, logn):
             assert m.last_schedule()["chains_checked"], name
     finally:
         m.set_variant(0)
+
+
+@pytest.mark.parametrize("curve,length,count", [("bn254_g1", 1, 3), ("bn254_g1", 100, 5), ("bn254_g1", 3001, 17),
+                                                ("bn254_g1", 1 << 14, 6), ("bn254_g2", 500, 4),
+                                                ("bls12_381_g1", 777, 5), ("bls12_381_g2", 300, 3)])
+def test_msm_batch_vs_oracle(curve, length, count):
+    """tachyon_mi355x_msm_gpu_batch_affine: `count` MSMs over the same device
+    bases in one launch sequence (a block of windows per MSM) -- every result
+    equal to the oracle's MSM of its scalar vector; ragged vectors (zero
+    padding), an all-zero vector, a NonUniform (one repeated scalar) vector,
+    host and device scalars."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    pb, sf = O.CURVE_INFO[curve]
+    bases = O.gen_bases(curve, 61, length, 64).tobytes()
+    d_bases = torch.frombuffer(bytearray(bases), dtype=torch.uint8).cuda()
+    vecs = []
+    for g in range(count):
+        v = O.gen_scalars(sf, 6100 + g, length).tobytes()
+        if g % 3 == 1:  # ragged: the tail zero
+            keep = max(1, length * (g + 1) // (count + 1))
+            v = v[:32 * keep] + bytes(32 * (length - keep))
+        if g == 2:
+            v = bytes(32 * length)
+        if g == 3:
+            v = O.gen_scalars(sf, 6200, 1).tobytes() * length
+        vecs.append(v)
+    scalars = b"".join(vecs)
+    m = VariableBaseMSMGpu(curve)
+    try:
+        got = m.run_batch(d_bases, scalars, length, count)
+        want = [O.msm(curve, bases, v)[0] for v in vecs]
+        assert got == want
+        d_scalars = torch.frombuffer(bytearray(scalars), dtype=torch.uint8).cuda()
+        torch.cuda.synchronize()
+        assert m.run_batch(d_bases, d_scalars, length, count) == want
+        with pytest.raises(ValueError):
+            m.run_batch(0, scalars, length, count)  # null bases: not device memory
+    finally:
+        m.close()
