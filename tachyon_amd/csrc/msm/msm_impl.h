@@ -1814,6 +1814,8 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   const size_t entries = n * Ws;
   const size_t nb = (size_t)W * B;
   if (n >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM size must be < 2^31 per device");
+  if (((uint64_t)W << c) > (uint64_t(1) << 32))  // 32-bit keys (window << c | digit)
+    throw std::runtime_error("tachyon_mi355x: too many windows for 32-bit bucket keys (MSM batch too large)");
   const uint32_t K = plan.K;
   // window groups: group g covers windows [g*G, min(W, (g+1)*G)), i.e. the
   // contiguous entry range [w0*n, w1*n); its sort (sort stream) overlaps the
