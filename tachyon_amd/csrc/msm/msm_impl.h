@@ -2662,10 +2662,23 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* 
   const size_t total = len * count;
   if (total >= (size_t(1) << 31) || count > 4096)
     throw std::runtime_error("tachyon_mi355x: MSM batch too large (< 2^31 scalars, <= 4096 MSMs)");
+  // the window size of one MSM of `len` points (not of the batch's total):
+  // accumulation and reduction both scale with count, and windows sized for
+  // the total leave count x more buckets than entries per bucket (2^14 x 32
+  // MSMs: 8.4 ms with the total's c = 15 -- profiles/r04c/batch_probe_*.log)
   struct Reset {
     MsmGpu* m;
-    ~Reset() { m->batch_ = 1; }
-  } reset{this};
+    unsigned c;
+    ~Reset() {
+      m->batch_ = 1;
+      m->force_c_ = c;
+    }
+  } reset{this, force_c_};
+  if (!force_c_) {
+    unsigned lg = 1;
+    while ((size_t(1) << lg) < len) ++lg;
+    force_c_ = default_window_bits(lg, Fr::Config::kModulusBits);
+  }
   batch_ = (unsigned)count;
   last_divisions_ = 1;
   std::vector<Point> ws;
