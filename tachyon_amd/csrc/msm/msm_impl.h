@@ -2684,10 +2684,23 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* 
   std::vector<Point> ws;
   MsmPlan plan;
   run_windows(bases, scalars, total, &ws, &plan);
+  // each MSM's Horner combination of its windows on the host (W c doublings
+  // apiece), spread over a few host threads for larger batches
   const unsigned Ws = plan.active();
-  for (size_t g = 0; g < count; ++g) {
-    std::vector<Point> one(ws.begin() + g * Ws, ws.begin() + (g + 1) * Ws);
-    res[g] = combine_windows(one, plan.c);
+  auto combine = [&](size_t g0, size_t g1) {
+    for (size_t g = g0; g < g1; ++g) {
+      std::vector<Point> one(ws.begin() + g * Ws, ws.begin() + (g + 1) * Ws);
+      res[g] = combine_windows(one, plan.c);
+    }
+  };
+  const size_t nth = std::min<size_t>({count / 4, 16, std::max(1u, std::thread::hardware_concurrency())});
+  if (nth <= 1) {
+    combine(0, count);
+  } else {
+    std::vector<std::thread> th;
+    const size_t step = (count + nth - 1) / nth;
+    for (size_t g0 = 0; g0 < count; g0 += step) th.emplace_back(combine, g0, std::min(count, g0 + step));
+    for (auto& t : th) t.join();
   }
   return res;
 }
