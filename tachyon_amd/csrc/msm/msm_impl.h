@@ -2662,10 +2662,14 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* 
   const size_t total = len * count;
   if (total >= (size_t(1) << 31) || count > 4096)
     throw std::runtime_error("tachyon_mi355x: MSM batch too large (< 2^31 scalars, <= 4096 MSMs)");
-  // the window size of one MSM of `len` points (not of the batch's total):
-  // accumulation and reduction both scale with count, and windows sized for
-  // the total leave count x more buckets than entries per bucket (2^14 x 32
-  // MSMs: 8.4 ms with the total's c = 15 -- profiles/r04c/batch_probe_*.log)
+  // window size from the length of one MSM, not the batch's total (windows
+  // sized for the total leave count x more buckets than entries per bucket:
+  // 2^14 x 32 MSMs 8.4 ms at the total's c = 15), but above one MSM's own
+  // default: the batch's count x W windows make the per-window work count
+  // times larger.  c = 8 up to len 2^13, 10 from 2^14 (c swept 5..16 over len
+  // 2^10..2^16 x count 8..128: 8 best or within noise at len <= 2^13, 10 at
+  // 2^14..2^16, odd 7 and 9 behind both neighbours;
+  // profiles/r04c/batch_probe_c_sweep*.log)
   struct Reset {
     MsmGpu* m;
     unsigned c;
@@ -2677,7 +2681,7 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* 
   if (!force_c_) {
     unsigned lg = 1;
     while ((size_t(1) << lg) < len) ++lg;
-    force_c_ = default_window_bits(lg, Fr::Config::kModulusBits);
+    force_c_ = std::max(default_window_bits(lg, Fr::Config::kModulusBits), lg <= 13 ? std::min(lg + 1, 8u) : 10u);
   }
   batch_ = (unsigned)count;
   last_divisions_ = 1;
