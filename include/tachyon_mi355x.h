@@ -339,8 +339,13 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_window_range_affine(int curve, void
 /* `count` MSMs over the same `len` bases (device memory of the current
  * device, e.g. a KZG SRS) in one recode / sort / accumulation / reduction:
  * MSM g takes scalars[g len, (g+1) len) (host or device; zero scalars pad
- * shorter ones) and writes its affine result to out_affine[g].  Returns 1, or
- * 0 (nothing written) when the bases are not device memory. */
+ * shorter ones) and writes its affine result to out_affine[g].  Runs on the
+ * context's own device even after set_devices (the bases live there).  Window
+ * bits: set_window_bits if forced, else 8 up to 2^13 points per MSM and 10
+ * from 2^14 (or one MSM's default where larger).  Returns 1, or 0 (nothing
+ * written) when the bases are not device memory; count x len must stay below
+ * 2^31 and count at most 4096 (else the call aborts with a message, as
+ * every failure of this library does). */
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_batch_affine(int curve, void* ctx, const void* bases, size_t len,
                                                         const void* scalars, size_t count, void* out_affine);
 /* Contexts for the C++ plugin boundary (include/tachyon_mi355x_msm.h):
