@@ -480,7 +480,7 @@ def test_chain_flags_pre_derived_match(curve, logn):
 
 
 @pytest.mark.parametrize("curve,length,count", [("bn254_g1", 1, 3), ("bn254_g1", 100, 5), ("bn254_g1", 3001, 17),
-                                                ("bn254_g1", 1 << 14, 6), ("bn254_g2", 500, 4),
+                                                ("bn254_g1", 1 << 14, 6), ("bn254_g1", 64, 70), ("bn254_g2", 500, 4),
                                                 ("bls12_381_g1", 777, 5), ("bls12_381_g2", 300, 3)])
 def test_msm_batch_vs_oracle(curve, length, count):
     """tachyon_mi355x_msm_gpu_batch_affine: `count` MSMs over the same device
