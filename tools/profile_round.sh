@@ -22,5 +22,5 @@ P=$OUT/publish
 mkdir -p $P
 cp $OUT/summary.md $OUT/pmc_traffic.json $P/
 cp $OUT/trace/run_kernel_stats.csv $P/kernel_stats.csv
-tail -n 1 $OUT/bench_under_trace.log > $P/bench_under_trace.json
+grep "^{\"metric\"" $OUT/bench_under_trace.log | tail -n 1 > $P/bench_under_trace.json
 echo done
