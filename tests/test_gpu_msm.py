@@ -517,3 +517,29 @@ def test_msm_batch_vs_oracle(curve, length, count):
             m.run_batch(0, scalars, length, count)  # null bases: not device memory
     finally:
         m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c", [5, 9, 12])
+def test_msm_batch_forced_window_bits(c):
+    """run_batch under set_window_bits: the forced c is used (any c gives the
+    same sums) and survives the batch -- the single MSM after it, and a second
+    batch, still match the oracle."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    curve, length, count = "bn254_g1", 700, 9
+    pb, sf = O.CURVE_INFO[curve]
+    bases = O.gen_bases(curve, 71, length, 64).tobytes()
+    d_bases = torch.frombuffer(bytearray(bases), dtype=torch.uint8).cuda()
+    vecs = [O.gen_scalars(sf, 7100 + g, length).tobytes() for g in range(count)]
+    want = [O.msm(curve, bases, v)[0] for v in vecs]
+    m = VariableBaseMSMGpu(curve)
+    try:
+        m.set_window_bits(c)
+        assert m.run_batch(d_bases, b"".join(vecs), length, count) == want
+        assert m.run(bases, vecs[4]) == want[4]
+        m.set_window_bits(0)
+        assert m.run_batch(d_bases, b"".join(vecs), length, count) == want
+        assert m.run(bases, vecs[7]) == want[7]
+    finally:
+        m.close()
