@@ -531,7 +531,11 @@ TACHYON_C_EXPORT int tachyon_mi355x_kzg_commit(tachyon_mi355x_kzg* kzg, int lagr
  * GetBatchCommitments, kzg.h:116-165,296-307): `count` polynomials,
  * scalars[i] of lens[i] elements (host or device), their commitments written
  * affine to out_affine[i], normalised together with one field inversion
- * (BatchNormalize).  Returns 1, or 0 (nothing written) when any lens[i] > N. */
+ * (BatchNormalize).  Polynomials of similar length run as batched MSMs
+ * (groups closed when zero-padding would more than double their work or at
+ * the batched MSM's size limits), the rest as single MSMs: any count and any
+ * mix of lengths <= N is accepted.  Returns 1, or 0 (nothing written) when
+ * any lens[i] > N. */
 TACHYON_C_EXPORT int tachyon_mi355x_kzg_commit_batch(tachyon_mi355x_kzg* kzg, int lagrange,
                                                      const void* const* scalars, const size_t* lens, size_t count,
                                                      void* out_affine);

@@ -70,11 +70,26 @@ static inline int FF_FN(root_of_unity)(size_t n, FF_T* out) {
   return 1;
 }
 
-/* F::GetSuccessivePowers(size, g) */
-static inline void FF_FN(powers)(FF_T* out, size_t n, FF_T g) {
-  FF_T p = FF_FN(one)();
-  for (size_t i = 0; i < n; ++i) { out[i] = p; p = FF_FN(mul)(p, g); }
+/* F::GetSuccessivePowers(size, g), out[i] = c * g^i.  Blocks of 2^16 run on
+ * OpenMP threads, each starting from c * g^start (field arithmetic is exact, so
+ * the values equal the serial running product's). */
+static inline void FF_FN(scaled_powers)(FF_T* out, size_t n, FF_T g, FF_T c, int mul_into) {
+  const size_t blk = (size_t)1 << 16;
+  const long nb = (long)((n + blk - 1) / blk);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (long b = 0; b < nb; ++b) {
+    size_t i0 = (size_t)b * blk, i1 = i0 + blk < n ? i0 + blk : n;
+    uint64_t e = (uint64_t)i0;
+    FF_T p = FF_FN(mul)(c, FF_FN(pow)(g, &e, 1));
+    for (size_t i = i0; i < i1; ++i) {
+      out[i] = mul_into ? FF_FN(mul)(out[i], p) : p;
+      p = FF_FN(mul)(p, g);
+    }
+  }
 }
+static inline void FF_FN(powers)(FF_T* out, size_t n, FF_T g) { FF_FN(scaled_powers)(out, n, g, FF_FN(one)(), 0); }
 
 static DOM_T* DOM_FN(create)(size_t num_coeffs) {
   DOM_T* d = (DOM_T*)calloc(1, sizeof(DOM_T));
@@ -99,6 +114,9 @@ static DOM_T* DOM_FN(create)(size_t num_coeffs) {
     size_t sz = d->size >> (i + 1);
     d->roots_vec[L - i - 1] = (FF_T*)malloc(sizeof(FF_T) * sz);
     d->inv_roots_vec[i] = (FF_T*)malloc(sizeof(FF_T) * sz);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
     for (size_t j = 0; j < sz; ++j) {
       d->roots_vec[L - i - 1][j] = d->roots_vec[L - 1][j << i];
       d->inv_roots_vec[i][j] = d->inv_roots_vec[0][j << i];
@@ -126,19 +144,19 @@ static void DOM_FN(set_offset)(DOM_T* d, FF_T offset) {
 }
 
 /* DistributePowersAndMulByConst: v[i] *= c * g^i */
-static void FF_FN(distribute_powers)(FF_T* v, size_t n, FF_T g, FF_T c) {
-  FF_T p = c;
-  for (size_t i = 0; i < n; ++i) { v[i] = FF_FN(mul)(v[i], p); p = FF_FN(mul)(p, g); }
-}
+static void FF_FN(distribute_powers)(FF_T* v, size_t n, FF_T g, FF_T c) { FF_FN(scaled_powers)(v, n, g, c, 1); }
 
 /* ApplyButterfly, radix2_evaluation_domain.h:290-312 */
 static void FF_FN(apply_butterfly)(FF_T* v, size_t n, const FF_T* roots, size_t gap, int in_out) {
+  /* one loop over all n/2 butterflies (i = chunk base, j = offset in the
+   * chunk), so the large-gap stages spread over the threads too */
   size_t chunk = 2 * gap;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static)
 #endif
-  for (size_t i = 0; i < n; i += chunk) {
-    for (size_t j = 0; j < gap; ++j) {
+  for (size_t b = 0; b < n / 2; ++b) {
+    {
+      size_t i = (b / gap) * chunk, j = b % gap;
       FF_T* lo = &v[i + j];
       FF_T* hi = &v[i + j + gap];
       if (in_out) { /* ButterflyFnInOut :518-524 */
@@ -199,6 +217,9 @@ static size_t DOM_FN(ifft)(const DOM_T* d, FF_T* v, size_t num_evals) {
   }
   FF_FN(swap_bitrev)(v, n, d->log_size);
   if (!d->has_offset) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static)
+#endif
     for (size_t i = 0; i < n; ++i) v[i] = FF_FN(mul)(v[i], d->size_inv);
   } else {
     FF_FN(distribute_powers)(v, n, d->offset_inv, d->size_inv);

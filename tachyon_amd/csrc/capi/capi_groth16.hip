@@ -256,13 +256,20 @@ void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, c
 }
 
 void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on) {
-  GUARD_BEGIN PROVER_DISPATCH(prover, impl->set_profile(on != 0)); GUARD_END
+  GUARD_BEGIN
+  PROVER_DISPATCH(prover, impl->set_profile(on != 0));
+  for (auto& p : prover->bn_dev) p->set_profile(on != 0);
+  for (auto& p : prover->bls_dev) p->set_profile(on != 0);
+  GUARD_END
 }
 
+// After set_devices the proof runs on the per-device provers: report the lead
+// device's (rank 0's) phases, as the MSM C-API reports multi->lead()
 void tachyon_mi355x_groth16_last_timings(const tachyon_mi355x_groth16_prover* prover, float* out8) {
   GUARD_BEGIN
   PROVER_DISPATCH(prover, {
-    const auto& t = impl->timings();
+    const auto& t = !prover->bn_dev.empty() ? prover->bn_dev[0]->timings()
+                    : !prover->bls_dev.empty() ? prover->bls_dev[0]->timings() : impl->timings();
     const float v[8] = {t.upload, t.qap, t.msm_a, t.msm_b2, t.msm_b1, t.msm_l, t.msm_h, t.total};
     memcpy(out8, v, sizeof(v));
   });

@@ -70,6 +70,18 @@ inline bool is_device_pointer(const void* p) {
   return attr.type == hipMemoryTypeDevice || attr.isManaged;
 }
 
+// The device that owns `p` (device or managed memory), or -1 for host memory.
+inline int pointer_device(const void* p) {
+  if (!p) return -1;
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  return (attr.type == hipMemoryTypeDevice || attr.isManaged) ? attr.device : -1;
+}
+
 inline unsigned ceil_div(size_t a, size_t b) { return (unsigned)((a + b - 1) / b); }
 
 inline void require_gpu() {

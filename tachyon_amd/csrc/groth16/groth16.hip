@@ -241,6 +241,7 @@ void Groth16Prover<G1, G2>::init_device_state() {
 template <class G1, class G2>
 Groth16Prover<G1, G2>::Groth16Prover(const Groth16Prover& src, int src_device, hipStream_t stream)
     : key_(src.key_), stream_(stream) {
+  profile_ = src.profile_;
   init_device_state();
   int dev = 0;
   TA_HIP(hipGetDevice(&dev));
@@ -349,9 +350,18 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   if (world == 0 || rank >= world) throw std::runtime_error("tachyon_mi355x: Groth16 shard rank >= world");
   auto t0 = Clock::now();
   const Fr* d_full = full;
-  if (!is_device_pointer(full)) {
+  int cur_device = 0;
+  TA_HIP(hipGetDevice(&cur_device));
+  const int src_device = pointer_device(full);
+  if (src_device < 0) {
     d_full = full_.as<Fr>();
     TA_HIP(hipMemcpyAsync(const_cast<Fr*>(d_full), full, m * sizeof(Fr), hipMemcpyHostToDevice, stream_));
+  } else if (src_device != cur_device) {
+    // an assignment in another GPU's HBM (the one-process multi-device prover
+    // hands every device the caller's pointer): a peer copy into this
+    // device's buffer, never a direct cross-device read by the kernels
+    d_full = full_.as<Fr>();
+    TA_HIP(hipMemcpyPeerAsync(const_cast<Fr*>(d_full), cur_device, full, src_device, m * sizeof(Fr), stream_));
   }
   if (profile_) {
     TA_HIP(hipStreamSynchronize(stream_));

@@ -172,19 +172,41 @@ template <class Curve>
 bool Kzg<Curve>::commit_batch(const Fr* const* scalars, const size_t* lens, size_t count, bool lagrange, Aff* out) {
   for (size_t i = 0; i < count; ++i)
     if (lens[i] > n_) return false;
-  // one batched MSM (MsmGpu::run_batch: a block of windows per polynomial,
-  // one recode / sort / accumulation / reduction) over the SRS prefix of the
-  // longest polynomial, the others zero-padded
-  size_t len = 0;
-  for (size_t i = 0; i < count; ++i) len = std::max(len, lens[i]);
+  // Polynomials of similar length go into one batched MSM (MsmGpu::run_batch:
+  // a block of windows per polynomial, one recode / sort / accumulation /
+  // reduction) over the SRS prefix of the group's longest one, the others
+  // zero-padded.  Groups are taken longest first and closed when padding
+  // would more than double the group's work (count x L > 2 x sum of lens),
+  // at run_batch's limits (max_batch_count) or at kGroupScalars padded
+  // scalars (the batch's sort buffers grow ~16 B per scalar-window); a
+  // group of one is a plain MSM.  So a ragged batch costs about its real
+  // work, and a halo2-sized batch (thousands of columns of 2^20) runs as
+  // several batched MSMs instead of one refused one.
+  constexpr size_t kGroupScalars = size_t(1) << 26;
+  std::vector<size_t> order;
+  for (size_t i = 0; i < count; ++i)
+    if (lens[i]) order.push_back(i);
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return lens[a] > lens[b]; });
   std::vector<XYZZ<F>> pts(count, XYZZ<F>::zero());
-  if (len > 0) {
-    Fr* padded = static_cast<Fr*>(batch_.ensure(count * len * sizeof(Fr)));
-    TA_HIP(hipMemsetAsync(padded, 0, count * len * sizeof(Fr), msm_->stream()));
-    for (size_t i = 0; i < count; ++i)  // host or device polynomials
-      if (lens[i])
-        TA_HIP(hipMemcpyAsync(padded + i * len, scalars[i], lens[i] * sizeof(Fr), hipMemcpyDefault, msm_->stream()));
-    pts = msm_->run_batch(d_srs(lagrange), padded, len, count);
+  const Aff* srs = d_srs(lagrange);
+  for (size_t i = 0; i < order.size();) {
+    const size_t L = lens[order[i]];
+    const size_t cap = std::min(msm_->max_batch_count(L), std::max<size_t>(1, kGroupScalars / L));
+    size_t j = i + 1, sum = L;
+    while (j < order.size() && j - i < cap && (j - i + 1) * L <= 2 * (sum + lens[order[j]])) sum += lens[order[j++]];
+    const size_t g = j - i;
+    if (g == 1) {
+      pts[order[i]] = msm_->run(srs, scalars[order[i]], L);
+    } else {
+      Fr* padded = static_cast<Fr*>(batch_.ensure(g * L * sizeof(Fr)));
+      TA_HIP(hipMemsetAsync(padded, 0, g * L * sizeof(Fr), msm_->stream()));
+      for (size_t k = 0; k < g; ++k)  // host or device polynomials
+        TA_HIP(hipMemcpyAsync(padded + k * L, scalars[order[i + k]], lens[order[i + k]] * sizeof(Fr),
+                              hipMemcpyDefault, msm_->stream()));
+      const auto res = msm_->run_batch(srs, padded, L, g);
+      for (size_t k = 0; k < g; ++k) pts[order[i + k]] = res[k];
+    }
+    i = j;
   }
   batch_to_affine(pts, out);
   return true;

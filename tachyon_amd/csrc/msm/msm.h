@@ -172,6 +172,10 @@ class MsmGpu {
   // len, host or device, zero-padded) as one recode / sort / accumulation /
   // reduction with a block of windows per MSM; returns the count results.
   std::vector<Point> run_batch(const void* bases, const void* scalars, size_t len, size_t count);
+  // The largest count run_batch takes for MSMs of `len` points (at most 4096
+  // MSMs, count x len < 2^31 scalars, count x W windows << c within the 32-bit
+  // bucket keys); 0 when len == 0.
+  size_t max_batch_count(size_t len) const;
 
   // The windows [w_begin, w_end) of the MSM only: sum_w 2^(c w) S_w over
   // them (c = the forced window bits or the size's default).  Summing the
@@ -209,6 +213,7 @@ class MsmGpu {
   unsigned last_schedule() const { return last_schedule_; }  // kSched* bits of the last run
 
  private:
+  unsigned batch_window_bits(size_t len) const;
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
   Point run_host_pipelined(const void* bases, const void* scalars, size_t n, size_t chunks);
   size_t work_bytes(size_t n) const;

@@ -2649,6 +2649,32 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* 
 // the key space (recode_scalar's glen), its result the Horner combination of
 // its own window sums.  One launch sequence instead of `count` -- the small
 // MSMs of a KZG batch commitment are latency-bound one by one.
+// window size from the length of one MSM, not the batch's total (windows
+// sized for the total leave count x more buckets than entries per bucket:
+// 2^14 x 32 MSMs 8.4 ms at the total's c = 15), but above one MSM's own
+// default: the batch's count x W windows make the per-window work count
+// times larger.  c = 8 up to len 2^13, 10 from 2^14 (c swept 5..16 over len
+// 2^10..2^16 x count 8..128: 8 best or within noise at len <= 2^13, 10 at
+// 2^14..2^16, odd 7 and 9 behind both neighbours;
+// profiles/r04c/batch_probe_c_sweep*.log)
+template <class Curve>
+unsigned MsmGpu<Curve>::batch_window_bits(size_t len) const {
+  if (force_c_) return force_c_;
+  unsigned lg = 1;
+  while ((size_t(1) << lg) < len) ++lg;
+  return std::max(default_window_bits(lg, Fr::Config::kModulusBits), lg <= 13 ? std::min(lg + 1, 8u) : 10u);
+}
+
+template <class Curve>
+size_t MsmGpu<Curve>::max_batch_count(size_t len) const {
+  if (len == 0) return 0;
+  const unsigned c = batch_window_bits(len);
+  const uint64_t W = (Fr::Config::kModulusBits + 1 + c - 1) / c;
+  const uint64_t by_keys = (uint64_t(1) << 32) / (W << c);
+  const uint64_t by_total = ((uint64_t(1) << 31) - 1) / len;
+  return (size_t)std::max<uint64_t>(1, std::min<uint64_t>({4096, by_keys, by_total}));
+}
+
 template <class Curve>
 std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* bases, const void* scalars,
                                                                     size_t len, size_t count) {
@@ -2662,14 +2688,7 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* 
   const size_t total = len * count;
   if (total >= (size_t(1) << 31) || count > 4096)
     throw std::runtime_error("tachyon_mi355x: MSM batch too large (< 2^31 scalars, <= 4096 MSMs)");
-  // window size from the length of one MSM, not the batch's total (windows
-  // sized for the total leave count x more buckets than entries per bucket:
-  // 2^14 x 32 MSMs 8.4 ms at the total's c = 15), but above one MSM's own
-  // default: the batch's count x W windows make the per-window work count
-  // times larger.  c = 8 up to len 2^13, 10 from 2^14 (c swept 5..16 over len
-  // 2^10..2^16 x count 8..128: 8 best or within noise at len <= 2^13, 10 at
-  // 2^14..2^16, odd 7 and 9 behind both neighbours;
-  // profiles/r04c/batch_probe_c_sweep*.log)
+  // (window size: batch_window_bits)
   struct Reset {
     MsmGpu* m;
     unsigned c;
@@ -2678,11 +2697,7 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* 
       m->force_c_ = c;
     }
   } reset{this, force_c_};
-  if (!force_c_) {
-    unsigned lg = 1;
-    while ((size_t(1) << lg) < len) ++lg;
-    force_c_ = std::max(default_window_bits(lg, Fr::Config::kModulusBits), lg <= 13 ? std::min(lg + 1, 8u) : 10u);
-  }
+  force_c_ = batch_window_bits(len);
   batch_ = (unsigned)count;
   last_divisions_ = 1;
   std::vector<Point> ws;

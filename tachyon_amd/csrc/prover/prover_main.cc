@@ -172,14 +172,20 @@ int main(int argc, char** argv) {
     else if (a == "--verify") { std::cerr << "--verify is not supported by this backend\n"; return 1; }
     else if (a == "--trace_path") next();
     else if (a == "--devices") {
+      // comma-separated non-negative ids; empty fields are skipped, anything
+      // else that is not a number is a usage error (not an uncaught throw)
       std::string list = next();
       size_t pos = 0;
       while (pos <= list.size()) {
         size_t comma = list.find(',', pos);
         if (comma == std::string::npos) comma = list.size();
-        devices.push_back(std::stoi(list.substr(pos, comma - pos)));
+        const std::string field = list.substr(pos, comma - pos);
         pos = comma + 1;
+        if (field.empty()) continue;
+        if (field.find_first_not_of("0123456789") != std::string::npos || field.size() > 6) return usage();
+        devices.push_back(std::stoi(field));
       }
+      if (devices.empty()) return usage();
     }
     else return usage();
   }

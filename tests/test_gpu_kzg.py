@@ -127,3 +127,32 @@ def test_device_resident_scalars():
     d = torch.from_numpy(coeffs.view(np.uint8).copy()).cuda()
     assert kzg.commit(d) == kzg.commit(coeffs.tobytes())
     kzg.close()
+
+
+def test_batch_grouping_ragged_and_over_limits():
+    """commit_batch groups polynomials of similar length into batched MSMs and
+    closes a group when zero-padding would more than double its work: one 2^12
+    polynomial beside 60 short ones (the short ones are not all padded to
+    2^12), and 4,500 three-term polynomials -- more than
+    one batched MSM takes (4,096) -- all equal the oracle's MSM over the
+    device SRS, in the caller's order."""
+    import random
+    from tachyon_amd.kzg import KZG
+    n = 1 << 12
+    kzg = KZG("bn254_g1")
+    kzg.unsafe_setup(n, pyref.Field("bn254_fr").to_bytes(991))
+    powers = kzg.g1_powers_of_tau()
+    rng = random.Random(5)
+    big = O.gen_scalars("bn254_fr", 31, n).tobytes()
+    pool = O.gen_scalars("bn254_fr", 32, 4096).tobytes()
+    polys = [pool[32 * rng.randrange(0, 2000):][:32 * rng.randrange(1, 41)] for _ in range(60)]
+    polys.insert(17, big)
+    got = kzg.commit_batch(polys)
+    assert got == [O.msm("bn254_g1", powers[:len(p) * 2], p)[0] for p in polys]
+    tiny = [pool[32 * (i % 4000):][:96] for i in range(4500)]
+    got = kzg.commit_batch(tiny)
+    assert len(got) == 4500
+    for i in range(0, 4500, 7):
+        assert got[i] == O.msm("bn254_g1", powers[:192], tiny[i])[0], i
+    assert got[4000] == got[0] and got[4499] == got[499]
+    kzg.close()

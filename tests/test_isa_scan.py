@@ -41,8 +41,9 @@ def test_scanner_flags_a_carry_mask_multiplicand():
 
 
 def test_generated_asm_outputs_are_early_clobber():
-    for name in ("f29_asm.h", "mont_asm.h"):
+    for name in ("f29_asm.h", "mont_asm.h", "f28_asm.h", "fr29_gen.h"):
         text = open(os.path.join(ROOT, "tachyon_amd", "csrc", "field", name)).read()
+        assert '"=&s"' in text, name  # the carry-out SGPR pairs are declared early-clobber
         assert not re.search(r'"=s"\(', text), name
         assert not re.search(r'"\+v"\(acc\)', text), name
 
