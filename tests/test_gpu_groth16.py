@@ -209,6 +209,15 @@ def test_multi_device_prover(curve, log_n, devices):
     assert list(prover.prove(fb, Fr.to_bytes(r_int), Fr.to_bytes(s_int))) == list(OG.prove(zk, full, r_int, s_int))
     with pytest.raises(ValueError):
         prover.set_devices([0, 4096])
+    # a device-resident assignment (a CUDA tensor): every device's prover
+    # copies it into its own HBM before its kernels read it
+    import numpy as np
+    import torch
+    d_full = torch.from_numpy(np.frombuffer(fb, dtype=np.uint8).copy()).cuda()
+    prover.set_profile(True)  # forwarded to the per-device provers
+    assert list(prover.prove(d_full)) == list(OG.prove(zk, full))
+    assert prover.last_timings()["total"] > 0  # the lead device's phases
+    prover.set_profile(False)
     prover.set_devices([])
     assert list(prover.prove(fb)) == list(OG.prove(zk, full))
     prover.close()
