@@ -361,6 +361,17 @@ TACHYON_C_EXPORT void* tachyon_mi355x_msm_gpu_create(int curve, void* stream);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_destroy(int curve, void* ctx);
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void* bases, size_t bases_size,
                                                const void* scalars, size_t scalars_size, int form, void* out);
+/* _run_points: the same with bases given in `base_form` -- 0 affine {x,y}, 1
+ * projective {x,y,z} (x/z, y/z), 2 jacobian {x,y,z} (x/z^2, y/z^3), 3 xyzz
+ * {x,y,zz,zzz} (x/zz, y/zzz); z (zz) = 0 is the identity -- normalised to
+ * affine on the device by batch inversion first: VariableBaseMSM<Point> for
+ * the non-affine point types the reference instantiates
+ * (variable_base_msm_unittest.cc:30-33; Bucket = the point's own add type,
+ * pippenger_base.h:18-28).  Returns 1, or 0 (out untouched) on a size
+ * mismatch. */
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_run_points(int curve, void* ctx, const void* bases, size_t bases_size,
+                                                      int base_form, const void* scalars, size_t scalars_size,
+                                                      int form, void* out);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c);
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule).

@@ -120,6 +120,7 @@ SIGNATURES = [
     ("tachyon_mi355x_msm_gpu_create", vp, [i32, vp]),
     ("tachyon_mi355x_msm_gpu_destroy", None, [i32, vp]),
     ("tachyon_mi355x_msm_gpu_run", i32, [i32, vp, vp, sz, vp, sz, i32, vp]),
+    ("tachyon_mi355x_msm_gpu_run_points", i32, [i32, vp, vp, sz, i32, vp, sz, i32, vp]),
     ("tachyon_mi355x_msm_gpu_set_window_bits", None, [i32, vp, ctypes.c_uint]),
     ("tachyon_mi355x_msm_gpu_set_profile", None, [i32, vp, i32]),
     ("tachyon_mi355x_msm_gpu_set_variant", i32, [i32, vp, i32]),

@@ -204,6 +204,16 @@ void msm_form_out(void* ctx, const void* bases, const void* scalars, size_t n, i
   }
 }
 
+// Non-affine bases (VariableBaseMSM<ProjectivePoint / JacobianPoint /
+// PointXYZZ>): normalised to affine on the device, then the MSM above
+template <class Curve>
+void msm_points_form_out(void* ctx, const void* bases, int base_form, const void* scalars, size_t n, int form,
+                         void* out) {
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  const void* aff = c->impl.affine_bases(bases, n, base_form);
+  msm_form_out<Curve>(ctx, aff, scalars, n, form, out);
+}
+
 template <class Curve>
 void affine_sum(const void* pts, size_t count, void* out) {
   using F = typename Curve::F;
@@ -397,6 +407,13 @@ int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void* bases, size_t b
                                size_t scalars_size, int form, void* out) {
   if (bases_size != scalars_size) return 0;  // IcicleMSM::Run / PippengerAdapter: sizes must match
   GUARD_BEGIN CURVE_DISPATCH(curve, msm_form_out<C>(ctx, bases, scalars, scalars_size, form, out)) GUARD_END
+  return 1;
+}
+int tachyon_mi355x_msm_gpu_run_points(int curve, void* ctx, const void* bases, size_t bases_size, int base_form,
+                                      const void* scalars, size_t scalars_size, int form, void* out) {
+  if (bases_size != scalars_size) return 0;
+  GUARD_BEGIN CURVE_DISPATCH(curve, msm_points_form_out<C>(ctx, bases, base_form, scalars, scalars_size, form, out))
+  GUARD_END
   return 1;
 }
 void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ctx, unsigned c) {

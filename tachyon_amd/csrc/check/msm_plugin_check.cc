@@ -16,7 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../../include/tachyon_mi355x_msm.h"
@@ -44,6 +46,106 @@ struct DeviceSpan {  // absl::Span-like view of device memory
   const T* data() const { return ptr; }
   size_t size() const { return len; }
 };
+
+// Base-field products on the device (tachyon_mi355x_field_op op 2) of
+// `count` elements of `fq` bytes each; field 0 = BN254 Fq, 2 = BLS12-381 Fq.
+std::vector<unsigned char> fq_mul(int field, size_t fq, const std::vector<unsigned char>& a,
+                                  const std::vector<unsigned char>& b) {
+  std::vector<unsigned char> out(a.size());
+  tachyon_mi355x_field_op(field, 2, a.data(), b.data(), out.data(), a.size() / fq);
+  return out;
+}
+
+// VariableBaseMSM<Point> over projective, Jacobian and XYZZ bases
+// (variable_base_msm_unittest.cc:30-33): the affine bases re-expressed with a
+// per-point z in Fq (Fq2 groups: z = (z, 0), so coordinates scale componentwise)
+// taken from the scalar bytes, and every 37th point (i % 37 == 3) the identity
+// (z = 0).  Bucket = the base's own form.  All three results must equal the
+// affine-input MSM over the same bases with those points zeroed; that bucket's
+// bytes are printed for the oracle check.
+template <typename Point, typename Scalar, int kGroup>
+bool check_non_affine(const std::vector<Point>& bases, const std::vector<Scalar>& scalars, std::string* json) {
+  constexpr size_t kC = tachyon_mi355x::kCoordBytes[kGroup];
+  constexpr bool kG2 = kGroup == tachyon_mi355x::kBn254G2 || kGroup == tachyon_mi355x::kBls12_381G2;
+  constexpr size_t kFq = kG2 ? kC / 2 : kC;
+  constexpr int kFqField = (kGroup == tachyon_mi355x::kBn254G1 || kGroup == tachyon_mi355x::kBn254G2) ? 0 : 2;
+  const size_t n = bases.size();
+  const size_t comps = kG2 ? 2 : 1;
+  // z per point (one Fq), and its square and cube
+  std::vector<unsigned char> z(n * kFq, 0);
+  for (size_t i = 0; i < n; ++i)
+    if (i % 37 != 3) std::memcpy(&z[i * kFq], &scalars[i], 32);  // < r < q: a valid Montgomery Fq
+  const std::vector<unsigned char> z2 = fq_mul(kFqField, kFq, z, z), z3 = fq_mul(kFqField, kFq, z2, z);
+  // coordinate c (0 = x, 1 = y) of every base as n x comps Fq elements, times a per-point factor
+  auto scaled = [&](int c, const std::vector<unsigned char>& f) {
+    std::vector<unsigned char> a(n * comps * kFq), b(n * comps * kFq);
+    for (size_t i = 0; i < n; ++i)
+      for (size_t k = 0; k < comps; ++k) {
+        std::memcpy(&a[(i * comps + k) * kFq], reinterpret_cast<const unsigned char*>(&bases[i]) + c * kC + k * kFq, kFq);
+        std::memcpy(&b[(i * comps + k) * kFq], &f[i * kFq], kFq);
+      }
+    return fq_mul(kFqField, kFq, a, b);
+  };
+  // a coordinate equal to z^e in Fq, embedded as (z^e, 0) for Fq2
+  auto embed = [&](const std::vector<unsigned char>& f) {
+    std::vector<unsigned char> v(n * kC, 0);
+    for (size_t i = 0; i < n; ++i) std::memcpy(&v[i * kC], &f[i * kFq], kFq);
+    return v;
+  };
+  auto pack = [&](std::initializer_list<const std::vector<unsigned char>*> coords) {
+    std::vector<unsigned char> v(n * coords.size() * kC);
+    for (size_t i = 0; i < n; ++i) {
+      size_t j = 0;
+      for (const auto* c : coords) std::memcpy(&v[(i * coords.size() + j++) * kC], &(*c)[i * kC], kC);
+    }
+    return v;
+  };
+  const auto xz = scaled(0, z), yz = scaled(1, z), xz2 = scaled(0, z2), yz3 = scaled(1, z3);
+  const auto ez = embed(z), ez2 = embed(z2), ez3 = embed(z3);
+  struct P3 { unsigned char b[3 * kC]; };
+  struct P4 { unsigned char b[4 * kC]; };
+  using CProj = std::conditional_t<kGroup == tachyon_mi355x::kBn254G1, tachyon_bn254_g1_projective,
+                std::conditional_t<kGroup == tachyon_mi355x::kBn254G2, tachyon_bn254_g2_projective,
+                std::conditional_t<kGroup == tachyon_mi355x::kBls12_381G1, tachyon_bls12_381_g1_projective,
+                                   tachyon_bls12_381_g2_projective>>>;
+  using CJac = std::conditional_t<kGroup == tachyon_mi355x::kBn254G1, tachyon_bn254_g1_jacobian,
+               std::conditional_t<kGroup == tachyon_mi355x::kBn254G2, tachyon_bn254_g2_jacobian,
+               std::conditional_t<kGroup == tachyon_mi355x::kBls12_381G1, tachyon_bls12_381_g1_jacobian,
+                                  tachyon_bls12_381_g2_jacobian>>>;
+  using CXyzz = std::conditional_t<kGroup == tachyon_mi355x::kBn254G1, tachyon_bn254_g1_xyzz,
+                std::conditional_t<kGroup == tachyon_mi355x::kBn254G2, tachyon_bn254_g2_xyzz,
+                std::conditional_t<kGroup == tachyon_mi355x::kBls12_381G1, tachyon_bls12_381_g1_xyzz,
+                                   tachyon_bls12_381_g2_xyzz>>>;
+  auto as_points = [&](const std::vector<unsigned char>& raw, auto tag) {
+    using T = decltype(tag);
+    std::vector<T> v(n);
+    std::memcpy(v.data(), raw.data(), raw.size());
+    return v;
+  };
+  const auto proj = as_points(pack({&xz, &yz, &ez}), CProj{});
+  const auto jac = as_points(pack({&xz2, &yz3, &ez}), CJac{});
+  const auto xyzz = as_points(pack({&xz2, &yz3, &ez2, &ez3}), CXyzz{});
+  std::vector<Point> zeroed = bases;
+  for (size_t i = 3; i < n; i += 37) std::memset(&zeroed[i], 0, sizeof(Point));
+
+  tachyon_mi355x::VariableBaseMSM<Point> m_aff;
+  tachyon_mi355x::VariableBaseMSM<CProj> m_proj;
+  tachyon_mi355x::VariableBaseMSM<CJac> m_jac;
+  tachyon_mi355x::VariableBaseMSM<CXyzz> m_xyzz;
+  P4 want{}, got_x{};
+  P3 got_p{}, got_j{};
+  bool ok = m_aff.Run(zeroed, scalars, &want) && m_proj.Run(proj, scalars, &got_p) && m_jac.Run(jac, scalars, &got_j) &&
+            m_xyzz.Run(xyzz.begin(), xyzz.end(), scalars.begin(), scalars.end(), &got_x);
+  // normalised results: x, y equal across forms; z = zz = zzz = the affine bucket's zz
+  ok = ok && std::memcmp(&got_x, &want, sizeof(want)) == 0 && std::memcmp(&got_p, &want, 3 * kC) == 0 &&
+       std::memcmp(&got_j, &want, 3 * kC) == 0;
+  // a size mismatch stays false for the non-affine path too
+  P3 untouched{};
+  std::vector<CProj> shorter(proj.begin(), proj.end() - 1);
+  ok = ok && !m_proj.Run(shorter, scalars, &untouched);
+  *json += ", \"non_affine_ok\": " + std::string(ok ? "true" : "false") + ", \"zeroed_xyzz\": \"" + hex(want) + "\"";
+  return ok;
+}
 
 template <typename Point, typename Scalar, int kField, int kGroup>
 bool check_group(size_t n, uint64_t seed, hipStream_t stream, std::string* json) {
@@ -94,8 +196,10 @@ bool check_group(size_t n, uint64_t seed, hipStream_t stream, std::string* json)
            mismatch_false ? "true" : "false");
   *json += head;
   *json += "\"projective\": \"" + hex(proj) + "\", \"xyzz\": \"" + hex(bucket) + "\", \"empty_xyzz\": \"" +
-           hex(empty) + "\"}";
-  return ok;
+           hex(empty) + "\"";
+  const bool ok_na = check_non_affine<Point, Scalar, kGroup>(bases, scalars, json);
+  *json += "}";
+  return ok && ok_na;
 }
 
 }  // namespace

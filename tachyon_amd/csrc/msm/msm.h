@@ -182,6 +182,11 @@ class MsmGpu {
   // results of ranges that tile [0, W) gives run(); multi-GPU window split.
   Point run_window_range(const void* bases, const void* scalars, size_t n, unsigned w_begin, unsigned w_end);
 
+  // Bases given as projective (form 1), Jacobian (2) or XYZZ (3) points (host or
+  // device) normalised to affine on the device; returns the device array of n
+  // affine points (valid until the next call).  Form 0 returns `bases` as is.
+  const Aff* affine_bases(const void* bases, size_t n, int form);
+
   static Point combine_windows(const std::vector<Point>& window_sums, unsigned c);
   // Mixed additions per second (G/s) of this curve's accumulation field code
   // in registers on the current device -- no gathers, no run logic: the VALU
@@ -257,6 +262,7 @@ class MsmGpu {
   hipEvent_t copy_done_ = nullptr;
   std::vector<hipEvent_t> chunk_ev_;  // host-resident pipeline: chunk k uploaded
   DeviceBuffer hist_, hscan_tmp_;
+  DeviceBuffer norm_in_, norm_out_, norm_prefix_;  // affine_bases
   DeviceBuffer maxlen_, lofs_;  // lofs_: every join level's output offsets
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket
   unsigned last_levels_ = 0;

@@ -280,6 +280,53 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
 }
 
 // ---------------------------------------------------------------------------
+// Non-affine bases -> affine (VariableBaseMSM<ProjectivePoint / JacobianPoint /
+// PointXYZZ>, variable_base_msm_unittest.cc:30-33): Montgomery's trick per
+// thread over `chunk` consecutive points -- the denominators' prefix products
+// to `prefix`, one inversion, then the backward pass.  form 1 projective
+// {X, Y, Z}: (X/Z, Y/Z); 2 Jacobian {X, Y, Z}: (X/Z^2, Y/Z^3); 3 XYZZ
+// {X, Y, ZZ, ZZZ}: (X (ZZ/ZZZ)^2, Y/ZZZ) (point_xyzz.h:199-212, ZZ^3 = ZZZ^2).
+// A zero denominator is the identity -> (0, 0).  Canonical outputs.
+template <class F>
+__global__ __launch_bounds__(kBlock) void points_to_affine_kernel(const F* __restrict__ in, int form,
+                                                                  Affine<F>* __restrict__ out,
+                                                                  F* __restrict__ prefix, size_t n, uint32_t chunk) {
+  const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const size_t s = t * chunk;
+  if (s >= n) return;
+  const size_t e = s + chunk < n ? s + chunk : n;
+  const unsigned stride = form == 3 ? 4 : 3;  // coordinates per input point
+  const unsigned den = form == 3 ? 3 : 2;     // the denominator's coordinate
+  F prod = F::one();
+  for (size_t i = s; i < e; ++i) {
+    const F d = in[i * stride + den];
+    if (!d.is_zero()) prod = prod * d;
+    prefix[i] = prod;
+  }
+  F inv = prod.inverse();  // product of the non-zero denominators
+  for (size_t i = e; i-- > s;) {
+    const F* p = in + i * stride;
+    const F d = p[den];
+    if (d.is_zero()) {
+      out[i] = Affine<F>::zero();
+      continue;
+    }
+    const F dinv = i > s ? inv * prefix[i - 1] : inv;
+    inv = inv * d;
+    Affine<F> a;
+    if (form == 1) {
+      a = {p[0] * dinv, p[1] * dinv};
+    } else if (form == 2) {
+      const F d2 = dinv.sqr();
+      a = {p[0] * d2, p[1] * (d2 * dinv)};
+    } else {
+      a = {p[0] * (p[2] * dinv).sqr(), p[1] * dinv};
+    }
+    out[i] = a.canonical();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Load-balanced bucket accumulation.
 //
 // The per-window sorted (bucket, point) lists are one array of W*n entries,
@@ -2641,6 +2688,27 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run(const void* bases, const void* 
     total = total + combine_windows(ws, plan.c);
   }
   return total;
+}
+
+template <class Curve>
+const typename MsmGpu<Curve>::Aff* MsmGpu<Curve>::affine_bases(const void* bases, size_t n, int form) {
+  if (form < 0 || form > 3) throw std::runtime_error("tachyon_mi355x: base form must be 0 affine, 1 projective, 2 jacobian or 3 xyzz");
+  if (form == 0 || n == 0) return static_cast<const Aff*>(bases);
+  const size_t in_bytes = n * (form == 3 ? 4 : 3) * sizeof(F);
+  const F* d_in = static_cast<const F*>(bases);
+  if (!is_device_pointer(bases)) {
+    d_in = static_cast<const F*>(norm_in_.ensure(in_bytes));
+    TA_HIP(hipMemcpyAsync(const_cast<F*>(d_in), bases, in_bytes, hipMemcpyHostToDevice, stream_));
+  }
+  Aff* out = static_cast<Aff*>(norm_out_.ensure(n * sizeof(Aff)));
+  F* prefix = static_cast<F*>(norm_prefix_.ensure(n * sizeof(F)));
+  constexpr uint32_t kChunk = 16;
+  const size_t threads = (n + kChunk - 1) / kChunk;
+  hipLaunchKernelGGL(detail::points_to_affine_kernel<F>, dim3(ceil_div(threads, detail::kBlock)), dim3(detail::kBlock),
+                     0, stream_, d_in, form, out, prefix, n, kChunk);
+  TA_HIP(hipGetLastError());
+  TA_HIP(hipStreamSynchronize(stream_));  // the caller may hand the array to another device's stream
+  return out;
 }
 
 // `count` MSMs over the same `len` device-resident bases in one recode, sort,

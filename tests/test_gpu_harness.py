@@ -189,3 +189,14 @@ def test_msm_cpp_plugin_boundary(log_n):
             assert proj == want + one
             assert xyzz == want + one + one
         assert bytes.fromhex(g["empty_xyzz"]) == one + one + zero + zero
+        # VariableBaseMSM<Projective / Jacobian / XYZZ bases> (the check requires
+        # all three to equal this affine-input bucket): the oracle's MSM over the
+        # same bases with every 37th point (i % 37 == 3) the identity
+        assert g["non_affine_ok"], (curve, g)
+        pb = 2 * cb
+        bases = bytearray(O.gen_bases(curve, seed, n, 16).tobytes())
+        for i in range(3, n, 37):
+            bases[i * pb:(i + 1) * pb] = bytes(pb)
+        want0 = O.msm(curve, bytes(bases), O.gen_scalars(sf, seed, n).tobytes())[0]
+        z0 = bytes.fromhex(g["zeroed_xyzz"])
+        assert z0 == (one + one + zero + zero if want0 == bytes(pb) else want0 + one + one), curve
