@@ -306,6 +306,50 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4*
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_synchronize(tachyon_mi355x_bn254_ntt4* plan);
 TACHYON_C_EXPORT void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn254_ntt4* plan);
 
+/* ---- communicators and library-level sharded entry points ------------------
+ * One process per MI355X: a multi-process C/C++ caller (benchmark/msm/
+ * msm_benchmark_gpu.cc:57-69 or vendors/circom/prover_main.cc:116-128 under a
+ * launcher) hands the library a communicator and the library does the
+ * exchange itself.  Backends:
+ *   rccl -- RCCL over xGMI: _comm_init_rccl (ncclCommInitRank on the current
+ *     device from a 128-byte ncclUniqueId that rank 0 got from
+ *     _comm_unique_id and shared) or _comm_from_rccl (wrap the caller's
+ *     ncclComm_t, not owned).  All-gathers are ncclAllGather, the NTT
+ *     all-to-all one ncclGroupStart/End of ncclSend/ncclRecv pairs on the
+ *     plan's stream.
+ *   host -- the HOST-STAGED FALLBACK (_comm_create_host): two callbacks
+ *     exchange host buffers (all_gather: every rank's `bytes` in rank order;
+ *     all_to_all: world blocks of `bytes`, block h to / from rank h); device
+ *     data are staged through the host.  For ranks RCCL refuses (two ranks on
+ *     one GPU: "Duplicate GPU detected") and CPU rehearsal backends (gloo). */
+typedef struct tachyon_mi355x_comm tachyon_mi355x_comm;
+typedef int (*tachyon_mi355x_all_gather_fn)(void* user, const void* send, void* recv, size_t bytes);
+typedef int (*tachyon_mi355x_all_to_all_fn)(void* user, const void* send, void* recv, size_t bytes);
+/* writes the 128-byte ncclUniqueId to out (cap >= 128); returns its size or 0 */
+TACHYON_C_EXPORT int tachyon_mi355x_comm_unique_id(void* out, size_t cap);
+TACHYON_C_EXPORT tachyon_mi355x_comm* tachyon_mi355x_comm_init_rccl(const void* unique_id, int world, int rank);
+TACHYON_C_EXPORT tachyon_mi355x_comm* tachyon_mi355x_comm_from_rccl(void* nccl_comm);
+TACHYON_C_EXPORT tachyon_mi355x_comm* tachyon_mi355x_comm_create_host(int world, int rank,
+                                                                     tachyon_mi355x_all_gather_fn all_gather,
+                                                                     tachyon_mi355x_all_to_all_fn all_to_all,
+                                                                     void* user);
+TACHYON_C_EXPORT void tachyon_mi355x_comm_destroy(tachyon_mi355x_comm* comm);
+/* every rank's `bytes` of host memory, gathered in rank order into recv
+ * (world x bytes): the exchange the sharded entries use, for callers that
+ * combine their own partial results */
+TACHYON_C_EXPORT void tachyon_mi355x_comm_all_gather(tachyon_mi355x_comm* comm, const void* send, void* recv,
+                                                    size_t bytes);
+TACHYON_C_EXPORT int tachyon_mi355x_comm_world(const tachyon_mi355x_comm* comm);
+TACHYON_C_EXPORT int tachyon_mi355x_comm_rank(const tachyon_mi355x_comm* comm);
+TACHYON_C_EXPORT const char* tachyon_mi355x_comm_backend(const tachyon_mi355x_comm* comm);
+/* The four-step NTT of this rank's slab: stage 1, the all-to-all over `comm`,
+ * stage 2 (layouts as _ntt4_stage; plan world/rank must be comm's).  Ordered
+ * on the plan's stream; d_out is ready there (the host backend returns with
+ * the exchange done and stage 2 enqueued). */
+TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_run(tachyon_mi355x_bn254_ntt4* plan, tachyon_mi355x_comm* comm,
+                                                   int inverse, const tachyon_bn254_fr* d_in,
+                                                   tachyon_bn254_fr* d_out);
+
 /* G2 MSM contexts (Groth16's B-in-G2, BLS12-381 config 4); same semantics as
  * the G1 *_msm_gpu entry points. */
 typedef struct tachyon_bn254_g2_msm_gpu* tachyon_bn254_g2_msm_gpu_ptr;
@@ -369,6 +413,14 @@ TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void
  * (variable_base_msm_unittest.cc:30-33; Bucket = the point's own add type,
  * pippenger_base.h:18-28).  Returns 1, or 0 (out untouched) on a size
  * mismatch. */
+/* _sharded_affine: this rank's shard (bases / scalars of `size` points, host
+ * or device; 0 allowed) over `comm`: the local partial, one all-gather of
+ * every rank's partial, the group sum in rank order -- every rank writes the
+ * whole MSM's affine result (the kParallelTerm split, pippenger_adapter.h:82-113,
+ * across processes). */
+TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_sharded_affine(int curve, void* ctx, tachyon_mi355x_comm* comm,
+                                                           const void* bases, const void* scalars, size_t size,
+                                                           void* out_affine);
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_run_points(int curve, void* ctx, const void* bases, size_t bases_size,
                                                       int base_form, const void* scalars, size_t scalars_size,
                                                       int form, void* out);
@@ -504,6 +556,14 @@ TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_partials(tachyon_mi355x_groth
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_assemble(tachyon_mi355x_groth16_prover* prover, const void* parts,
                                                       size_t world, const void* r, const void* s, void* out_a,
                                                       void* out_b, void* out_c);
+/* The proof across the ranks of `comm` (one process per GPU): every rank runs
+ * the witness map and its chunk of every MSM (_prove_partials with the
+ * comm's rank / world), one all-gather of the partials blobs, and the same
+ * assembly -- every rank writes the same proof, equal to the single-GPU one. */
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_sharded(tachyon_mi355x_groth16_prover* prover,
+                                                          tachyon_mi355x_comm* comm, const void* full, size_t count,
+                                                          const void* r, const void* s, void* out_a, void* out_b,
+                                                          void* out_c);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                          size_t count, void* out_h);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on);

@@ -27,6 +27,8 @@ _lib = None
 # (name, restype, argtypes) of every entry point declared in include/tachyon_mi355x.h
 vp, sz, i32, u8, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint8, ctypes.c_uint64
 fp = ctypes.POINTER(ctypes.c_float)
+# tachyon_mi355x_all_gather_fn / _all_to_all_fn: (user, send, recv, bytes) -> 0 on success
+COMM_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 SIGNATURES = [
     # reference C-ABI: MSM
     ("tachyon_bn254_g1_init", None, []),
@@ -161,6 +163,19 @@ SIGNATURES = [
     ("tachyon_mi355x_kzg_commit", i32, [vp, i32, vp, sz, vp]),
     ("tachyon_mi355x_kzg_commit_batch", i32, [vp, i32, ctypes.POINTER(ctypes.c_void_p),
                                               ctypes.POINTER(ctypes.c_size_t), sz, vp]),
+    # communicators and library-level sharded entry points
+    ("tachyon_mi355x_comm_unique_id", i32, [vp, sz]),
+    ("tachyon_mi355x_comm_init_rccl", vp, [vp, i32, i32]),
+    ("tachyon_mi355x_comm_from_rccl", vp, [vp]),
+    ("tachyon_mi355x_comm_create_host", vp, [i32, i32, COMM_FN, COMM_FN, vp]),
+    ("tachyon_mi355x_comm_destroy", None, [vp]),
+    ("tachyon_mi355x_comm_all_gather", None, [vp, vp, vp, sz]),
+    ("tachyon_mi355x_comm_world", i32, [vp]),
+    ("tachyon_mi355x_comm_rank", i32, [vp]),
+    ("tachyon_mi355x_comm_backend", ctypes.c_char_p, [vp]),
+    ("tachyon_mi355x_msm_gpu_sharded_affine", None, [i32, vp, vp, vp, vp, sz, vp]),
+    ("tachyon_mi355x_bn254_ntt4_run", None, [vp, vp, i32, vp, vp]),
+    ("tachyon_mi355x_groth16_prove_sharded", None, [vp, vp, vp, sz, vp, vp, vp, vp, vp]),
     ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
     ("tachyon_mi355x_version", ctypes.c_char_p, []),
     ("tachyon_mi355x_device_count", i32, []),

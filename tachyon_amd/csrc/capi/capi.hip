@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "../dist/comm.h"
 #include "../msm/msm.h"
 #include "../msm/msm_multi.h"
 #include "../ntt/ntt.h"
@@ -214,6 +215,24 @@ void msm_points_form_out(void* ctx, const void* bases, int base_form, const void
   msm_form_out<Curve>(ctx, aff, scalars, n, form, out);
 }
 
+// One rank's shard of an MSM over a communicator: the local XYZZ partial,
+// one all-gather of every rank's partial, the group sum in rank order (the
+// same point on every rank) -- the kParallelTerm chunk-and-sum
+// (pippenger_adapter.h:82-113) across processes, with the exchange inside
+// the library (tachyon_amd.dist.sharded_msm is the torch.distributed form)
+template <class Curve>
+void msm_sharded_out(void* ctx, dist::Comm* comm, const void* bases, const void* scalars, size_t n, void* out) {
+  using F = typename Curve::F;
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  const XYZZ<F> part = c->run(bases, scalars, n);
+  std::vector<XYZZ<F>> all((size_t)comm->world());
+  comm->all_gather_host(&part, all.data(), sizeof(part));
+  XYZZ<F> acc = XYZZ<F>::zero();
+  for (const auto& p : all) acc = acc + p;
+  const Affine<F> a = acc.to_affine();
+  memcpy(out, &a, sizeof(a));
+}
+
 template <class Curve>
 void affine_sum(const void* pts, size_t count, void* out) {
   using F = typename Curve::F;
@@ -408,6 +427,13 @@ int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void* bases, size_t b
   if (bases_size != scalars_size) return 0;  // IcicleMSM::Run / PippengerAdapter: sizes must match
   GUARD_BEGIN CURVE_DISPATCH(curve, msm_form_out<C>(ctx, bases, scalars, scalars_size, form, out)) GUARD_END
   return 1;
+}
+void tachyon_mi355x_msm_gpu_sharded_affine(int curve, void* ctx, tachyon_mi355x_comm* comm, const void* bases,
+                                           const void* scalars, size_t size, void* out_affine) {
+  GUARD_BEGIN
+  if (!comm || !comm->impl) throw std::runtime_error("null communicator");
+  CURVE_DISPATCH(curve, msm_sharded_out<C>(ctx, comm->impl.get(), bases, scalars, size, out_affine))
+  GUARD_END
 }
 int tachyon_mi355x_msm_gpu_run_points(int curve, void* ctx, const void* bases, size_t bases_size, int base_form,
                                       const void* scalars, size_t scalars_size, int form, void* out) {
@@ -914,6 +940,7 @@ int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timings(const tachyon
 
 struct tachyon_mi355x_bn254_ntt4 {
   ntt::Ntt4Step<Bn254Fr>* impl;
+  DeviceBuffer send, recv;  // tachyon_mi355x_bn254_ntt4_run's exchange buffers
 };
 tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create(uint32_t log_n, uint32_t log_world, uint32_t rank,
                                                            void* stream) {
@@ -938,6 +965,73 @@ void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4* plan, int stage,
   else (stage == 1) ? plan->impl->inverse_stage1(in, out) : plan->impl->inverse_stage2(in, out);
   GUARD_END
 }
+// Both stages and the all-to-all between them, on the plan's stream (RCCL:
+// no host synchronisation; the host-staged communicator synchronises it)
+void tachyon_mi355x_bn254_ntt4_run(tachyon_mi355x_bn254_ntt4* plan, tachyon_mi355x_comm* comm, int inverse,
+                                   const tachyon_bn254_fr* d_in, tachyon_bn254_fr* d_out) {
+  GUARD_BEGIN
+  if (!comm || !comm->impl) throw std::runtime_error("null communicator");
+  auto& p = *plan->impl;
+  if ((uint32_t)comm->impl->world() != p.world() || (uint32_t)comm->impl->rank() != p.rank())
+    throw std::runtime_error("tachyon_mi355x: ntt4 plan world/rank differ from the communicator's");
+  const size_t bytes = p.local_size() * sizeof(Bn254Fr);
+  Bn254Fr* send = static_cast<Bn254Fr*>(plan->send.ensure(bytes));
+  Bn254Fr* recv = static_cast<Bn254Fr*>(plan->recv.ensure(bytes));
+  const Bn254Fr* in = reinterpret_cast<const Bn254Fr*>(d_in);
+  Bn254Fr* out = reinterpret_cast<Bn254Fr*>(d_out);
+  if (!inverse) p.forward_stage1(in, send);
+  else p.inverse_stage1(in, send);
+  comm->impl->all_to_all_device(send, recv, bytes / p.world(), p.stream());
+  if (!inverse) p.forward_stage2(recv, out);
+  else p.inverse_stage2(recv, out);
+  GUARD_END
+}
+
+// ---- communicators (dist/comm.h) ----
+int tachyon_mi355x_comm_unique_id(void* out, size_t cap) {
+  if (cap < sizeof(ncclUniqueId)) return 0;
+  GUARD_BEGIN
+  const ncclUniqueId id = dist::rccl_unique_id();
+  memcpy(out, &id, sizeof(id));
+  return (int)sizeof(id);
+  GUARD_END
+  return 0;
+}
+tachyon_mi355x_comm* tachyon_mi355x_comm_init_rccl(const void* unique_id, int world, int rank) {
+  GUARD_BEGIN
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof(id));
+  auto* c = new tachyon_mi355x_comm();
+  c->impl = std::make_unique<dist::RcclComm>(id, world, rank);
+  return c;
+  GUARD_END
+  return nullptr;
+}
+tachyon_mi355x_comm* tachyon_mi355x_comm_from_rccl(void* nccl_comm) {
+  GUARD_BEGIN
+  auto* c = new tachyon_mi355x_comm();
+  c->impl = std::make_unique<dist::RcclComm>(static_cast<ncclComm_t>(nccl_comm));
+  return c;
+  GUARD_END
+  return nullptr;
+}
+tachyon_mi355x_comm* tachyon_mi355x_comm_create_host(int world, int rank, tachyon_mi355x_all_gather_fn all_gather,
+                                                     tachyon_mi355x_all_to_all_fn all_to_all, void* user) {
+  GUARD_BEGIN
+  auto* c = new tachyon_mi355x_comm();
+  c->impl = std::make_unique<dist::HostComm>(world, rank, all_gather, all_to_all, user);
+  return c;
+  GUARD_END
+  return nullptr;
+}
+void tachyon_mi355x_comm_destroy(tachyon_mi355x_comm* comm) { delete comm; }
+void tachyon_mi355x_comm_all_gather(tachyon_mi355x_comm* comm, const void* send, void* recv, size_t bytes) {
+  GUARD_BEGIN comm->impl->all_gather_host(send, recv, bytes); GUARD_END
+}
+int tachyon_mi355x_comm_world(const tachyon_mi355x_comm* comm) { return comm->impl->world(); }
+int tachyon_mi355x_comm_rank(const tachyon_mi355x_comm* comm) { return comm->impl->rank(); }
+const char* tachyon_mi355x_comm_backend(const tachyon_mi355x_comm* comm) { return comm->impl->backend(); }
+
 void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn254_ntt4* plan) {
   return static_cast<void*>(plan->impl->stream());
 }

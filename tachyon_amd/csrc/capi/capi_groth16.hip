@@ -13,6 +13,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "../dist/comm.h"
 #include "../groth16/groth16.h"
 
 using namespace tachyon_amd;
@@ -109,6 +110,26 @@ void multi_prove_into(P* primary, std::vector<std::unique_ptr<P>>& provs, const 
   for (auto& e : err)
     if (e) std::rethrow_exception(e);
   auto proof = primary->assemble(parts.data(), N, static_cast<const Fr*>(r), static_cast<const Fr*>(s));
+  memcpy(a, &proof.a, sizeof(proof.a));
+  memcpy(b, &proof.b, sizeof(proof.b));
+  memcpy(c, &proof.c, sizeof(proof.c));
+}
+
+// One rank's share of a proof over a communicator: the witness map and this
+// rank's chunk of every MSM (partials), one all-gather of the fixed-size
+// partials blobs, and the same assembly on every rank -- the multi-process
+// form of multi_prove_into with the exchange inside the library
+// (Groth16Prover.prove_sharded in tachyon_amd/groth16.py is the torch.distributed form)
+template <class P>
+void sharded_prove_into(P* p, dist::Comm* comm, const void* full, size_t count, const void* r, const void* s, void* a,
+                        void* b, void* c) {
+  using Fr = typename P::Fr;
+  using Parts = PartialsOf<P*>;
+  const uint32_t world = (uint32_t)comm->world(), rank = (uint32_t)comm->rank();
+  const Parts mine = p->partials(static_cast<const Fr*>(full), count, r != nullptr, rank, world);
+  std::vector<Parts> all(world);
+  comm->all_gather_host(&mine, all.data(), sizeof(Parts));
+  auto proof = p->assemble(all.data(), world, static_cast<const Fr*>(r), static_cast<const Fr*>(s));
   memcpy(a, &proof.a, sizeof(proof.a));
   memcpy(b, &proof.b, sizeof(proof.b));
   memcpy(c, &proof.c, sizeof(proof.c));
@@ -212,6 +233,15 @@ void tachyon_mi355x_groth16_prove(tachyon_mi355x_groth16_prover* prover, const v
     return;
   }
   PROVER_DISPATCH(prover, prove_into(impl, full, count, r, s, out_a, out_b, out_c));
+  GUARD_END
+}
+
+void tachyon_mi355x_groth16_prove_sharded(tachyon_mi355x_groth16_prover* prover, tachyon_mi355x_comm* comm,
+                                          const void* full, size_t count, const void* r, const void* s, void* out_a,
+                                          void* out_b, void* out_c) {
+  GUARD_BEGIN
+  if (!comm || !comm->impl) throw std::runtime_error("null communicator");
+  PROVER_DISPATCH(prover, sharded_prove_into(impl, comm->impl.get(), full, count, r, s, out_a, out_b, out_c));
   GUARD_END
 }
 

@@ -162,6 +162,8 @@ class Ntt4Step {
   Ntt4Step& operator=(const Ntt4Step&) = delete;
 
   size_t local_size() const { return n_ >> log_g_; }
+  uint32_t world() const { return 1u << log_g_; }
+  uint32_t rank() const { return rank_; }
   uint32_t log_rows() const { return log_r_; }
   const Fr& root() const { return w_; }  // w_n of the plan (the generator set active at construction)
   hipStream_t stream() const { return stream_; }

@@ -11,12 +11,130 @@ The NTT shards as a four-step (Bailey) transform with ONE all-to-all
 (sharded_ntt): local R-point NTTs on column slabs, twiddles,
 all-to-all transpose, local C-point NTTs on row slabs.
 """
+import ctypes
+import sys
+import traceback
 from typing import Callable
 
 import numpy as np
 
-from ._lib import CURVE_INFO
+from ._lib import COMM_FN, CURVE_INFO, lib
 from .msm import affine_sum
+
+
+class LibComm:
+    """A communicator of the library (tachyon_mi355x_comm, include/tachyon_mi355x.h
+    "communicators"): the sharded entry points -- msm.VariableBaseMSMGpu.run_sharded,
+    ntt.FourStepNtt.run, groth16.Groth16Prover.prove_sharded(comm=...) -- do
+    their exchange inside the C++ library through it.
+
+    * LibComm.rccl(group): RCCL over xGMI, ncclCommInitRank from a unique id
+      that rank 0 creates and broadcasts over the torch process group (one
+      GPU per rank; RCCL refuses two ranks on one GPU).
+    * LibComm.from_process_group(group): the HOST-STAGED FALLBACK -- the
+      library calls back into torch.distributed (gloo: host tensors; nccl:
+      device tensors) with host buffers.
+    """
+
+    def __init__(self, handle, keep=()):
+        if not handle:
+            raise RuntimeError("communicator creation failed")
+        self._h = handle
+        self._keep = keep  # the ctypes callbacks must outlive the handle
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def world(self) -> int:
+        return lib().tachyon_mi355x_comm_world(self._h)
+
+    @property
+    def rank(self) -> int:
+        return lib().tachyon_mi355x_comm_rank(self._h)
+
+    @property
+    def backend(self) -> str:
+        return lib().tachyon_mi355x_comm_backend(self._h).decode()
+
+    def all_gather(self, blob: bytes) -> bytes:
+        """Every rank's equal-length blob, concatenated in rank order
+        (tachyon_mi355x_comm_all_gather)."""
+        out = ctypes.create_string_buffer(max(1, len(blob) * self.world))
+        lib().tachyon_mi355x_comm_all_gather(self._h, ctypes.create_string_buffer(blob, max(1, len(blob))), out,
+                                             len(blob))
+        return out.raw[:len(blob) * self.world]
+
+    def close(self):
+        if self._h:
+            lib().tachyon_mi355x_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @classmethod
+    def rccl(cls, group=None):
+        """RCCL communicator over the ranks of `group` (world 1 without a group)."""
+        import torch.distributed as dist
+        multi = dist.is_available() and dist.is_initialized()
+        world = dist.get_world_size(group) if multi else 1
+        rank = dist.get_rank(group) if multi else 0
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0 and lib().tachyon_mi355x_comm_unique_id(uid, 128) != 128:
+            raise RuntimeError("ncclGetUniqueId failed")
+        raw = uid.raw
+        if world > 1:
+            obj = [raw if rank == 0 else None]
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast_object_list(obj, src=src, group=group)
+            raw = obj[0]
+        return cls(lib().tachyon_mi355x_comm_init_rccl(ctypes.create_string_buffer(raw, 128), world, rank))
+
+    @classmethod
+    def from_process_group(cls, group=None):
+        """Host-staged communicator whose exchanges are torch.distributed collectives."""
+        import torch
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        device = None if _host_collectives(group) else torch.device("cuda", torch.cuda.current_device())
+
+        def tensor(ptr, nbytes):
+            t = torch.frombuffer(bytearray(ctypes.string_at(ptr, nbytes)), dtype=torch.uint8)
+            return t.to(device) if device is not None else t
+
+        def store(ptr, t):
+            h = t.cpu().numpy()
+            ctypes.memmove(ptr, h.ctypes.data, h.nbytes)
+
+        def all_gather(_user, send, recv, nbytes):
+            try:
+                t = tensor(send, nbytes)
+                out = torch.empty(world * nbytes, dtype=torch.uint8, device=t.device)
+                dist.all_gather_into_tensor(out, t, group=group)
+                store(recv, out)
+                return 0
+            except Exception:
+                traceback.print_exc(file=sys.stderr)
+                return 1
+
+        def all_to_all(_user, send, recv, nbytes):
+            try:
+                t = tensor(send, world * nbytes)
+                out = torch.empty_like(t)
+                dist.all_to_all_single(out, t, group=group)
+                store(recv, out)
+                return 0
+            except Exception:
+                traceback.print_exc(file=sys.stderr)
+                return 1
+
+        ag, a2a = COMM_FN(all_gather), COMM_FN(all_to_all)
+        return cls(lib().tachyon_mi355x_comm_create_host(world, rank, ag, a2a, None), keep=(ag, a2a))
 
 
 def shard_range(n_total: int, rank: int, world: int):

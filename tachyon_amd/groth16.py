@@ -115,12 +115,23 @@ class Groth16Prover:
         lib().tachyon_mi355x_groth16_assemble(self._h, p, len(parts) // size, rb, sb, a, b, c)
         return a.raw, b.raw, c.raw
 
-    def prove_sharded(self, full, r: bytes = None, s: bytes = None, group=None, device=None):
+    def prove_sharded(self, full, r: bytes = None, s: bytes = None, group=None, device=None, comm=None):
         """prove() across the ranks of `group`: every rank runs the witness map
         and its MSM shard, one all-gather exchanges the partials, every rank
-        assembles the same proof.  World size 1 (or no process group) is prove()."""
+        assembles the same proof.  World size 1 (or no process group) is prove().
+        With `comm` (a tachyon_amd.dist.LibComm) the whole flow runs inside the
+        library (tachyon_mi355x_groth16_prove_sharded) over that communicator."""
         import torch.distributed as dist
         from .dist import all_gather_bytes
+        if comm is not None:
+            p, n, keep = _ptr(full)
+            a = ctypes.create_string_buffer(self.g1_bytes)
+            b = ctypes.create_string_buffer(self.g2_bytes)
+            c = ctypes.create_string_buffer(self.g1_bytes)
+            rb = ctypes.create_string_buffer(r, 32) if r is not None else None
+            sb = ctypes.create_string_buffer(s, 32) if s is not None else None
+            lib().tachyon_mi355x_groth16_prove_sharded(self._h, comm.handle, p, n // 32, rb, sb, a, b, c)
+            return a.raw, b.raw, c.raw
         if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
             return self.prove(full, r, s)
         rank, world = dist.get_rank(group), dist.get_world_size(group)

@@ -83,6 +83,17 @@ class VariableBaseMSMGpu:
         del keep
         return out.raw
 
+    def run_sharded(self, comm, bases, scalars, n=None) -> bytes:
+        """This rank's shard of an MSM over a library communicator
+        (tachyon_amd.dist.LibComm): the local partial, the all-gather and the
+        group sum inside the library (tachyon_mi355x_msm_gpu_sharded_affine);
+        every rank returns the whole MSM (affine bytes)."""
+        pb, ps, n, keep = self._args(bases, scalars, n)
+        out = ctypes.create_string_buffer(self.point_bytes)
+        lib().tachyon_mi355x_msm_gpu_sharded_affine(self.curve_id, self._ctx, comm.handle, pb, ps, n, out)
+        del keep
+        return out.raw
+
     def run_batch(self, d_bases, scalars, length: int, count: int) -> list:
         """`count` MSMs over the same `length` device-resident bases (a CUDA
         tensor or device pointer) in one launch sequence: MSM g takes

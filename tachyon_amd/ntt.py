@@ -228,6 +228,15 @@ class FourStepNtt:
         """Tensor form of stage() for tachyon_amd.dist.sharded_ntt (device tensors)."""
         self.stage(stage, inverse, src.data_ptr(), dst.data_ptr())
 
+    def run(self, comm, src, dst, inverse: bool = False):
+        """Both stages and the all-to-all between them inside the library
+        (tachyon_mi355x_bn254_ntt4_run) over a tachyon_amd.dist.LibComm whose
+        world / rank are this plan's; src / dst: device tensors of local_size
+        elements, ordered on the plan's stream."""
+        if comm.world != self.world or comm.rank != self.rank:
+            raise ValueError("communicator world/rank differ from the plan's")
+        lib().tachyon_mi355x_bn254_ntt4_run(self._p, comm.handle, 1 if inverse else 0, src.data_ptr(), dst.data_ptr())
+
     def synchronize(self):
         lib().tachyon_mi355x_bn254_ntt4_synchronize(self._p)
 

@@ -222,3 +222,37 @@ def test_groth16_prove_sharded_world2():
         assert proof == (b"A", b"B", b"C")
         assert calls[0] == ("partials", rank, 2, True)
         assert calls[1] == ("assemble", bytes([0]) * 48 + bytes([1]) * 48, r, r)
+
+
+def _lib_comm_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tachyon_amd import dist as D
+        comm = D.LibComm.from_process_group()
+        blob = bytes((rank * 53 + i) & 0xFF for i in range(777))
+        got = (comm.backend, comm.world, comm.rank, comm.all_gather(blob), comm.all_gather(b""))
+        comm.close()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_library_host_comm_world3():
+    """The host-staged communicator of the library (tachyon_mi355x_comm_create_host
+    with torch.distributed callbacks; no GPU work): tachyon_mi355x_comm_all_gather
+    -- the exchange of the library's sharded MSM / Groth16 entries -- returns
+    every rank's blob in rank order on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lib_comm_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=240) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = b"".join(bytes((r * 53 + i) & 0xFF for i in range(777)) for r in range(3))
+    for rank, (backend, world, rk, g, empty) in got:
+        assert (backend, world, rk) == ("host", 3, rank) and g == want and empty == b""
