@@ -305,6 +305,12 @@ TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4*
                                                       const tachyon_bn254_fr* d_in, tachyon_bn254_fr* d_out);
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_synchronize(tachyon_mi355x_bn254_ntt4* plan);
 TACHYON_C_EXPORT void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn254_ntt4* plan);
+/* A/B (every variant gives the same bytes): bit 0 = the round-4 stages (an
+ * input copy, the passes, a separate twiddle kernel) instead of the exchange's
+ * twiddle and packing fused into the sub-transforms' passes; bit 1 = the
+ * sub-transforms on the 8 x 32-bit-limb passes instead of their size's
+ * default (29-bit up to 2^20).  Returns 0 for other values. */
+TACHYON_C_EXPORT int tachyon_mi355x_bn254_ntt4_set_variant(tachyon_mi355x_bn254_ntt4* plan, int variant);
 
 /* ---- communicators and library-level sharded entry points ------------------
  * One process per MI355X: a multi-process C/C++ caller (benchmark/msm/

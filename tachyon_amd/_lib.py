@@ -175,6 +175,7 @@ SIGNATURES = [
     ("tachyon_mi355x_comm_backend", ctypes.c_char_p, [vp]),
     ("tachyon_mi355x_msm_gpu_sharded_affine", None, [i32, vp, vp, vp, vp, sz, vp]),
     ("tachyon_mi355x_bn254_ntt4_run", None, [vp, vp, i32, vp, vp]),
+    ("tachyon_mi355x_bn254_ntt4_set_variant", i32, [vp, i32]),
     ("tachyon_mi355x_groth16_prove_sharded", None, [vp, vp, vp, sz, vp, vp, vp, vp, vp]),
     ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
     ("tachyon_mi355x_version", ctypes.c_char_p, []),

@@ -1032,6 +1032,11 @@ int tachyon_mi355x_comm_world(const tachyon_mi355x_comm* comm) { return comm->im
 int tachyon_mi355x_comm_rank(const tachyon_mi355x_comm* comm) { return comm->impl->rank(); }
 const char* tachyon_mi355x_comm_backend(const tachyon_mi355x_comm* comm) { return comm->impl->backend(); }
 
+int tachyon_mi355x_bn254_ntt4_set_variant(tachyon_mi355x_bn254_ntt4* plan, int variant) {
+  if (variant < 0 || variant > 3) return 0;
+  GUARD_BEGIN plan->impl->set_variant(variant); GUARD_END
+  return 1;
+}
 void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn254_ntt4* plan) {
   return static_cast<void*>(plan->impl->stream());
 }

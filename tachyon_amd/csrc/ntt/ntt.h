@@ -32,6 +32,18 @@ struct NttTimings {
   std::vector<float> passes;
 };
 
+// The four-step's exchange fused into a domain's passes (Ntt4Step): element
+// k of batch entry b (the rank's local column c_l) is multiplied by
+// w_N^(+-(c0 + b) k) (two-level power tables lo / hi of N = 2^log_n, split at
+// `bits`) and read from / written to its packed position
+// ((k >> log_rg) << log_cg + b) << log_rg | (k mod 2^log_rg).
+template <class Fr>
+struct FourStepTw {
+  const Fr* lo = nullptr;
+  const Fr* hi = nullptr;
+  uint32_t bits = 0, log_n = 0, log_rg = 0, log_cg = 0, c0 = 0;
+};
+
 template <class Fr>
 class NttDomain {
  public:
@@ -57,6 +69,11 @@ class NttDomain {
   // Not synchronised.
   void forward_device(Fr* d_data, size_t batch = 1);
   void inverse_device(Fr* d_data, size_t batch = 1);
+  // Out of place (`src` read by the first pass, `dst` written by the last;
+  // dst may equal src) with the four-step's twiddle and packed layout fused
+  // (fs: forward -> into the last pass's store, inverse -> into the first
+  // pass's load; null = plain batched layout).
+  void transform_device(const Fr* src, Fr* dst, bool inverse, size_t batch, const FourStepTw<Fr>* fs);
 
   // Host vector in/out: `len` <= n input elements, zero-padded to n; writes n
   // outputs to `out` (may alias `in`).  Synchronises.
@@ -81,8 +98,8 @@ class NttDomain {
   const std::vector<Pass>& plan() const { return plan_; }
 
  private:
-  void run(Fr* d_data, bool inverse, size_t batch);
-  void run29(Fr* d_data, bool inverse, size_t batch);
+  void run(Fr* d_data, bool inverse, size_t batch, const Fr* src = nullptr, const FourStepTw<Fr>* fs = nullptr);
+  void run29(Fr* d_data, bool inverse, size_t batch, const Fr* src = nullptr, const FourStepTw<Fr>* fs = nullptr);
   void build_twiddles();
   void build_tables29();
   void ensure_tables32();
@@ -172,8 +189,22 @@ class Ntt4Step {
   void forward_stage2(const Fr* recv, Fr* out);
   void inverse_stage1(const Fr* in, Fr* send);
   void inverse_stage2(const Fr* recv, Fr* out);
+  // A/B: bit 0 = the round-4 stages (copies, separate twiddle kernel), bit 1
+  // = the sub-transforms on the 32-bit passes
+  void set_variant(int v) {
+    fused_ = !(v & 1);
+    const int sub = (v & 2) ? 0 : -1;
+    if (sub == 0) {
+      dom_r_->set_variant(0);
+      dom_c_->set_variant(0);
+    } else {
+      dom_r_->set_variant(dom_r_->log_size() <= 20 ? 1 : 0);
+      dom_c_->set_variant(dom_c_->log_size() <= 20 ? 1 : 0);
+    }
+  }
 
  private:
+  bool fused_ = true;
   uint32_t log_n_, log_g_, rank_, log_r_, log_c_;
   size_t n_;
   hipStream_t stream_ = nullptr;

@@ -24,7 +24,7 @@ constexpr uint32_t kMaxPassStages = 8;
 // 1024/r2 1.95, 1024/r3 2.82 (half the threads idle), 512/r2 2.54 ms.
 constexpr uint32_t kMaxLdsElems = 1024;
 
-enum : uint32_t { kLoadCoset = 1, kStoreScale = 2, kStoreCoset = 4 };
+enum : uint32_t { kLoadCoset = 1, kStoreScale = 2, kStoreCoset = 4, kLoadTw4 = 8, kStoreTw4 = 16 };
 
 // Twiddle tables.  BN254 Fr butterflies multiply by a Shoup product
 // (Fp::mul_shoup, mont_asm.h shoup_mul_8): an entry is the plain twiddle and
@@ -61,7 +61,24 @@ struct PassArgs {
   const Fr* store_lo;
   const Fr* store_hi;
   Fr scale;
+  // four-step exchange (kStoreTw4: the forward stage 1's last pass; kLoadTw4:
+  // the inverse stage 2's first pass): element k of batch entry b (the local
+  // column c_l) times w_N^(+-(c0 + b) k), at its packed send / recv position
+  FourStepTw<Fr> fs;
 };
+
+// packed position of element k1 of local column c_l (twiddle_exchange_kernel's layout):
+// ((h Cg + c_l) Rg + k1_l), h = k1 >> log_rg
+template <class Fr>
+__device__ __forceinline__ size_t fs_packed(const FourStepTw<Fr>& f, uint32_t k1, uint32_t c_l) {
+  return ((((size_t)(k1 >> f.log_rg) << f.log_cg) + c_l) << f.log_rg) + (k1 & ((1u << f.log_rg) - 1));
+}
+// w_N^((c0 + c_l) k1) from the two-level power tables of the four-step's root
+template <class Fr>
+__device__ __forceinline__ Fr fs_twiddle(const FourStepTw<Fr>& f, uint32_t k1, uint32_t c_l) {
+  const uint64_t e = ((uint64_t)(f.c0 + c_l) * k1) & ((uint64_t(1) << f.log_n) - 1);
+  return f.lo[e & ((1u << f.bits) - 1)] * f.hi[e >> f.bits];
+}
 
 __device__ __forceinline__ uint32_t bitrev(uint32_t x, uint32_t bits) {
   return bits == 0 ? 0u : (__brev(x) >> (32 - bits));
@@ -155,8 +172,10 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
   const uint32_t M = 1u << log_m;
   const uint32_t elems = M << k;
   const uint32_t b = blockIdx.x;
-  in += (size_t)blockIdx.y << L;  // batch of independent contiguous transforms
-  out += (size_t)blockIdx.y << L;
+  // batch of independent contiguous transforms (the packed four-step
+  // layouts address the whole buffer themselves)
+  if (!(a.mode & kLoadTw4)) in += (size_t)blockIdx.y << L;
+  if (!(a.mode & kStoreTw4)) out += (size_t)blockIdx.y << L;
 
   // index(mid, m) of element m of the block's set, position mid in the set
   uint32_t hi_shift = L - a.s0;            // set stride in the hi dimension
@@ -179,8 +198,13 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
   for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
     uint32_t mid = e >> log_m, m = e & (M - 1);
     uint32_t i = index(mid, m);
-    Fr v = in[i];
-    if (a.mode & kLoadCoset) v = v * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
+    Fr v;
+    if (a.mode & kLoadTw4) {
+      v = in[fs_packed(a.fs, i, blockIdx.y)] * fs_twiddle(a.fs, i, blockIdx.y);
+    } else {
+      v = in[i];
+      if (a.mode & kLoadCoset) v = v * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
+    }
     lds[e] = v;
   }
   __syncthreads();
@@ -221,7 +245,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
       uint32_t o = (q << (L - k)) + r0 + m;
       if (a.mode & kStoreCoset) v = v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits]);
       else if (a.mode & kStoreScale) v = v * a.scale;
-      out[o] = v.canonical();
+      if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, blockIdx.y)] = (v * fs_twiddle(a.fs, o, blockIdx.y)).canonical();
+      else out[o] = v.canonical();
     }
   }
 }
@@ -351,8 +376,13 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
     const uint32_t i = index(mid, m);
     F29 v;
     if constexpr (kFirst) {
-      Bn254Fr x = static_cast<const Bn254Fr*>(in_v)[batch_off + i];
-      if (a.mode & kLoadCoset) x = x * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
+      Bn254Fr x;
+      if (a.mode & kLoadTw4) {
+        x = static_cast<const Bn254Fr*>(in_v)[fs_packed(a.fs, i, blockIdx.y)] * fs_twiddle(a.fs, i, blockIdx.y);
+      } else {
+        x = static_cast<const Bn254Fr*>(in_v)[batch_off + i];
+        if (a.mode & kLoadCoset) x = x * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
+      }
       v = fr29::from_words(x.v);
     } else {
       v = static_cast<const F29*>(in_v)[batch_off + i];
@@ -383,7 +413,7 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
       out[index(mid, m)] = lds29_load<kSwz>(lds, e);
     }
   } else {
-    Bn254Fr* out = static_cast<Bn254Fr*>(out_v) + batch_off;
+    Bn254Fr* out = static_cast<Bn254Fr*>(out_v) + ((a.mode & kStoreTw4) ? 0 : batch_off);
     for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
       const uint32_t q = e >> log_m, m = e & (M - 1);
       const uint32_t mid = bitrev(q, k);
@@ -392,7 +422,8 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
       const uint32_t o = (q << (L - k)) + r0 + m;
       if (a.mode & kStoreCoset) v = (v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits])).canonical();
       else if (a.mode & kStoreScale) v = (v * a.scale).canonical();
-      out[o] = v;
+      if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, blockIdx.y)] = (v * fs_twiddle(a.fs, o, blockIdx.y)).canonical();
+      else out[o] = v;
     }
   }
 }
@@ -752,14 +783,17 @@ void NttDomain<Fr>::set_offset(const Fr& h) {
 }
 
 template <class Fr>
-void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
+void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch, const Fr* src_in, const FourStepTw<Fr>* fs) {
   if (log_n_ == 0 || batch == 0) {
     // size-1 domain: forward is the identity (h^0 = 1); inverse scales by n^-1 = 1
+    if (fs) throw std::runtime_error("tachyon_mi355x: four-step sub-transforms need >= 2 points");
+    if (src_in && src_in != d_data && batch)
+      TA_HIP(hipMemcpyAsync(d_data, src_in, batch * n_ * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
     return;
   }
   if (batch > 65535) throw std::runtime_error("tachyon_mi355x: NTT batch exceeds the grid limit");
   if constexpr (std::is_same_v<Fr, Bn254Fr>) {
-    if (variant_ & 1) return run29(d_data, inverse, batch);
+    if (variant_ & 1) return run29(d_data, inverse, batch, src_in, fs);
   }
   using Tw = typename NttTw<Fr>::type;
   constexpr bool kShoup = !std::is_same_v<Tw, Fr>;
@@ -792,8 +826,13 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
         a.scale = size_inv_;
       }
     }
-    // first pass: data -> scratch; middle: scratch in place; last: scratch -> data
-    const Fr* src = (p == 0) ? d_data : scratch;
+    if (fs) {
+      a.fs = *fs;
+      if (p == 0 && inverse) a.mode |= kLoadTw4;
+      if (ps.final_pass && !inverse) a.mode |= kStoreTw4;
+    }
+    // first pass: data (or src_in) -> scratch; middle: scratch in place; last: scratch -> data
+    const Fr* src = (p == 0) ? (src_in ? src_in : d_data) : scratch;
     Fr* dst = ps.final_pass ? d_data : scratch;
     uint32_t elems = (1u << ps.log_m) << ps.k;
     uint32_t blocks = (uint32_t)(n_ / elems);
@@ -842,7 +881,7 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch) {
 // BN254 Fr: the passes over 9 x 29-bit limbs (dif29_pass_kernel); the same
 // pass plan, modes and scratch discipline as run()
 template <class Fr>
-void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch) {
+void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch, const Fr* src_in, const FourStepTw<Fr>* fs) {
   if constexpr (std::is_same_v<Fr, Bn254Fr>) {
     const auto* tm = (inverse ? t29m_inv_ : t29m_fwd_).template as<fr29::TwMont29>();
     const auto* ts = (inverse ? t29s_inv_ : t29s_fwd_).template as<fr29::TwShoup29>();
@@ -873,8 +912,13 @@ void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch) {
           a.scale = size_inv_;
         }
       }
-      // first pass: data (32 B) -> scratch (36 B); middle: scratch in place; last: scratch -> data
-      const void* src = (p == 0) ? static_cast<const void*>(d_data) : scratch;
+      if (fs) {
+        a.fs = *fs;
+        if (p == 0 && inverse) a.mode |= kLoadTw4;
+        if (ps.final_pass && !inverse) a.mode |= kStoreTw4;
+      }
+      // first pass: data / src_in (32 B) -> scratch (36 B); middle: scratch in place; last: scratch -> data
+      const void* src = (p == 0) ? static_cast<const void*>(src_in ? src_in : d_data) : scratch;
       void* dst = ps.final_pass ? static_cast<void*>(d_data) : scratch;
       const uint32_t elems = (1u << ps.log_m) << ps.k;
       const uint32_t blocks = (uint32_t)(n_ / elems);
@@ -903,6 +947,11 @@ void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch) {
 
 template <class Fr>
 void NttDomain<Fr>::forward_device(Fr* d_data, size_t batch) { run(d_data, false, batch); }
+
+template <class Fr>
+void NttDomain<Fr>::transform_device(const Fr* src, Fr* dst, bool inverse, size_t batch, const FourStepTw<Fr>* fs) {
+  run(dst, inverse, batch, src, fs);
+}
 
 template <class Fr>
 void NttDomain<Fr>::inverse_device(Fr* d_data, size_t batch) { run(d_data, true, batch); }
@@ -972,12 +1021,22 @@ Ntt4Step<Fr>::~Ntt4Step() {
   if (own_stream_) (void)hipStreamDestroy(stream_);
 }
 
+// Stage 1 forward: the R-point NTTs of the local columns read `in` directly
+// (no copy) and their last pass multiplies by w_n^(c k1) and writes the packed
+// send layout (no separate twiddle kernel): two HBM round trips for R <= 2^16.
+// (Before round 5: a copy, the passes, and twiddle_exchange_kernel -- kept as
+// the unfused path, fused_ = false, for A/B.)
 template <class Fr>
 void Ntt4Step<Fr>::forward_stage1(const Fr* in, Fr* send) {
   const size_t m = local_size();
+  const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
+  if (fused_) {
+    const FourStepTw<Fr> fs{w_lo_.as<Fr>(), w_hi_.as<Fr>(), pow_bits_, log_n_, log_rg, log_cg, rank_ << log_cg};
+    dom_r_->transform_device(in, send, false, size_t(1) << log_cg, &fs);
+    return;
+  }
   Fr* work = static_cast<Fr*>(work_.ensure(m * sizeof(Fr)));
   TA_HIP(hipMemcpyAsync(work, in, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
-  const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
   dom_r_->forward_device(work, size_t(1) << log_cg);
   hipLaunchKernelGGL(twiddle_exchange_kernel<Fr>, dim3(ceil_div(m, kBlock)), dim3(kBlock), 0, stream_, work, send,
                      log_r_, log_rg, log_cg, rank_ << log_cg, log_n_, w_lo_.as<Fr>(), w_hi_.as<Fr>(), pow_bits_, 0u);
@@ -999,9 +1058,13 @@ void Ntt4Step<Fr>::inverse_stage1(const Fr* in, Fr* send) {
   // in = [k1_l][k2] (Rg x C): inverse C-point NTTs, then transpose to [c][k1_l] = G chunks [c_l][k1_l]
   const size_t m = local_size();
   Fr* work = static_cast<Fr*>(work_.ensure(m * sizeof(Fr)));
-  TA_HIP(hipMemcpyAsync(work, in, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
   const uint32_t rows = 1u << (log_r_ - log_g_), cols = 1u << log_c_;
-  dom_c_->inverse_device(work, rows);
+  if (fused_) {
+    dom_c_->transform_device(in, work, true, rows, nullptr);  // out of place: no copy
+  } else {
+    TA_HIP(hipMemcpyAsync(work, in, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+    dom_c_->inverse_device(work, rows);
+  }
   hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(cols, 32), ceil_div(rows, 32)), dim3(kBlock), 0, stream_,
                      work, send, rows, cols);
   TA_HIP(hipGetLastError());
@@ -1011,6 +1074,11 @@ template <class Fr>
 void Ntt4Step<Fr>::inverse_stage2(const Fr* recv, Fr* out) {
   const size_t m = local_size();
   const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
+  if (fused_) {  // the unpack and w_n^-(c k1) in the first pass's load
+    const FourStepTw<Fr> fs{wi_lo_.as<Fr>(), wi_hi_.as<Fr>(), pow_bits_, log_n_, log_rg, log_cg, rank_ << log_cg};
+    dom_r_->transform_device(recv, out, true, size_t(1) << log_cg, &fs);
+    return;
+  }
   hipLaunchKernelGGL(twiddle_exchange_kernel<Fr>, dim3(ceil_div(m, kBlock)), dim3(kBlock), 0, stream_, recv, out,
                      log_r_, log_rg, log_cg, rank_ << log_cg, log_n_, wi_lo_.as<Fr>(), wi_hi_.as<Fr>(), pow_bits_, 1u);
   TA_HIP(hipGetLastError());

@@ -237,6 +237,13 @@ class FourStepNtt:
             raise ValueError("communicator world/rank differ from the plan's")
         lib().tachyon_mi355x_bn254_ntt4_run(self._p, comm.handle, 1 if inverse else 0, src.data_ptr(), dst.data_ptr())
 
+    def set_variant(self, variant: int):
+        """A/B (same bytes): bit 0 = the round-4 stages (copy + passes +
+        separate twiddle kernel) instead of the fused exchange; bit 1 = the
+        32-bit-limb passes for the sub-transforms."""
+        if not lib().tachyon_mi355x_bn254_ntt4_set_variant(self._p, variant):
+            raise ValueError(f"unknown four-step variant {variant}")
+
     def synchronize(self):
         lib().tachyon_mi355x_bn254_ntt4_synchronize(self._p)
 

@@ -94,11 +94,15 @@ def test_device_round_trip_2_24():
     assert torch.equal(y[:32 * 1024], ones) and torch.equal(y[-32 * 1024:], ones)
 
 
-@pytest.mark.parametrize("log_n,world", [(2, 1), (6, 2), (9, 4), (12, 8), (13, 8), (20, 8), (14, 1)])
-def test_four_step_simulated_ranks(log_n, world):
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("log_n,world", [(2, 1), (6, 2), (9, 4), (12, 8), (13, 8), (20, 8), (14, 1), (19, 2)])
+def test_four_step_simulated_ranks(log_n, world, variant):
     """The distributed four-step plan on one GPU with `world` simulated ranks:
     stage 1 on every rank, the all-to-all done by slicing, stage 2 -> each
-    rank's slab of the oracle FFT; the inverse returns every rank's input."""
+    rank's slab of the oracle FFT; the inverse returns every rank's input.
+    Every plan variant (the exchange's twiddle + packing fused into the
+    sub-transforms' passes or the round-4 separate kernels; 29- or 32-bit
+    passes) gives the same bytes."""
     import torch
     from tachyon_amd.ntt import FourStepNtt
     n = 1 << log_n
@@ -109,6 +113,8 @@ def test_four_step_simulated_ranks(log_n, world):
     stream = torch.cuda.Stream()  # the plans and every tensor op below share it
     torch.cuda.set_stream(stream)
     plans = [FourStepNtt(log_n, world, r, stream) for r in range(world)]
+    for p in plans:
+        p.set_variant(variant)
     m = n // world
     chunk = (m // world) * 32
 

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""A/B of the four-step NTT's local stages (rank 0 of an N-rank plan, the
+stages bench.py's project_ntt_scaling times) over the plan variants:
+bit 0 = the round-4 stages (input copy + passes + separate twiddle kernel),
+bit 1 = 32-bit-limb sub-transform passes.  Rounds alternate the variants.
+
+  python tools/ntt4_probe.py --log-n 24 --worlds 2 4 8 --variants 0 1 2 3 --rounds 3
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3])
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    from tachyon_amd import msm as M
+    from tachyon_amd.ntt import FourStepNtt
+    for world in args.worlds:
+        plan = FourStepNtt(args.log_n, world, 0)
+        m = plan.local_size
+        x = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
+        y = torch.empty_like(x)
+        M.gen_scalars("bn254_fr", 99, m, x.data_ptr())
+        torch.cuda.synchronize()
+        s = plan.torch_stream
+        ref = None
+        for rnd in range(args.rounds):
+            for v in args.variants:
+                plan.set_variant(v)
+                x0 = x.clone()
+                plan.run_stage(1, False, x0, y)
+                s.synchronize()
+                out = y.clone()
+                if ref is None:
+                    ref = out
+                assert torch.equal(out, ref), (world, v)
+                for _ in range(2):
+                    plan.run_stage(1, False, x, y)
+                    plan.run_stage(2, False, y, x0)
+                s.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(args.reps):
+                    plan.run_stage(1, False, x, y)
+                    plan.run_stage(2, False, y, x0)
+                s.synchronize()
+                ms = (time.perf_counter() - t0) / args.reps * 1e3
+                print(json.dumps({"log_n": args.log_n, "world": world, "variant": v, "round": rnd,
+                                  "local_stages_ms": round(ms, 4)}), flush=True)
+        plan.close()
+
+
+if __name__ == "__main__":
+    main()
