@@ -573,6 +573,11 @@ TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_sharded(tachyon_mi355x_groth1
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                          size_t count, void* out_h);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on);
+/* Window bits of the proof's MSMs (0 = each MSM's size default): A (and B in
+ * G1), the merged witness + h MSM, B in G2.  Tuning / A/B; the proof is the
+ * same for every choice. */
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_msm_window_bits(tachyon_mi355x_groth16_prover* prover, unsigned c_a,
+                                                               unsigned c_lh, unsigned c_b2);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_last_timings(const tachyon_mi355x_groth16_prover* prover,
                                                           float* out8);
 /* zkey curve (0 bn254, 1 bls12_381) without building a prover. */

@@ -293,6 +293,15 @@ void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, i
   GUARD_END
 }
 
+void tachyon_mi355x_groth16_set_msm_window_bits(tachyon_mi355x_groth16_prover* prover, unsigned c_a, unsigned c_lh,
+                                               unsigned c_b2) {
+  GUARD_BEGIN
+  PROVER_DISPATCH(prover, impl->set_msm_window_bits(c_a, c_lh, c_b2));
+  for (auto& p : prover->bn_dev) p->set_msm_window_bits(c_a, c_lh, c_b2);
+  for (auto& p : prover->bls_dev) p->set_msm_window_bits(c_a, c_lh, c_b2);
+  GUARD_END
+}
+
 // After set_devices the proof runs on the per-device provers: report the lead
 // device's (rank 0's) phases, as the MSM C-API reports multi->lead()
 void tachyon_mi355x_groth16_last_timings(const tachyon_mi355x_groth16_prover* prover, float* out8) {

@@ -96,6 +96,13 @@ class Groth16Prover {
 
   const Key& key() const { return key_; }
   void set_profile(bool on) { profile_ = on; }
+  // window bits of the proof's MSMs (0 = each MSM's default): A (and B in G1),
+  // the merged witness + h MSM, B in G2 -- tuning and A/B only
+  void set_msm_window_bits(unsigned c_a, unsigned c_lh, unsigned c_b2) {
+    c_a_ = c_a;
+    c_lh_ = c_lh;
+    c_b2_ = c_b2;
+  }
   const ProveTimings& timings() const { return timings_; }
   hipStream_t stream() const { return stream_; }
 
@@ -105,6 +112,7 @@ class Groth16Prover {
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;
   bool profile_ = false;
+  unsigned c_a_ = 0, c_lh_ = 0, c_b2_ = 0;  // set_msm_window_bits
   size_t n_ = 0;  // domain size
   std::unique_ptr<ntt::NttDomain<Fr>> dom_, coset_;
   std::unique_ptr<msm::MsmGpu<G1>> msm1_;

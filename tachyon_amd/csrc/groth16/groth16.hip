@@ -242,6 +242,9 @@ template <class G1, class G2>
 Groth16Prover<G1, G2>::Groth16Prover(const Groth16Prover& src, int src_device, hipStream_t stream)
     : key_(src.key_), stream_(stream) {
   profile_ = src.profile_;
+  c_a_ = src.c_a_;
+  c_lh_ = src.c_lh_;
+  c_b2_ = src.c_b2_;
   init_device_state();
   int dev = 0;
   TA_HIP(hipGetDevice(&dev));
@@ -398,6 +401,7 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     try {
       TA_HIP(hipSetDevice(device));
       auto tb = Clock::now();
+      msm2_->set_force_window_bits(c_b2_);
       if (q_len) acc_b2 = msm2_->run(b2 + 1 + q_lo, d_full + 1 + q_lo, q_len);
       timings_.msm_b2 = ms_since(tb);
     } catch (...) {
@@ -425,6 +429,7 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   // MSM after B2 on the G2 stream, 12.34-13.13 vs 11.81-12.09 -- the GPU is
   // already full with the G2 MSM beside the G1 ones.)
   auto t2 = Clock::now();
+  msm1_->set_force_window_bits(c_a_);
   out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
   timings_.msm_a = ms_since(t2);
   t2 = Clock::now();
@@ -435,6 +440,7 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   // == domain size: the else branch of prove.h:103-112
   size_t lh_lo = 0;
   const size_t lh_len = shard(nw + n_, &lh_lo);
+  msm1_->set_force_window_bits(c_lh_);
   out.lh = lh_len ? msm1_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
   timings_.msm_l = ms_since(t2);
   timings_.msm_h = 0;

@@ -148,6 +148,11 @@ class Groth16Prover:
         if not lib().tachyon_mi355x_groth16_set_devices(self._h, arr, len(ids)):
             raise ValueError(f"device ids out of range: {ids}")
 
+    def set_msm_window_bits(self, c_a: int = 0, c_lh: int = 0, c_b2: int = 0):
+        """Window bits of the proof's MSMs (0 = default): A / B in G1, the merged
+        witness + h MSM, B in G2 (tuning; same proof)."""
+        lib().tachyon_mi355x_groth16_set_msm_window_bits(self._h, c_a, c_lh, c_b2)
+
     def set_profile(self, on: bool):
         lib().tachyon_mi355x_groth16_set_profile(self._h, 1 if on else 0)
 
