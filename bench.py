@@ -411,8 +411,14 @@ def project_ntt_scaling(log_n, t1_ms, reps=20):
         plan.close()
         pair_bytes = (1 << log_n) // (world * world) * 32
         a2a = pair_bytes / (XGMI_LINK_GBS * 1e9) * 1e3 + RCCL_SMALL_ALLGATHER_MS
-        t = local + a2a
+        t_split = local + a2a
+        # the plan the bench (and the library's set_devices) runs: the split
+        # where it projects faster than one GPU, else the single device
+        split = t_split < t1_ms
+        t = t_split if split else t1_ms
         out[f"n{world}"] = {"local_stages_ms": round(local, 4), "all_to_all_ms_model": round(a2a, 4),
+                            "split_ms": round(t_split, 4),
+                            "plan": "four-step" if split else "single GPU (the split projects slower)",
                             "ms": round(t, 4), "elems_per_s": (1 << log_n) / (t * 1e-3),
                             "efficiency": round(t1_ms / (world * t), 3)}
         del x, y
@@ -707,7 +713,47 @@ def main():
         del d_nu
 
     # ---- NTT 2^24: one GPU, or the four-step sharded transform (one RCCL all-to-all) ----
-    if not args.no_ntt and world > 1:
+    # Two ranks: the four-step exchanges n/4 elements over ONE xGMI link (134 MB
+    # at 2^24), which costs more than the whole transform on one GPU
+    # (projected_scaling.ntt; the library's set_devices applies the same rule),
+    # so the transform runs on rank 0 alone; from four ranks the exchange
+    # spreads over several links and the split pays.
+    if not args.no_ntt and world == 2:
+        from tachyon_amd.ntt import Radix2EvaluationDomain
+        nn = 1 << args.ntt_log_n
+        reps = max(2, args.steps)
+        dt_local, ok_local = 0.0, 1
+        if rank == 0:
+            dom = Radix2EvaluationDomain(nn)
+            x = torch.empty(nn * 32, dtype=torch.uint8, device="cuda")
+            M.gen_scalars("bn254_fr", SEED + 1, nn, x.data_ptr())
+            torch.cuda.synchronize()
+            orig = x.clone()
+            for _ in range(2):
+                dom.transform_device(x.data_ptr(), inverse=False)
+                dom.transform_device(x.data_ptr(), inverse=True)
+            torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        if rank == 0:
+            for _ in range(reps):
+                dom.transform_device(x.data_ptr(), inverse=False)
+                dom.transform_device(x.data_ptr(), inverse=True)
+            torch.cuda.synchronize()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item()) / (2 * reps)
+        if rank == 0:
+            ok_local = 1 if torch.equal(x, orig) else 0
+            dom.close()
+        ok = torch.tensor([ok_local], dtype=torch.int32, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
+                      "round_trip_ok": bool(ok.item()), "scaling": "strong",
+                      "mode": "single GPU (rank 0): a 2-rank four-step would exchange "
+                              f"{nn * 32 // 4} B over one xGMI link, projected slower than one GPU"}
+    if not args.no_ntt and world > 2:
         from tachyon_amd.ntt import FourStepNtt
         plan = FourStepNtt(args.ntt_log_n, world, rank)  # its own stream; sharded_ntt orders on it
         m = plan.local_size

@@ -263,7 +263,11 @@ TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_set_varia
  * on the device the domain was created on (transform_device: a buffer there).
  * The four-step splits by a power of two: the first 2^k ids are used, the
  * largest 2^k <= count with 2^k <= 2^floor(log n / 2) (_devices reports
- * them); count <= 1 restores the single device.  Returns 1, or 0 (nothing
+ * them); count <= 1 restores the single device, and so does 2^k = 2: two
+ * parts exchange n/4 elements over ONE xGMI link, which takes longer than
+ * the whole transform on one MI355X (2^24: 134 MB at <= 153 GB/s >= 0.9 ms
+ * plus 2 x 0.55 ms of local stages, against 1.84 ms) -- from four parts the
+ * all-to-all spreads over 3+ links and the split pays.  Returns 1, or 0 (nothing
  * changed) for a bad id, a domain too small for two parts, or when the
  * generator set active now differs from the domain's (the plans would use
  * another root).  Same results as one device. */

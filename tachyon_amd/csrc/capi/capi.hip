@@ -909,6 +909,10 @@ int tachyon_mi355x_bn254_univariate_evaluation_domain_set_devices(tachyon_bn254_
   size_t use = 1;
   while (use * 2 <= count && use * 2 <= (size_t(1) << (d->impl->log_size() / 2))) use *= 2;
   if (use < 2) return 0;
+  if (use == 2) {  // two parts: the one-link all-to-all costs more than the transform (see the header)
+    d->multi.reset();
+    return 1;
+  }
   const std::vector<int> dev(ids, ids + use);
   std::unique_ptr<ntt::NttMultiDevice<Bn254Fr>> m;
   try {

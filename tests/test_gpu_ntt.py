@@ -224,7 +224,7 @@ def test_field29_extreme_inputs():
 
 
 @pytest.mark.parametrize("log_n,devices", [(4, [0, 0]), (10, [0, 0]), (13, [0, 0, 0, 0]), (16, [0] * 8),
-                                           (20, [0, 0]), (11, [0, 0, 0])])
+                                           (20, [0, 0]), (11, [0, 0, 0]), (20, [0, 0, 0, 0]), (9, [0] * 5)])
 def test_multi_device_domain_logical(log_n, devices):
     """One process, several devices (set_devices): the plain domain's fft / ifft,
     transform_host and transform_device run the four-step over `devices`
@@ -236,8 +236,8 @@ def test_multi_device_domain_logical(log_n, devices):
     coeffs = O.gen_scalars("bn254_fr", 3000 + log_n, n).tobytes()
     d = domain(n)
     d.set_devices(devices)
-    used = 1 << (len(devices).bit_length() - 1)  # the first 2^k ids
-    assert d.devices() == devices[:used]
+    used = 1 << (len(devices).bit_length() - 1)  # the first 2^k ids; two parts -> the single device
+    assert d.devices() == (devices[:used] if used >= 4 else [])
     ev = d.fft(coeffs)
     assert ev == O.fft(coeffs, n)
     assert d.ifft(ev) == O.ifft(ev, n)
@@ -275,6 +275,8 @@ def test_multi_device_domain_refused():
         assert d.devices() == []
     d.set_devices([0] * 64)
     assert d.devices() == [0] * 32
+    d.set_devices([0, 0])  # two parts: the single device (the one-link exchange costs more)
+    assert d.devices() == []
     d.set_devices([])
     tiny = domain(2)
     with pytest.raises(ValueError):

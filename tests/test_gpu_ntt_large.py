@@ -156,7 +156,7 @@ def test_four_step_2_25(world):
 
 @pytest.mark.timeout(600)
 def test_multi_device_domain_2_25_logical():
-    """set_devices([0, 0]) at 2^25: the one-process four-step inside the
+    """set_devices([0, 0, 0, 0]) at 2^25: the one-process four-step inside the
     domain (peer-copy all-to-all) equals the oracle, forward and inverse."""
     torch = pytest.importorskip("torch")
     from tachyon_amd.ntt import Radix2EvaluationDomain
@@ -164,7 +164,8 @@ def test_multi_device_domain_2_25_logical():
     x = _device_input(torch, n, SEED + 125)
     coeffs = x.cpu().numpy().view(np.uint64).copy()
     d = Radix2EvaluationDomain(n)
-    d.set_devices([0, 0])
+    d.set_devices([0, 0, 0, 0])
+    assert d.devices() == [0, 0, 0, 0]
     d.transform_device(x.data_ptr())
     torch.cuda.synchronize()
     evals = x.cpu().numpy().view(np.uint64).copy()
