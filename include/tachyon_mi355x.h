@@ -577,6 +577,11 @@ TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_sharded(tachyon_mi355x_groth1
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                          size_t count, void* out_h);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on);
+/* A/B: variant 1 runs A and the witness + h MSM as two MSMs (round 4); 0
+ * (default) as one grouped MSM over their own bases (one recode / sort /
+ * accumulation / reduction; single-device proofs).  Same proof; returns 0
+ * for other values. */
+TACHYON_C_EXPORT int tachyon_mi355x_groth16_set_variant(tachyon_mi355x_groth16_prover* prover, int variant);
 /* Window bits of the proof's MSMs (0 = each MSM's size default): A (and B in
  * G1), the merged witness + h MSM, B in G2.  Tuning / A/B; the proof is the
  * same for every choice. */

@@ -151,6 +151,7 @@ SIGNATURES = [
     ("tachyon_mi355x_groth16_assemble", None, [vp, vp, sz, vp, vp, vp, vp, vp]),
     ("tachyon_mi355x_groth16_set_profile", None, [vp, i32]),
     ("tachyon_mi355x_groth16_set_msm_window_bits", None, [vp, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]),
+    ("tachyon_mi355x_groth16_set_variant", i32, [vp, i32]),
     ("tachyon_mi355x_groth16_set_devices", i32, [vp, vp, sz]),
     ("tachyon_mi355x_groth16_last_timings", None, [vp, fp]),
     ("tachyon_mi355x_zkey_curve", i32, [vp, sz]),

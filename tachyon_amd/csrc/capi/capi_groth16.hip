@@ -293,6 +293,16 @@ void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, i
   GUARD_END
 }
 
+int tachyon_mi355x_groth16_set_variant(tachyon_mi355x_groth16_prover* prover, int variant) {
+  if (variant < 0 || variant > 1) return 0;
+  GUARD_BEGIN
+  PROVER_DISPATCH(prover, impl->set_variant(variant));
+  for (auto& p : prover->bn_dev) p->set_variant(variant);
+  for (auto& p : prover->bls_dev) p->set_variant(variant);
+  GUARD_END
+  return 1;
+}
+
 void tachyon_mi355x_groth16_set_msm_window_bits(tachyon_mi355x_groth16_prover* prover, unsigned c_a, unsigned c_lh,
                                                unsigned c_b2) {
   GUARD_BEGIN

@@ -98,6 +98,10 @@ class Groth16Prover {
   void set_profile(bool on) { profile_ = on; }
   // window bits of the proof's MSMs (0 = each MSM's default): A (and B in G1),
   // the merged witness + h MSM, B in G2 -- tuning and A/B only
+  // A/B: bit 0 = A and the witness + h MSM as two MSMs (round 4) instead of
+  // one grouped MSM (MsmGpu::run_groups, one process one device)
+  void set_variant(int v) { variant_ = v; }
+  int variant() const { return variant_; }
   void set_msm_window_bits(unsigned c_a, unsigned c_lh, unsigned c_b2) {
     c_a_ = c_a;
     c_lh_ = c_lh;
@@ -108,11 +112,15 @@ class Groth16Prover {
 
  private:
   void init_device_state();
+  void build_groups();
   Key key_;  // host copy: verifying-key points and the query heads used on the host
   hipStream_t stream_ = nullptr;
   bool own_stream_ = false;
   bool profile_ = false;
   unsigned c_a_ = 0, c_lh_ = 0, c_b2_ = 0;  // set_msm_window_bits
+  int variant_ = 0;
+  size_t glen_ = 0;                          // build_groups: points per group (0 = no grouped MSM)
+  DeviceBuffer gbases_, gscalars_;           // 3 x glen_ bases / scalars of the grouped MSM
   size_t n_ = 0;  // domain size
   std::unique_ptr<ntt::NttDomain<Fr>> dom_, coset_;
   std::unique_ptr<msm::MsmGpu<G1>> msm1_;

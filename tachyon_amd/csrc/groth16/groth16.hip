@@ -258,6 +258,8 @@ Groth16Prover<G1, G2>::Groth16Prover(const Groth16Prover& src, int src_device, h
   lh_.ensure(src.lh_.capacity());
   abc_.ensure(src.abc_.capacity());
   full_.ensure(src.full_.capacity());
+  variant_ = src.variant_;
+  build_groups();
 }
 
 template <class G1, class G2>
@@ -315,6 +317,31 @@ Groth16Prover<G1, G2>::Groth16Prover(const Key& key, hipStream_t stream) : key_(
   key_.h1.shrink_to_fit();
   key_.coefficients.clear();
   key_.coefficients.shrink_to_fit();
+  build_groups();
+}
+
+// A (queries 1..m-1 of a1) and the merged witness + h MSM (C1 | H1, nw + n
+// points) as three groups of glen points with their own bases for
+// MsmGpu::run_groups: [a1[1..m) | pad], [lh1[0, glen)], [lh1[glen, nw + n) |
+// pad], identity bases and zero scalars as padding (they add nothing).  One
+// recode / sort / accumulation / reduction for both MSMs: the smaller one's
+// latency-bound reduction runs inside the larger one's launches.
+template <class G1, class G2>
+void Groth16Prover<G1, G2>::build_groups() {
+  const size_t m = key_.num_vars, nlh = key_.num_witness() + n_;
+  const size_t qa = m > 1 ? m - 1 : 0;
+  glen_ = std::max(qa, (nlh + 1) / 2);
+  if (glen_ == 0 || msm1_->max_batch_count(glen_) < 3) {
+    glen_ = 0;
+    return;
+  }
+  auto* gb = static_cast<Affine<F1>*>(gbases_.ensure(3 * glen_ * sizeof(Affine<F1>)));
+  auto* gs = static_cast<Fr*>(gscalars_.ensure(3 * glen_ * sizeof(Fr)));
+  TA_HIP(hipMemsetAsync(gb, 0, 3 * glen_ * sizeof(Affine<F1>), stream_));
+  TA_HIP(hipMemsetAsync(gs, 0, 3 * glen_ * sizeof(Fr), stream_));
+  if (qa) TA_HIP(hipMemcpyAsync(gb, a1_.as<Affine<F1>>() + 1, qa * sizeof(Affine<F1>), hipMemcpyDeviceToDevice, stream_));
+  if (nlh) TA_HIP(hipMemcpyAsync(gb + glen_, lh1_.as<Affine<F1>>(), nlh * sizeof(Affine<F1>), hipMemcpyDeviceToDevice, stream_));
+  TA_HIP(hipStreamSynchronize(stream_));
 }
 
 template <class G1, class G2>
@@ -416,7 +443,12 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   auto t1 = Clock::now();
   // scalars of the merged witness + h MSM: [witness values | h]
   const size_t nw = key_.num_witness();
-  Fr* d_lh = lh_.as<Fr>();
+  // one process, one device: A and the witness + h MSM as ONE grouped MSM
+  // (run_groups over the padded group layout of build_groups)
+  const bool grouped = world == 1 && glen_ > 0 && !(variant_ & 1);
+  Fr* d_lh = grouped ? gscalars_.as<Fr>() + glen_ : lh_.as<Fr>();
+  if (grouped && q_len)
+    TA_HIP(hipMemcpyAsync(gscalars_.as<Fr>(), d_full + 1, q_len * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
   if (nw)
     TA_HIP(hipMemcpyAsync(d_lh, d_full + key_.num_instance(), nw * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
   witness_map(d_full, d_lh + nw);
@@ -430,7 +462,14 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   // already full with the G2 MSM beside the G1 ones.)
   auto t2 = Clock::now();
   msm1_->set_force_window_bits(c_a_);
-  out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
+  if (grouped) {
+    // groups: [A | pad], [witness + h, first glen], [the rest | pad]
+    const auto r = msm1_->run_groups(gbases_.as<Affine<F1>>(), gscalars_.as<Fr>(), glen_, 3);
+    out.a = r[0];
+    out.lh = r[1] + r[2];
+  } else {
+    out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
+  }
   timings_.msm_a = ms_since(t2);
   t2 = Clock::now();
   out.b1 = (with_b1 && q_len) ? msm1_->run(b1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
@@ -438,11 +477,13 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   t2 = Clock::now();
   // witness (l) and h MSMs merged; h_coefficients.size() == h_g1_query.size()
   // == domain size: the else branch of prove.h:103-112
-  size_t lh_lo = 0;
-  const size_t lh_len = shard(nw + n_, &lh_lo);
-  msm1_->set_force_window_bits(c_lh_);
-  out.lh = lh_len ? msm1_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
-  timings_.msm_l = ms_since(t2);
+  if (!grouped) {
+    size_t lh_lo = 0;
+    const size_t lh_len = shard(nw + n_, &lh_lo);
+    msm1_->set_force_window_bits(c_lh_);
+    out.lh = lh_len ? msm1_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
+  }
+  timings_.msm_l = grouped ? 0.f : ms_since(t2);
   timings_.msm_h = 0;
   g2_thread.join();
   if (g2_error) std::rethrow_exception(g2_error);

@@ -176,6 +176,10 @@ class MsmGpu {
   // MSMs, count x len < 2^31 scalars, count x W windows << c within the 32-bit
   // bucket keys); 0 when len == 0.
   size_t max_batch_count(size_t len) const;
+  // `count` MSMs of `len` points with their own device-resident bases: MSM g
+  // over bases[g len, (g+1) len) and scalars[g len, (g+1) len), one launch
+  // sequence (same limits as run_batch).
+  std::vector<Point> run_groups(const void* bases, const void* scalars, size_t len, size_t count);
 
   // The windows [w_begin, w_end) of the MSM only: sum_w 2^(c w) S_w over
   // them (c = the forced window bits or the size's default).  Summing the
@@ -219,6 +223,7 @@ class MsmGpu {
 
  private:
   unsigned batch_window_bits(size_t len) const;
+  std::vector<Point> run_batch_impl(const void* bases, const void* scalars, size_t len, size_t count, bool distinct);
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
   Point run_host_pipelined(const void* bases, const void* scalars, size_t n, size_t chunks);
   size_t work_bytes(size_t n) const;
@@ -270,6 +275,7 @@ class MsmGpu {
   unsigned last_schedule_ = 0;
   unsigned range_begin_ = 0, range_end_ = ~0u;  // window range of the next run_windows
   unsigned batch_ = 1;                           // MSMs in the next run_windows (run_batch)
+  bool batch_distinct_ = false;                  // ... each over its own bases (run_groups)
 };
 
 extern template class MsmGpu<Bn254G1>;

@@ -48,11 +48,12 @@ enum : uint32_t { kHead = 1, kTail = 2, kSingle = 4 };
 // Windows [w0, w0 + wr) of W are emitted, as local windows 0 .. wr-1 (the
 // lower windows still run for their carries).
 template <class Fr, class Emit>
-// glen > 0 (a batch of MSMs over shared bases, run_batch): scalar i belongs to
+// glen > 0 (a batch of MSMs, run_batch / run_groups): scalar i belongs to
 // MSM g = i / glen, its windows are g * wr .. g * wr + wr - 1 of the key space
-// and its base index is i - g * glen
+// and its base index is i - g * gstep (gstep = glen: the MSMs share one base
+// array; gstep = 0: MSM g has its own bases at [g glen, (g+1) glen))
 __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsigned c, unsigned W, unsigned w0,
-                                              unsigned wr, Emit emit, uint32_t glen = 0) {
+                                              unsigned wr, Emit emit, uint32_t glen = 0, uint32_t gstep = 0) {
   constexpr int N = Fr::N;
   Fr s = scalar.from_mont();
   uint32_t limbs[N];
@@ -64,7 +65,7 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
   if (glen) {
     const uint32_t g = i / glen;
     gw = g * wr;
-    vi = i - g * glen;
+    vi = i - g * gstep;
   }
   uint32_t carry = 0;
   for (unsigned w = 0; w < w0 + wr; ++w) {
@@ -95,12 +96,12 @@ __device__ __forceinline__ uint32_t entry_val(uint64_t e) { return (uint32_t)e; 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
                                                         unsigned c, unsigned W, unsigned w0, unsigned wr,
-                                                        uint64_t* __restrict__ ents, uint32_t glen) {
+                                                        uint64_t* __restrict__ ents, uint32_t glen, uint32_t gstep) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   recode_scalar(
       scalars[i], i, c, W, w0, wr,
-      [&](unsigned w, uint32_t key, uint32_t val) { ents[(size_t)w * n + i] = make_entry(key, val); }, glen);
+      [&](unsigned w, uint32_t key, uint32_t val) { ents[(size_t)w * n + i] = make_entry(key, val); }, glen, gstep);
 }
 
 // Recode fused with the first radix pass (key bits 0..7), in two launches:
@@ -146,7 +147,8 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
                                                              uint32_t nblocks, uint32_t spt, uint32_t places,
                                                              uint32_t* __restrict__ hist,
                                                              uint32_t* __restrict__ later,
-                                                             uint4* __restrict__ zero, size_t zero_n, uint32_t glen) {
+                                                             uint4* __restrict__ zero, size_t zero_n, uint32_t glen,
+                                                             uint32_t gstep) {
   __shared__ uint32_t cnt[3][256];
   const uint32_t t = threadIdx.x;
   // the bucket sums start as the identity (all-zero words): cleared here, not by a memset launch
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
           if (places > 0) atomicAdd(&cnt[1][(key >> 8) & 255], 1u);
           if (places > 1) atomicAdd(&cnt[2][(key >> 16) & 255], 1u);
         }
-      }, glen);
+      }, glen, gstep);
   }
   __syncthreads();
   hist[(size_t)t * nblocks + blockIdx.x] = cnt[0][t];
@@ -222,7 +224,8 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
                                                                 uint32_t nblocks, uint32_t spt,
                                                                 const uint32_t* __restrict__ hist,
                                                                 const uint32_t* __restrict__ off,
-                                                                uint64_t* __restrict__ ents, uint32_t glen) {
+                                                                uint64_t* __restrict__ ents, uint32_t glen,
+                                                                uint32_t gstep) {
   // the block's entries are binned in LDS first, then written out bin run by
   // bin run, so consecutive lanes store to consecutive addresses
   extern __shared__ uint64_t lds_u64[];
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
         } else {
           lents[p] = make_entry(key, val);
         }
-      }, glen);
+      }, glen, gstep);
   }
   __syncthreads();
   const uint32_t total = loff[255] + cur[255];
@@ -1858,6 +1861,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   const unsigned Ws = plan.active(), Wt = plan.windows, wr0 = plan.w_begin, B = plan.buckets, c = plan.c;
   const unsigned W = Ws * batch_;
   const uint32_t glen = batch_ > 1 ? (uint32_t)(n / batch_) : 0u;
+  const uint32_t gstep = batch_distinct_ ? 0u : glen;  // shared bases (run_batch) or one array per MSM (run_groups)
   const size_t entries = n * Ws;
   const size_t nb = (size_t)W * B;
   if (n >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM size must be < 2^31 per device");
@@ -1966,7 +1970,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     uint32_t* digit_cnt = later + later_places * hn;  // 2 x 256 counts, 2 x 256 offsets, 256 spare
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
                        Wt, wr0, Ws, nblocks, spt, later_places, hist, later, reinterpret_cast<uint4*>(bucket_sum),
-                       nb * slot / 16, glen);
+                       nb * slot / 16, glen, gstep);
     TA_HIP(hipGetLastError());
     if (later_places > 0) {
       digit_off = digit_cnt + 2 * 256;
@@ -1993,10 +1997,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       scatter_lds_set_[narrow ? 1 : 0] = true;
     }
     hipLaunchKernelGGL(scatter, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars, (uint32_t)n, c, Wt, wr0,
-                       Ws, nblocks, spt, hist, hoff, dst, glen);
+                       Ws, nblocks, spt, hist, hoff, dst, glen, gstep);
   } else {
     hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       Wt, wr0, Ws, ents, glen);
+                       Wt, wr0, Ws, ents, glen, gstep);
   }
   TA_HIP(hipGetLastError());
   // every bucket without an entry stays the identity (the fused recode clears them)
@@ -2746,6 +2750,22 @@ size_t MsmGpu<Curve>::max_batch_count(size_t len) const {
 template <class Curve>
 std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* bases, const void* scalars,
                                                                     size_t len, size_t count) {
+  return run_batch_impl(bases, scalars, len, count, false);
+}
+
+// `count` MSMs of `len` points each with their OWN bases -- MSM g over
+// bases[g len, (g+1) len) and scalars[g len, (g+1) len) -- in one launch
+// sequence, as run_batch (the recode's base index keeps the global i).  The
+// Groth16 prover's A and witness + h MSMs run this way.
+template <class Curve>
+std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_groups(const void* bases, const void* scalars,
+                                                                     size_t len, size_t count) {
+  return run_batch_impl(bases, scalars, len, count, true);
+}
+
+template <class Curve>
+std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch_impl(const void* bases, const void* scalars,
+                                                                         size_t len, size_t count, bool distinct) {
   std::vector<Point> res(count, Point::zero());
   if (count == 0 || len == 0) return res;
   if (count == 1) {
@@ -2762,10 +2782,12 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch(const void* 
     unsigned c;
     ~Reset() {
       m->batch_ = 1;
+      m->batch_distinct_ = false;
       m->force_c_ = c;
     }
   } reset{this, force_c_};
   force_c_ = batch_window_bits(len);
+  batch_distinct_ = distinct;
   batch_ = (unsigned)count;
   last_divisions_ = 1;
   std::vector<Point> ws;

@@ -148,6 +148,12 @@ class Groth16Prover:
         if not lib().tachyon_mi355x_groth16_set_devices(self._h, arr, len(ids)):
             raise ValueError(f"device ids out of range: {ids}")
 
+    def set_variant(self, variant: int):
+        """A/B: 1 = A and the witness + h MSM as two MSMs (round 4), 0 = one
+        grouped MSM (default); same proof."""
+        if not lib().tachyon_mi355x_groth16_set_variant(self._h, variant):
+            raise ValueError(f"unknown Groth16 variant {variant}")
+
     def set_msm_window_bits(self, c_a: int = 0, c_lh: int = 0, c_b2: int = 0):
         """Window bits of the proof's MSMs (0 = default): A / B in G1, the merged
         witness + h MSM, B in G2 (tuning; same proof)."""

@@ -67,7 +67,15 @@ def test_synthetic_parity(curve, log_n, num_public, seed):
     assert list(prover.prove(fb)) == list(OG.prove(zk, full, h=h))
     Fr = pyref.Field("bn254_fr" if curve == "bn254" else "bls12_381_fr")
     r, s = 0x5EED + seed, Fr.p - 3 - seed
-    assert list(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == list(OG.prove(zk, full, r, s, h=h))
+    want_zk = list(OG.prove(zk, full, r, s, h=h))
+    assert list(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == want_zk
+    # A and the witness + h MSM as two MSMs (variant 1, round 4) instead of the
+    # default grouped MSM: the same proofs; then forced window bits
+    prover.set_variant(1)
+    assert list(prover.prove(fb)) == list(OG.prove(zk, full, h=h))
+    prover.set_variant(0)
+    prover.set_msm_window_bits(5, 6, 7)
+    assert list(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == want_zk
     prover.close()
 
 
@@ -109,6 +117,8 @@ def test_configs4_size_parity():
     Fr = pyref.Field("bn254_fr")
     r, s = 0x1234_5678_9ABC, Fr.p - 2
     assert tuple(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == tuple(OG.prove_np(zkey, full, r, s))
+    prover.set_variant(1)  # the round-4 separate A and witness + h MSMs: the same proof
+    assert tuple(prover.prove(fb)) == tuple(OG.prove_np(zkey, full))
     prover.close()
 
 

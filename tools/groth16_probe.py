@@ -19,7 +19,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--log-n", type=int, default=20)
-    ap.add_argument("--configs", nargs="+", default=["0,0,0"], help="c_a,c_lh,c_b2 (0 = default)")
+    ap.add_argument("--configs", nargs="+", default=["0,0,0"],
+                    help="c_a,c_lh,c_b2[,variant] (0 = default; variant 1 = separate A and witness + h MSMs)")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=8)
     args = ap.parse_args()
@@ -30,7 +31,10 @@ def main():
     ref = p.prove(full)
     for rnd in range(args.rounds):
         for cfg in args.configs:
-            ca, clh, cb2 = (int(x) for x in cfg.split(","))
+            vals = [int(x) for x in cfg.split(",")]
+            ca, clh, cb2 = vals[:3]
+            var = vals[3] if len(vals) > 3 else 0
+            p.set_variant(var)
             p.set_msm_window_bits(ca, clh, cb2)
             assert p.prove(full) == ref, cfg
             ts = []
@@ -42,7 +46,7 @@ def main():
             p.prove(full)
             ph = p.last_timings()
             p.set_profile(False)
-            print(json.dumps({"log_n": args.log_n, "c_a": ca, "c_lh": clh, "c_b2": cb2, "round": rnd,
+            print(json.dumps({"log_n": args.log_n, "c_a": ca, "c_lh": clh, "c_b2": cb2, "variant": var, "round": rnd,
                               "median_ms": round(sorted(ts)[len(ts) // 2], 3), "min_ms": round(min(ts), 3),
                               "phases": {k: round(v, 3) for k, v in ph.items()}}), flush=True)
     p.close()
