@@ -318,6 +318,49 @@ EXPORT int oracle_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, vo
   return -1;
 }
 
+/* ---- discrete-log identity of the synthetic inputs ---------------------------
+ * The generated bases are known multiples of G: point i (global index start+i)
+ * = k_j 2^t G with j = (start+i) / chunk, t = (start+i) mod chunk.  So for any
+ * scalars s_i, MSM(bases, s) = (sum_i s_i k_j 2^t mod r) G: one inner product
+ * over Fr and one scalar multiplication -- an answer for full-size MSMs that
+ * shares nothing with the Pippenger restatement (the test multiplies G in
+ * pure Python, oracle/pyref.py).  scalars: Montgomery Fr; out: canonical
+ * 4 limbs of the sum. */
+#define DLOG_DOT(FRN)                                                                      \
+  {                                                                                        \
+    const FRN##_t* S = (const FRN##_t*)scalars;                                            \
+    const size_t first = start / chunk, last = (start + n + chunk - 1) / chunk;            \
+    FRN##_t total = FRN##_zero();                                                          \
+    _Pragma("omp parallel")                                                                \
+    {                                                                                      \
+      FRN##_t part = FRN##_zero();                                                         \
+      _Pragma("omp for schedule(static) nowait")                                           \
+      for (size_t j = first; j < last; ++j) {                                              \
+        uint64_t k[4];                                                                     \
+        rand_scalar_canonical(seed ^ BASE_SEED_XOR, j, m, k);                              \
+        FRN##_t d = FRN##_from_bigint(k);                                                  \
+        size_t g0 = j * chunk, g1 = g0 + chunk;                                            \
+        for (size_t g = g0; g < g1; ++g) {                                                 \
+          if (g >= start && g < start + n) part = FRN##_add(part, FRN##_mul(S[g - start], d)); \
+          d = FRN##_add(d, d);                                                             \
+        }                                                                                  \
+      }                                                                                    \
+      _Pragma("omp critical")                                                              \
+      total = FRN##_add(total, part);                                                      \
+    }                                                                                      \
+    FRN##_to_bigint(&total, (uint64_t*)out);                                               \
+    return 0;                                                                              \
+  }
+
+EXPORT int oracle_dlog_dot(int scalar_field, uint64_t seed, size_t start, size_t n, size_t chunk,
+                           const void* scalars, void* out) {
+  if (chunk == 0) return -1;
+  const uint64_t* m = scalar_field == 1 ? BN254_FR_P : BLS12_381_FR_P;
+  if (scalar_field == 1) DLOG_DOT(bn254_fr)
+  if (scalar_field == 3) DLOG_DOT(bls12_381_fr)
+  return -1;
+}
+
 /* ---- MSM ------------------------------------------------------------------ */
 /* method: 0 PippengerAdapter kParallelTerm (reference default), 1 single
  * Pippenger (kNone), 2 naive double-and-add.  Writes the affine result (x, y)

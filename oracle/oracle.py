@@ -59,6 +59,8 @@ def lib():
         L.oracle_domain_info.argtypes = [i, sz, vp]
         L.oracle_domain_info.restype = i
         L.oracle_max_threads.restype = i
+        L.oracle_dlog_dot.argtypes = [i, u64, sz, sz, sz, vp, vp]
+        L.oracle_dlog_dot.restype = i
         L.oracle_groth16_witness_map.argtypes = [i, sz, vp, sz, vp, sz, vp]
         L.oracle_groth16_witness_map.restype = i
         L.oracle_bn254_fr_set_halo2.argtypes = [i]
@@ -123,6 +125,20 @@ def gen_bases(curve, seed, n, chunk) -> np.ndarray:
     rc = lib().oracle_gen_bases(CURVES[curve], seed, n, chunk, out.ctypes.data)
     assert rc == 0
     return out
+
+
+def dlog_dot(field, seed, chunk, scalars, start=0) -> int:
+    """sum_i s_i k_j 2^t mod r over the synthetic bases' known discrete logs
+    (oracle_dlog_dot): MSM(gen_bases(seed, chunk) [start, start + n), scalars)
+    = dlog_dot(...) * G.  `scalars`: Montgomery bytes / uint8 or uint64 array."""
+    buf = np.ascontiguousarray(np.frombuffer(bytes(scalars), np.uint8) if isinstance(scalars, (bytes, bytearray))
+                               else scalars)
+    n = buf.nbytes // 32
+    out = (ctypes.c_uint64 * 4)()
+    fid = {"bn254_fr": 1, "bls12_381_fr": 3}[field]
+    rc = lib().oracle_dlog_dot(fid, seed, start, n, chunk, buf.ctypes.data, out)
+    assert rc == 0
+    return sum(int(out[k]) << (64 * k) for k in range(4))
 
 
 def fft(coeffs: bytes, domain_num_coeffs, offset_mont: bytes = None, field="bn254_fr"):

@@ -7,6 +7,7 @@ import os
 import pytest
 
 from oracle import oracle as O
+from oracle import pyref
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -119,3 +120,28 @@ def test_jacobian_return_matches_affine():
     scalars = O.gen_scalars("bn254_fr", 3, n).tobytes()
     aff, jac = O.msm("bn254_g1", bases, scalars)
     assert O.ec_op("bn254_g1", "jac_to_affine", jac) == aff
+
+
+@pytest.mark.parametrize("curve,sf", [("bn254_g1", "bn254_fr"), ("bn254_g2", "bn254_fr"),
+                                      ("bls12_381_g1", "bls12_381_fr"), ("bls12_381_g2", "bls12_381_fr")])
+def test_dlog_identity_pins_the_synthetic_msm(curve, sf):
+    """oracle_dlog_dot: the synthetic bases are known multiples of G (chunk j
+    starts at k_j G and doubles), so MSM(bases, s) = (sum s_i k_j 2^t mod r) G.
+    The identity equals the oracle's Pippenger MSM and the pure-Python
+    textbook MSM, for shards that start mid-chunk too -- it is the large-size
+    answer of tests/test_gpu_full_size.py::test_msm_dlog_identity."""
+    C = pyref.Curve(curve)
+    for n, chunk, start in ((37, 8, 0), (29, 5, 13)):
+        full = O.gen_bases(curve, 21, start + n, chunk).tobytes()
+        pb = len(full) // (start + n)
+        bases = full[start * pb:]
+        sc = O.gen_scalars(sf, 22, n).tobytes()
+        d = O.dlog_dot(sf, 21, chunk, sc, start=start)
+        want = C.to_bytes(C.mul(C.G, d))
+        assert want == O.msm(curve, bases, sc)[0]
+        pts = [C.from_bytes(bases[i * pb:(i + 1) * pb]) for i in range(n)]
+        ks = [pyref.Field(sf).from_bytes(sc[32 * i:32 * (i + 1)]) for i in range(n)]
+        acc = None
+        for P, k in zip(pts, ks):
+            acc = C.add(acc, C.mul(P, k))
+        assert C.to_bytes(acc) == want
