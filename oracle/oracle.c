@@ -318,6 +318,48 @@ EXPORT int oracle_gen_bases(int curve, uint64_t seed, size_t n, size_t chunk, vo
   return -1;
 }
 
+/* ---- direct polynomial evaluation -------------------------------------------
+ * out[q] = sum_j coeffs[j] x_q^j with x_q = w^idx[q] (Montgomery in/out): the
+ * FFT's output idx[q] computed without the butterfly network, so large
+ * transforms are checked at sampled indices independently of the radix-2
+ * restatement.  Blocks of 2^16 coefficients run Horner on OpenMP threads; the
+ * block sums are scaled by x^(block start). */
+#define EVAL_POINTS(FRN)                                                                   \
+  {                                                                                        \
+    const FRN##_t* c = (const FRN##_t*)coeffs;                                             \
+    FRN##_t w;                                                                             \
+    memcpy(&w, w_mont, sizeof w);                                                          \
+    const size_t B = (size_t)1 << 16, nb = (n + B - 1) / B;                                \
+    for (size_t q = 0; q < nidx; ++q) {                                                    \
+      uint64_t e = idx[q];                                                                 \
+      const FRN##_t x = FRN##_pow(w, &e, 1);                                               \
+      FRN##_t total = FRN##_zero();                                                        \
+      _Pragma("omp parallel")                                                              \
+      {                                                                                    \
+        FRN##_t part = FRN##_zero();                                                       \
+        _Pragma("omp for schedule(static) nowait")                                         \
+        for (size_t b = 0; b < nb; ++b) {                                                  \
+          const size_t lo = b * B, hi = lo + B < n ? lo + B : n;                           \
+          FRN##_t h = FRN##_zero();                                                        \
+          for (size_t j = hi; j-- > lo;) h = FRN##_add(FRN##_mul(h, x), c[j]);             \
+          uint64_t eb = (uint64_t)lo;                                                      \
+          part = FRN##_add(part, FRN##_mul(h, FRN##_pow(x, &eb, 1)));                      \
+        }                                                                                  \
+        _Pragma("omp critical")                                                            \
+        total = FRN##_add(total, part);                                                    \
+      }                                                                                    \
+      ((FRN##_t*)out)[q] = total;                                                          \
+    }                                                                                      \
+    return 0;                                                                              \
+  }
+
+EXPORT int oracle_eval_at_powers(int field, const void* coeffs, size_t n, const void* w_mont, const uint64_t* idx,
+                                 size_t nidx, void* out) {
+  if (field == 1) EVAL_POINTS(bn254_fr)
+  if (field == 3) EVAL_POINTS(bls12_381_fr)
+  return -1;
+}
+
 /* ---- discrete-log identity of the synthetic inputs ---------------------------
  * The generated bases are known multiples of G: point i (global index start+i)
  * = k_j 2^t G with j = (start+i) / chunk, t = (start+i) mod chunk.  So for any

@@ -59,6 +59,8 @@ def lib():
         L.oracle_domain_info.argtypes = [i, sz, vp]
         L.oracle_domain_info.restype = i
         L.oracle_max_threads.restype = i
+        L.oracle_eval_at_powers.argtypes = [i, vp, sz, vp, vp, sz, vp]
+        L.oracle_eval_at_powers.restype = i
         L.oracle_dlog_dot.argtypes = [i, u64, sz, sz, sz, vp, vp]
         L.oracle_dlog_dot.restype = i
         L.oracle_groth16_witness_map.argtypes = [i, sz, vp, sz, vp, sz, vp]
@@ -139,6 +141,19 @@ def dlog_dot(field, seed, chunk, scalars, start=0) -> int:
     rc = lib().oracle_dlog_dot(fid, seed, start, n, chunk, buf.ctypes.data, out)
     assert rc == 0
     return sum(int(out[k]) << (64 * k) for k in range(4))
+
+
+def eval_at_powers(coeffs, w_mont: bytes, indices, field="bn254_fr") -> list:
+    """[sum_j c_j (w^i)^j for i in indices] as Montgomery bytes (oracle_eval_at_powers):
+    the FFT's outputs at those indices without the butterfly network."""
+    buf = np.ascontiguousarray(np.frombuffer(bytes(coeffs), np.uint8) if isinstance(coeffs, (bytes, bytearray))
+                               else coeffs)
+    n = buf.nbytes // 32
+    idx = np.ascontiguousarray(np.array(indices, dtype=np.uint64))
+    out = ctypes.create_string_buffer(32 * max(1, len(idx)))
+    rc = lib().oracle_eval_at_powers(FIELDS[field], buf.ctypes.data, n, _buf(w_mont), idx.ctypes.data, len(idx), out)
+    assert rc == 0
+    return [out.raw[32 * q:32 * (q + 1)] for q in range(len(idx))]
 
 
 def fft(coeffs: bytes, domain_num_coeffs, offset_mont: bytes = None, field="bn254_fr"):

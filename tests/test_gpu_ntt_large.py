@@ -177,3 +177,34 @@ def test_multi_device_domain_2_25_logical():
     O.fft_np(expect)
     assert np.array_equal(evals, expect)
     assert np.array_equal(back, coeffs)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("logn", [24, 26, 28])
+def test_ntt_direct_evaluation_samples(logn):
+    """Full-size transforms checked without the butterfly network: output i of
+    the forward transform equals sum_j c_j w^(ij) (oracle_eval_at_powers, a
+    blocked Horner over all n coefficients) at sampled indices, with w the
+    pure-Python root of unity (oracle/pyref.py, the arkworks generator); the
+    inverse returns the coefficients."""
+    torch = pytest.importorskip("torch")
+    from oracle import pyref
+    from tachyon_amd.ntt import Radix2EvaluationDomain
+    n = 1 << logn
+    Fr = pyref.Field("bn254_fr")
+    d = Radix2EvaluationDomain(n)
+    w = Fr.to_bytes(Fr.root_of_unity(n))
+    assert d.group_gen == w
+    x = _device_input(torch, n, SEED + 100 + logn)
+    coeffs = x.cpu().numpy().view(np.uint64).copy()
+    evals = _transform(torch, d, x, False)
+    back = _transform(torch, d, x, True)
+    d.close()
+    del x
+    assert np.array_equal(back, coeffs)
+    rng = np.random.default_rng(logn)
+    idx = [0, 1, n - 1, n // 2, n // 3] + rng.integers(0, n, 3).tolist()
+    ev = evals.view(np.uint8).reshape(n, 32)
+    want = O.eval_at_powers(coeffs, w, idx)
+    for q, i in enumerate(idx):
+        assert ev[i].tobytes() == want[q], i
