@@ -145,3 +145,17 @@ def test_dlog_identity_pins_the_synthetic_msm(curve, sf):
         for P, k in zip(pts, ks):
             acc = C.add(acc, C.mul(P, k))
         assert C.to_bytes(acc) == want
+
+
+@pytest.mark.parametrize("logn", [1, 6, 13, 17])
+def test_direct_evaluation_equals_fft(logn):
+    """oracle_eval_at_powers (sum_j c_j (w^i)^j, blocked Horner) equals the
+    radix-2 FFT restatement at every sampled index, with w the pure-Python
+    root of unity: the independent check the full-size GPU NTT tests use."""
+    n = 1 << logn
+    Fr = pyref.Field("bn254_fr")
+    c = O.gen_scalars("bn254_fr", 40 + logn, n).tobytes()
+    ev = O.fft(c, n)
+    idx = sorted({0, 1, n - 1, n // 2, (5 * n) // 7})
+    got = O.eval_at_powers(c, Fr.to_bytes(Fr.root_of_unity(n)), idx)
+    assert got == [ev[32 * i:32 * (i + 1)] for i in idx]
