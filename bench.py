@@ -545,9 +545,22 @@ def main():
             return msm.run_window_range(d_bases, d_scalars, w_lo, w_hi, n)
         return msm.run(d_bases, d_scalars, n)
 
+    # N > 1 point shards: the library's sharded entry (local partial, all-gather,
+    # group sum in rank order inside libtachyon_mi355x) over a communicator:
+    # TACHYON_BENCH_COMM=host (default) -- the host-staged one whose exchange is
+    # this process group's collective (torch.distributed over RCCL / gloo);
+    # rccl -- the library's own RCCL communicator; torch -- the Python
+    # combine (tachyon_amd.dist.sharded_msm)
+    comm_kind = os.environ.get("TACHYON_BENCH_COMM", "host")
+    lib_comm = None
+    if world > 1 and split == "points" and comm_kind != "torch":
+        lib_comm = D.LibComm.rccl() if (comm_kind == "rccl" and backend == "nccl") else D.LibComm.from_process_group()
+
     def step():
         if split == "windows":
             return D.window_split_msm("bn254_g1", msm, d_bases, d_scalars, n, split_c, device="cuda")
+        if lib_comm is not None:
+            return msm.run_sharded(lib_comm, d_bases, d_scalars, n)
         return D.sharded_msm("bn254_g1", local_run, device="cuda")
 
     for _ in range(args.warmup):
@@ -623,7 +636,8 @@ def main():
                    "windows_per_gpu": rank_windows,
                    "parallelism": (f"msm window ranges x{world} (every rank all points, {rank_windows} of {windows} "
                                    f"windows) + RCCL all-gather of partial points" if split == "windows" else
-                                   f"msm point shards x{world} + RCCL all-gather of partial points")},
+                                   f"msm point shards x{world} + RCCL all-gather of partial points"
+                                   + (f" (inside the library, {lib_comm.backend} communicator)" if lib_comm else ""))},
         "consistent_across_steps": consistent,
         "consistent_with_1gpu": consistent_1gpu,
         "roofline": {"bound": "hbm", "achieved": acc_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
