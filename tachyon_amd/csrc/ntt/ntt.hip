@@ -609,12 +609,16 @@ NttDomain<Fr>::NttDomain(size_t num_coeffs, hipStream_t stream) : stream_(stream
   // elements per workgroup (LDS footprint); TACHYON_NTT_LDS_ELEMS overrides it
   // in tuning builds only (-DTACHYON_TUNING_KNOBS, tools/tune_ntt.py)
   uint32_t lds_elems = kMaxLdsElems;
+  uint32_t max_stages = kMaxPassStages;
 #ifdef TACHYON_TUNING_KNOBS
-  if (const char* e = getenv("TACHYON_NTT_LDS_ELEMS")) lds_elems = std::clamp<uint32_t>(atoi(e), 256, 2048);
+  if (const char* e = getenv("TACHYON_NTT_LDS_ELEMS")) lds_elems = std::clamp<uint32_t>(atoi(e), 256, 4096);
+  // (A/B of fewer, longer passes: 12 stages with 4096-element tiles = the
+  // 2-pass 2^12 x 2^12 plan of 2^24, 128 KiB of LDS per workgroup)
+  if (const char* e = getenv("TACHYON_NTT_PASS_STAGES")) max_stages = std::clamp<uint32_t>(atoi(e), 4, 12);
 #endif
   // pass plan: ceil(L / 8) passes, stages split evenly
   if (log_n_ > 0) {
-    uint32_t P = (log_n_ + kMaxPassStages - 1) / kMaxPassStages;
+    uint32_t P = (log_n_ + max_stages - 1) / max_stages;
     uint32_t s0 = 0;
     for (uint32_t p = 0; p < P; ++p) {
       uint32_t k = (log_n_ - s0) / (P - p);
@@ -846,19 +850,26 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch, const Fr* src_in
     // waves/SIMD, bit 1 = the Shoup radix-4 passes without the twiddle
     // prefetch at >= 5 waves/SIMD)
 #ifdef TACHYON_TUNING_KNOBS
+    // tiles above 64 KiB (TACHYON_NTT_LDS_ELEMS > 2048) need the kernel's dynamic-LDS limit raised
+    auto allow = [&](const void* k) {
+      if (lds > 64 * 1024) TA_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    };
     if (shoup) {
       auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Tw, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Tw, 2>
                                                                          : dif_pass_kernel<Fr, Tw, 3>;
       if (radix_ == 2 && (ntt_variant_ & 2)) kern = dif_pass_kernel<Fr, Tw, 2, false, 5>;
+      allow(reinterpret_cast<const void*>(kern));
       hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw, a);
     } else {
       auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Fr, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Fr, 2>
                                                                          : dif_pass_kernel<Fr, Fr, 3>;
       if (radix_ == 2 && (ntt_variant_ & 1)) kern = dif_pass_kernel<Fr, Fr, 2, true, 5>;
+      allow(reinterpret_cast<const void*>(kern));
       hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, twm, a);
     }
 #else
     // release schedule: radix-4 register steps (2 DIF stages per LDS round trip)
+    if (lds > 64 * 1024) throw std::runtime_error("tachyon_mi355x: NTT pass tile above 64 KiB in a release build");
     if (shoup)
       hipLaunchKernelGGL((dif_pass_kernel<Fr, Tw, 2>), dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src,
                          dst, tw, a);
@@ -922,6 +933,8 @@ void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch, const Fr* src_
       void* dst = ps.final_pass ? static_cast<void*>(d_data) : scratch;
       const uint32_t elems = (1u << ps.log_m) << ps.k;
       const uint32_t blocks = (uint32_t)(n_ / elems);
+      // the 29-bit kernel's LDS planes are sized for kMaxLdsElems (tuning plans with larger tiles: 32-bit only)
+      if (elems > kMaxLdsElems) throw std::runtime_error("tachyon_mi355x: 29-bit NTT pass tile above its LDS planes");
       const bool swz = (variant_ & 2) != 0;
       if (p == 0) {
         auto* k0 = swz ? &dif29_pass_kernel<true, true, fr29::TwMont29> : &dif29_pass_kernel<true, false, fr29::TwMont29>;

@@ -47,6 +47,8 @@ def main():
         _, passes = dom.last_timings()
         dom.set_profile(False)
         print(json.dumps({"log_n": lg, "radix_log": os.environ.get("TACHYON_NTT_RADIX_LOG", "default"),
+                          "pass_stages": os.environ.get("TACHYON_NTT_PASS_STAGES", "default"),
+                          "lds_elems": os.environ.get("TACHYON_NTT_LDS_ELEMS", "default"),
                           "ms_per_transform": round(dt * 1e3, 4), "pass_ms": [round(p, 4) for p in passes],
                           "round_trip_ok": ok}), flush=True)
         dom.close()
