@@ -80,3 +80,17 @@ def test_ntt_holder_header_compiles(tmp_path):
     r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
                         str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_circom_prover_device_list_parsing():
+    """bin/circom_prover --devices: malformed lists (a non-numeric id, only
+    separators) print the usage and exit 1 instead of an uncaught
+    std::invalid_argument (no GPU work happens before the parse)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tachyon_amd", "bin", "circom_prover")
+    if not os.path.exists(exe):
+        pytest.skip("circom_prover not built")
+    for bad in ("0,x", ",", "", "1,-2"):
+        r = subprocess.run([exe, "--zkey", "a", "--wtns", "b", "--proof", "c", "--public", "d", "--devices", bad],
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 1 and "usage:" in r.stderr + r.stdout, (bad, r.returncode, r.stderr)
