@@ -137,3 +137,28 @@ def test_host_staged_comm_world2():
         assert msm == want_msm, rank
         assert out == np.ascontiguousarray(want_ntt[oidx]).tobytes() and round_trip, rank
         assert proofs == want_proofs, rank
+
+
+def test_cpp_sharded_client_world1(tmp_path):
+    """bin/comm_check: a C++ caller of the communicator entry points without
+    torch (the rank writes / reads the RCCL unique id through a file, joins with
+    tachyon_mi355x_comm_init_rccl, runs tachyon_mi355x_msm_gpu_sharded_affine on
+    its shard of one seeded input and the four-step round trip through
+    tachyon_mi355x_bn254_ntt4_run).  World 1 on the box's GPU: the MSM equals
+    the oracle's and the discrete-log identity of the inputs."""
+    import json
+    import subprocess
+    from oracle import pyref
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tachyon_amd", "bin", "comm_check")
+    log_n = 12
+    r = subprocess.run([exe, str(log_n), "1", "0", str(tmp_path / "uid")], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["backend"] == "rccl" and res["ntt_round_trip"]
+    n, seed = 1 << log_n, 0xC0FFEE
+    bases = O.gen_bases("bn254_g1", seed, n, 16).tobytes()
+    scalars = O.gen_scalars("bn254_fr", seed, n).tobytes()
+    want = O.msm("bn254_g1", bases, scalars)[0]
+    assert bytes.fromhex(res["msm"]) == want
+    C = pyref.Curve("bn254_g1")
+    assert want == C.to_bytes(C.mul(C.G, O.dlog_dot("bn254_fr", seed, 16, scalars)))
