@@ -8,4 +8,6 @@ timeout -k 10 400 python -u tools/tune_msm.py --curve bn254_g1 --log-n 23 24 25 
 timeout -k 10 300 python -u tools/tune_msm.py --curve bls12_381_g1 --log-n 21 22 23 --c 14 15 16 18 19 20 --reps 3 --rounds 2 \
   > gpurun_out/r05c/sweep_bls12_381_g1.jsonl 2>&1 || exit $?
 timeout -k 10 400 python -u tools/tune_msm.py --curve bls12_381_g2 --log-n 21 22 23 --c 14 15 16 18 19 --reps 3 --rounds 1 \
-  > gpurun_out/r05c/sweep_bls12_381_g2.jsonl 2>&1
+  > gpurun_out/r05c/sweep_bls12_381_g2.jsonl 2>&1 || exit $?
+timeout -k 10 400 python -u tools/split_probe.py --log-n 26 --worlds 2 4 8 --hybrid --hybrid-c 17 19 20 --reps 3 \
+  > gpurun_out/r05c/hybrid_split_probe.jsonl 2>&1

@@ -32,6 +32,10 @@ def main():
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--c", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--hybrid", action="store_true",
+                    help="N = P point groups x Q window groups: the slowest rank runs n/P points over the first "
+                         "ceil(W/Q) windows, for Q in 1, 2, 4 and the window bits of --hybrid-c")
+    ap.add_argument("--hybrid-c", type=int, nargs="+", default=[17, 19, 20])
     args = ap.parse_args()
     import torch
     from tachyon_amd import dist as D
@@ -44,6 +48,28 @@ def main():
     torch.cuda.synchronize()
     m = M.VariableBaseMSMGpu("bn254_g1")
     whole = best_ms(lambda: m.run(d_b, d_s, n), args.reps)
+    if args.hybrid:
+        for world in args.worlds:
+            for q in (1, 2, 4):
+                if q > world:
+                    continue
+                shard = n // (world // q)
+                for c in args.hybrid_c:
+                    W = D._windows_for("bn254_g1", c)
+                    w1 = -(-W // q)
+                    m.set_window_bits(c)
+                    t = best_ms(lambda: m.run_window_range(d_b, d_s, 0, w1, shard), args.reps)
+                    m.set_profile(True)
+                    m.run_window_range(d_b, d_s, 0, w1, shard)
+                    ph = {k: round(v, 3) for k, v in m.last_timings().items()}
+                    m.set_profile(False)
+                    m.set_window_bits(0)
+                    print(json.dumps({"log_n": args.log_n, "world": world, "point_groups": world // q,
+                                      "window_groups": q, "c": c, "windows_slowest_rank": w1, "points_per_rank": shard,
+                                      "whole_ms": round(whole, 3), "rank_ms": round(t, 3),
+                                      "efficiency": round(whole / (world * t), 3), "phases": ph}), flush=True)
+        m.close()
+        return
     W = D._windows_for("bn254_g1", args.c)
     for world in args.worlds:
         shard = n // world
