@@ -39,6 +39,7 @@ def main():
             for v in args.variants:
                 plan.set_variant(v)
                 x0 = x.clone()
+                torch.cuda.synchronize()  # the clone (current stream) before the plan's stream reads x0
                 plan.run_stage(1, False, x0, y)
                 s.synchronize()
                 out = y.clone()
