@@ -259,7 +259,7 @@ Groth16Prover<G1, G2>::Groth16Prover(const Groth16Prover& src, int src_device, h
   abc_.ensure(src.abc_.capacity());
   full_.ensure(src.full_.capacity());
   variant_ = src.variant_;
-  build_groups();
+  // (no grouped-MSM layout: device copies only run the multi-rank split, world >= 2)
 }
 
 template <class G1, class G2>
