@@ -40,9 +40,13 @@ def main():
                 plan.set_variant(v)
                 x0 = x.clone()
                 torch.cuda.synchronize()  # the clone (current stream) before the plan's stream reads x0
+                # both stages (the round-4 stage 1 leaves lazy [0, 2p) values in the send buffer, the fused
+                # one canonical ones, so the variants agree on the transform, not on the packed bytes)
                 plan.run_stage(1, False, x0, y)
+                plan.run_stage(2, False, y, x0)
                 s.synchronize()
-                out = y.clone()
+                out = x0.clone()
+                torch.cuda.synchronize()
                 if ref is None:
                     ref = out
                 assert torch.equal(out, ref), (world, v)
