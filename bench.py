@@ -87,9 +87,11 @@ def parse():
     ap.add_argument("--no-host-resident", action="store_true")
     ap.add_argument("--no-non-uniform", action="store_true",
                     help="skip the NonUniform(n, 1) leg (benchmark/msm --test_set non_uniform)")
-    ap.add_argument("--msm-split", choices=("points", "windows"), default="points",
+    ap.add_argument("--msm-split", choices=("points", "windows", "hybrid"), default="points",
                     help="N > 1 MSM partition: point shards (default), or window ranges with every rank holding "
-                         "all points (c = 16: W = 16 windows; measured slower per rank, tools/split_probe.py)")
+                         "all points (c = 16: W = 16 windows; measured slower per rank, tools/split_probe.py), or "
+                         "hybrid: N / Q point groups x Q window groups (--window-groups; c = --window-bits or 20)")
+    ap.add_argument("--window-groups", type=int, default=2, help="Q of --msm-split hybrid")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the configs[1]/[2] size sweeps (profiling runs: one MSM and one NTT size only)")
     ap.add_argument("--bls-log-n", type=int, default=24,
@@ -523,7 +525,14 @@ def main():
     split = args.msm_split
     if world == 1:
         split = "points"
-    start, n = D.shard_range(n_total, rank, world) if split == "points" else (0, n_total)
+    if split == "hybrid":  # P = N / Q point groups x Q window groups; this rank: point group p, window group q
+        q_groups = max(1, min(args.window_groups, world))
+        p_groups = world // q_groups
+        if p_groups * q_groups != world:
+            raise SystemExit("--window-groups must divide the world size")
+        start, n = D.shard_range(n_total, rank // q_groups, p_groups)
+    else:
+        start, n = D.shard_range(n_total, rank, world) if split == "points" else (0, n_total)
     d_bases = torch.empty(max(1, n) * 64, dtype=torch.uint8, device="cuda")
     d_scalars = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
     chunk = 1 << 10
@@ -533,15 +542,18 @@ def main():
     torch.cuda.synchronize()
 
     msm = M.VariableBaseMSMGpu("bn254_g1")
-    split_c = args.window_bits or 16
+    split_c = args.window_bits or (20 if split == "hybrid" else 16)
     if split == "windows":
         w_lo, w_hi = D.window_range(D._windows_for("bn254_g1", split_c), rank, world)
+        msm.set_window_bits(split_c)
+    elif split == "hybrid":
+        w_lo, w_hi = D.window_range(D._windows_for("bn254_g1", split_c), rank % q_groups, q_groups)
         msm.set_window_bits(split_c)
     elif args.window_bits:
         msm.set_window_bits(args.window_bits)
 
     def local_run():
-        if split == "windows":
+        if split in ("windows", "hybrid"):
             return msm.run_window_range(d_bases, d_scalars, w_lo, w_hi, n)
         return msm.run(d_bases, d_scalars, n)
 
@@ -559,6 +571,8 @@ def main():
     def step():
         if split == "windows":
             return D.window_split_msm("bn254_g1", msm, d_bases, d_scalars, n, split_c, device="cuda")
+        if split == "hybrid":  # every (point group, window range) partial, summed on every rank
+            return D.sharded_msm("bn254_g1", local_run, device="cuda")
         if lib_comm is not None:
             return msm.run_sharded(lib_comm, d_bases, d_scalars, n)
         return D.sharded_msm("bn254_g1", local_run, device="cuda")
@@ -591,7 +605,7 @@ def main():
     acc_ms = sorted(p["acc"] for p in prof)[1] / launches
     c, windows = M.plan("bn254_g1", n)
     rank_windows = windows
-    if split == "windows":
+    if split in ("windows", "hybrid"):
         c, windows = split_c, D._windows_for("bn254_g1", split_c)
         rank_windows = w_hi - w_lo
     elif args.window_bits:
@@ -636,6 +650,9 @@ def main():
                    "windows_per_gpu": rank_windows,
                    "parallelism": (f"msm window ranges x{world} (every rank all points, {rank_windows} of {windows} "
                                    f"windows) + RCCL all-gather of partial points" if split == "windows" else
+                                   f"msm point groups x{world // max(1, (q_groups if split == 'hybrid' else 1))} x window "
+                                   f"groups x{q_groups if split == 'hybrid' else 1} ({rank_windows} of {windows} windows "
+                                   f"per rank) + RCCL all-gather of partial points" if split == "hybrid" else
                                    f"msm point shards x{world} + RCCL all-gather of partial points"
                                    + (f" (inside the library, {lib_comm.backend} communicator)" if lib_comm else ""))},
         "consistent_across_steps": consistent,
