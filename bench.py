@@ -87,10 +87,11 @@ def parse():
     ap.add_argument("--no-host-resident", action="store_true")
     ap.add_argument("--no-non-uniform", action="store_true",
                     help="skip the NonUniform(n, 1) leg (benchmark/msm --test_set non_uniform)")
-    ap.add_argument("--msm-split", choices=("points", "windows", "hybrid"), default="points",
+    ap.add_argument("--msm-split", choices=("auto", "points", "windows", "hybrid"), default="auto",
                     help="N > 1 MSM partition: point shards (default), or window ranges with every rank holding "
                          "all points (c = 16: W = 16 windows; measured slower per rank, tools/split_probe.py), or "
-                         "hybrid: N / Q point groups x Q window groups (--window-groups; c = --window-bits or 20)")
+                         "hybrid: N / Q point groups x Q window groups (--window-groups; c = --window-bits or 19); "
+                         "auto (default): points below 8 GPUs, hybrid with Q = 2 from 8")
     ap.add_argument("--window-groups", type=int, default=2, help="Q of --msm-split hybrid")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the configs[1]/[2] size sweeps (profiling runs: one MSM and one NTT size only)")
@@ -332,6 +333,12 @@ def full_msm_equals(curve, n_total, sharded, rank, dist):
 # all-gather latency; both are ASSUMPTIONS (no multi-GPU box here), every other
 # term of a projection is measured in this run.
 XGMI_LINK_GBS = 76.0
+# --msm-split auto: point shards up to 4 GPUs, from 8 the hybrid partition (N/2
+# point groups x 2 window groups at c = 19) -- per slowest rank at 2^26 / 8
+# GPUs 11.45 ms vs 12.11 ms for the 2^23 point shard; at 4 GPUs 21.45 vs 21.40
+# (tools/split_probe.py --hybrid, profiles/r05c/hybrid_split_probe.jsonl)
+HYBRID_C = 19
+HYBRID_MIN_WORLD = 8
 RCCL_SMALL_ALLGATHER_MS = 0.03
 
 
@@ -359,23 +366,31 @@ def combine_cost_ms(curve, world, reps=20):
     return sorted(ts)[len(ts) // 2] * 1e3
 
 
-def project_msm_scaling(curve, log_n, sweep):
-    """Point-shard projection of the 2^log_n MSM onto N = 2, 4, 8 GPUs from
-    THIS run's single-GPU shard times (the 2^(log_n - log N) entries of the
-    sweep, prefixes of the same input): per rank T_shard + the combine (host
-    side measured here + the assumed RCCL all-gather latency).  Efficiency =
-    projected value / (N x the 1-GPU value)."""
+def project_msm_scaling(curve, log_n, sweep, hybrid=None):
+    """Projection of the 2^log_n MSM onto N = 2, 4, 8 GPUs from THIS run's
+    single-GPU times: point shards (the 2^(log_n - log N) entries of the
+    sweep, prefixes of the same input) and, where measured, the hybrid
+    partition's slowest rank (`hybrid[N]`: N/2 point groups x 2 window groups);
+    per rank T + the combine (host side measured here + the assumed RCCL
+    all-gather latency).  `plan` is the faster one -- the partition
+    --msm-split auto runs.  Efficiency = projected value / (N x the 1-GPU value)."""
     t1 = sweep[str(log_n)]["ms"]
-    out = {"model": "t(N) = t_1gpu(2^log_n / N points, measured above) + combine (measured host side + "
-                    f"{RCCL_SMALL_ALLGATHER_MS} ms assumed RCCL small all-gather)", "t1_ms": t1}
+    out = {"model": "t(N) = min(t_1gpu(2^log_n / N points), t_1gpu(hybrid rank)) (measured above) + combine "
+                    f"(measured host side + {RCCL_SMALL_ALLGATHER_MS} ms assumed RCCL small all-gather)", "t1_ms": t1}
     for lg_world in (1, 2, 3):
         world = 1 << lg_world
         key = str(log_n - lg_world)
         if key not in sweep:
             continue
         comb = combine_cost_ms(curve, world) + RCCL_SMALL_ALLGATHER_MS
-        t = sweep[key]["ms"] + comb
-        out[f"n{world}"] = {"shard_log_n": log_n - lg_world, "shard_ms": sweep[key]["ms"],
+        t_points = sweep[key]["ms"]
+        t_hybrid = (hybrid or {}).get(str(world))
+        use_hybrid = t_hybrid is not None and world >= HYBRID_MIN_WORLD
+        t = (t_hybrid if use_hybrid else t_points) + comb
+        out[f"n{world}"] = {"shard_log_n": log_n - lg_world, "shard_ms": t_points,
+                            "hybrid_rank_ms": t_hybrid,
+                            "plan": f"hybrid {world // 2} point groups x 2 window groups, c = {HYBRID_C}"
+                                    if use_hybrid else "point shards",
                             "combine_ms": round(comb, 4), "ms": round(t, 3),
                             "scalars_per_s": (1 << log_n) / (t * 1e-3), "efficiency": round(t1 / (world * t), 3)}
     return out
@@ -521,8 +536,13 @@ def main():
     # windows; default) or the window split (each rank all n points, W/N of
     # W = 16 windows) -- per-rank cost at 2^26 / 8 ranks 14.4 vs 16.2 ms: the
     # split's recode of all n scalars per rank and its 2 x 2^26 additions
-    # (vs 15 x 2^23 at the shard's c = 17) outweigh the smaller bucket set
+    # (vs 15 x 2^23 at the shard's c = 17) outweigh the smaller bucket set.
+    # The hybrid (N/2 point groups x 2 window groups, c = 19) sits between:
+    # 2^24 points over 7 windows per rank at N = 8, 11.45 vs 12.11 ms for the
+    # point shard (profiles/r05c), so auto picks it from 8 GPUs
     split = args.msm_split
+    if split == "auto":
+        split = "hybrid" if world >= HYBRID_MIN_WORLD else "points"
     if world == 1:
         split = "points"
     if split == "hybrid":  # P = N / Q point groups x Q window groups; this rank: point group p, window group q
@@ -542,7 +562,7 @@ def main():
     torch.cuda.synchronize()
 
     msm = M.VariableBaseMSMGpu("bn254_g1")
-    split_c = args.window_bits or (20 if split == "hybrid" else 16)
+    split_c = args.window_bits or (HYBRID_C if split == "hybrid" else 16)
     if split == "windows":
         w_lo, w_hi = D.window_range(D._windows_for("bn254_g1", split_c), rank, world)
         msm.set_window_bits(split_c)
@@ -700,7 +720,24 @@ def main():
             sweep[str(k)] = {"ms": round(best * 1e3, 3), "scalars_per_s": m / best}
         sweep[str(args.log_n)] = {"ms": round(ms_per_step, 3), "scalars_per_s": value}
         out["msm_sweep"] = sweep
-        out["projected_scaling"] = {"msm": project_msm_scaling("bn254_g1", args.log_n, sweep)}
+        # the hybrid partition's slowest rank (N / 2 point groups x 2 window
+        # groups, c = 19: 2N^-1 of the points over the first 7 of 14 windows),
+        # the plan --msm-split auto runs from 8 GPUs (tools/split_probe.py
+        # --hybrid, profiles/r05c: 11.45 vs 12.11 ms per rank at N = 8)
+        hybrid = {}
+        for lg_world in (2, 3):
+            m = (1 << args.log_n) >> (lg_world - 1)
+            w1 = -(-D._windows_for("bn254_g1", HYBRID_C) // 2)
+            msm.set_window_bits(HYBRID_C)
+            msm.run_window_range(d_bases, d_scalars, 0, w1, m)
+            ts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                msm.run_window_range(d_bases, d_scalars, 0, w1, m)
+                ts.append(time.perf_counter() - t0)
+            msm.set_window_bits(args.window_bits or 0)
+            hybrid[str(1 << lg_world)] = round(sorted(ts)[1] * 1e3, 3)
+        out["projected_scaling"] = {"msm": project_msm_scaling("bn254_g1", args.log_n, sweep, hybrid)}
 
     # ---- NonUniform(n, 1) test set (variable_base_msm_test_set.h:43-53), the set of the reference's
     # published GPU table (benchmark/msm/README.md:97-111): every scalar equal, so every window puts
