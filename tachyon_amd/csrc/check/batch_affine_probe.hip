@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kBlock, BatchWaves<G>::value) void batch_affine_ker
     if constexpr (kFermat) {
       inv = fermat_inverse(pre[G - 1]);
       const F29 one = mul(inv, pre[G - 1]);
-      bad |= is_zero_mod_p(add_ksub(one, kK4, konst(kOne29))) ? 0u : 1u;
+      bad |= is_zero_mod_p(normalize(add_ksub(one, kK4, konst(kOne29)))) ? 0u : 1u;  // limbs carried first
     } else {
       inv = mul(pre[G - 1], pre[G - 1]);
     }
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kThreads) void batch_affine_lds_kernel(const uint32
     if constexpr (kFermat) {
       inv = fermat_inverse(pre);
       const F29 one = mul(inv, pre);
-      bad |= is_zero_mod_p(add_ksub(one, kK4, konst(kOne29))) ? 0u : 1u;
+      bad |= is_zero_mod_p(normalize(add_ksub(one, kK4, konst(kOne29)))) ? 0u : 1u;  // limbs carried first
     } else {
       inv = mul(pre, pre);
     }
