@@ -85,6 +85,31 @@ def main(d):
                           "traffic_bytes": 2 * fb + wb}
         with open(os.path.join(d, "pmc_traffic.json"), "w") as fh:
             json.dump(traffic, fh, indent=1)
+        derived(agg, traffic)
+
+
+def derived(agg, traffic, msm_log_n=26, windows=13, ntt_log_n=24):
+    """Per-unit figures of the default bench command: VALU instructions per NTT
+    butterfly (a 2^24 pass = 8 stages x 2^23 butterflies) and HBM bytes per
+    sorted MSM entry (13 x 2^26 entries of 8 B at the default plan)."""
+    lines = []
+    v = agg.get(("dif_pass_kernel", "SQ_INSTS_VALU"))
+    if v:
+        bfly = 8 * (1 << (ntt_log_n - 1))
+        lines.append(f"* `dif_pass_kernel`: {sum(v) / len(v) * 64 / bfly:.0f} VALU instructions per butterfly "
+                     f"(per-dispatch SQ_INSTS_VALU x 64 / (8 stages x 2^{ntt_log_n - 1} butterflies), "
+                     f"{len(v)} dispatches of 2^{ntt_log_n} passes)")
+    entries = windows * (1 << msm_log_n)
+    for k, what in (("onesweep_iteration", "rocprim::onesweep_iteration"), ("recode_scatter_kernel", None),
+                    ("recode_hist_kernel", None), ("seg_acc29_kernel", None)):
+        t = traffic.get(what or k)
+        if t:
+            lines.append(f"* `{what or k}`: {t['traffic_bytes'] / entries:.2f} HBM B per entry "
+                         f"({t['fetch_bytes_x2'] / entries:.2f} read x2-corrected + {t['write_bytes'] / entries:.2f} "
+                         f"written; {windows} x 2^{msm_log_n} entries of 8 B)")
+    if lines:
+        print("\n## Per-unit figures (default bench plan: MSM 2^26, c = 20, 13 windows; NTT 2^24)\n")
+        print("\n".join(lines))
 
 
 if __name__ == "__main__":
