@@ -464,8 +464,11 @@ def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backen
     reps = max(2, min(args.steps, 5))
     barrier()
     t0 = time.perf_counter()
+    rep_ms = []
     for _ in range(reps):
+        t_rep = time.perf_counter()
         proof = step()
+        rep_ms.append((time.perf_counter() - t_rep) * 1e3)
     barrier()
     dt = (time.perf_counter() - t0) / reps
     if dist is not None:
@@ -485,7 +488,8 @@ def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backen
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import groth16 as OG  # checker only: the CPU restatement of the same proof
         equals_oracle = tuple(OG.prove_np(zkey, full)) == tuple(proof)
-    out = {"ms_per_proof": dt * 1e3, "proofs_per_s": 1 / dt, "constraints": 1 << args.groth16_log_n,
+    out = {"ms_per_proof": dt * 1e3, "proofs_per_s": 1 / dt, "ms_per_proof_reps": [round(x, 3) for x in rep_ms],
+           "constraints": 1 << args.groth16_log_n,
            "num_vars": prover.num_vars, "mode": "NoZK, host-resident witness, device-resident proving key",
            "consistent": proof == ref, "equals_cpu_oracle": equals_oracle, "phase_ms": phases,
            "setup_s": round(setup_s, 1),
