@@ -106,8 +106,11 @@ __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ s
 
 // Recode fused with the first radix pass (key bits 0..7), in two launches:
 // recode_hist_kernel counts, per block of spt x 256 scalars, the entries
-// of each low-byte bin (LDS atomics) into hist[bin * nblocks + block]; after
-// an exclusive scan of hist, recode_scatter_kernel recomputes the digits and
+// of each low-byte bin (LDS atomics) into the block's row hist[block * 256 +
+// bin]; bin_chunk_sums / bin_chunk_scan / bin_offsets_kernel turn the rows
+// into every (block, bin)'s global slot (bin-major order: all of bin 0's
+// entries first, blocks in order within a bin), written as rows again, and
+// recode_scatter_kernel recomputes the digits and
 // writes every (key, val) to its bin's slot (the rank inside the block's run
 // from LDS atomics).  This pass need not be stable -- the later stable passes
 // over bits 8.. keep the bin grouping, and the order inside a bucket does not
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
       }, glen, gstep);
   }
   __syncthreads();
-  hist[(size_t)t * nblocks + blockIdx.x] = cnt[0][t];
+  hist[(size_t)blockIdx.x * 256 + t] = cnt[0][t];  // one coalesced 1 KiB row per block
   for (uint32_t p = 1; p <= places; ++p) later[((size_t)(p - 1) * nblocks + blockIdx.x) * 256 + t] = cnt[p][t];
 }
 
@@ -215,6 +218,75 @@ __global__ __launch_bounds__(kBlock) void digit_scan_kernel(const uint32_t* __re
   offsets[q * 256 + t] = v - mine + add;
 }
 
+// The fused recode's slots from its per-block bin rows (hist[block][bin],
+// 256 bins): slot(block, bin) = sum_{bin' < bin} total(bin') + sum_{block' <
+// block} hist[block'][bin] -- the exclusive scan of the bin-major flattening,
+// computed over coalesced 1 KiB rows (the bin-major array itself would be
+// written and read one 4-byte word per 64-byte line by the recode kernels).
+// Chunks of per_chunk consecutive blocks: csum[chunk][bin] = the chunk's sum.
+__global__ __launch_bounds__(kBlock) void bin_chunk_sums_kernel(const uint32_t* __restrict__ rows, uint32_t nblocks,
+                                                                uint32_t per_chunk, uint32_t* __restrict__ csum) {
+  const uint32_t t = threadIdx.x, b0 = blockIdx.x * per_chunk, b1 = min(nblocks, b0 + per_chunk);
+  uint32_t acc = 0;
+  for (uint32_t b = b0; b < b1; ++b) acc += rows[(size_t)b * 256 + t];
+  csum[(size_t)blockIdx.x * 256 + t] = acc;
+}
+
+// workgroup = one bin: cpre[chunk][bin] = exclusive prefix of csum[.][bin]
+// over the chunks, total[bin] = the bin's count (a block scan per 256 chunks)
+__global__ __launch_bounds__(kBlock) void bin_chunk_scan_kernel(const uint32_t* __restrict__ csum, uint32_t chunks,
+                                                                uint32_t* __restrict__ cpre,
+                                                                uint32_t* __restrict__ total) {
+  const uint32_t bin = blockIdx.x, t = threadIdx.x;
+  __shared__ uint32_t wave_tot[kBlock / 64];
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < chunks; c0 += kBlock) {
+    const uint32_t ch = c0 + t;
+    const uint32_t mine = ch < chunks ? csum[(size_t)ch * 256 + bin] : 0u;
+    uint32_t v = mine;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t u = __shfl_up(v, d, 64);
+      if ((t & 63) >= (uint32_t)d) v += u;
+    }
+    if ((t & 63) == 63) wave_tot[t >> 6] = v;
+    __syncthreads();
+    uint32_t add = carry, tile = 0;
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+      if (w < (t >> 6)) add += wave_tot[w];
+      tile += wave_tot[w];
+    }
+    if (ch < chunks) cpre[(size_t)ch * 256 + bin] = v - mine + add;
+    carry += tile;
+    __syncthreads();  // wave_tot is rewritten by the next tile
+  }
+  if (t == 0) total[bin] = carry;
+}
+
+// workgroup = one chunk, thread = one bin: the chunk's rows of slots
+__global__ __launch_bounds__(kBlock) void bin_offsets_kernel(const uint32_t* __restrict__ rows, uint32_t nblocks,
+                                                             uint32_t per_chunk, const uint32_t* __restrict__ cpre,
+                                                             const uint32_t* __restrict__ total,
+                                                             uint32_t* __restrict__ off) {
+  const uint32_t t = threadIdx.x, b0 = blockIdx.x * per_chunk, b1 = min(nblocks, b0 + per_chunk);
+  // exclusive scan of the 256 bin totals: this bin's base
+  const uint32_t mine = total[t];
+  uint32_t v = mine;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(v, d, 64);
+    if ((t & 63) >= (uint32_t)d) v += u;
+  }
+  __shared__ uint32_t wave_tot[kBlock / 64];
+  if ((t & 63) == 63) wave_tot[t >> 6] = v;
+  __syncthreads();
+  uint32_t run = v - mine + cpre[(size_t)blockIdx.x * 256 + t];
+  for (uint32_t w = 0; w < (t >> 6); ++w) run += wave_tot[w];
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = rows[(size_t)b * 256 + t];
+    off[(size_t)b * 256 + t] = run;
+    run += c;
+  }
+}
+
 // kNarrow: keys of <= 24 bits are staged as 7 bytes (val, key >> 8, bin),
 // 47 KiB instead of 53 KiB per block at 13 windows -- three workgroups per
 // CU instead of two.
@@ -235,8 +307,8 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
   uint8_t* lbins = reinterpret_cast<uint8_t*>(lkeys + (size_t)spt * kBlock * wr);
   __shared__ uint32_t base[256], loff[256], cur[256];
   const uint32_t t = threadIdx.x;
-  base[t] = off[(size_t)t * nblocks + blockIdx.x];
-  const uint32_t mine = hist[(size_t)t * nblocks + blockIdx.x];
+  base[t] = off[(size_t)blockIdx.x * 256 + t];
+  const uint32_t mine = hist[(size_t)blockIdx.x * 256 + t];
   // exclusive scan of the block's 256 bin counts (4 waves x 64 lanes)
   uint32_t v = mine;
   for (int d = 1; d < 64; d <<= 1) {
@@ -1964,10 +2036,16 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     const uint32_t nblocks = (uint32_t)((n + spt * kBlock - 1) / (spt * kBlock));
     const size_t hn = (size_t)256 * nblocks;
     const unsigned later_places = own_sort ? places : 0;
-    uint32_t* hist = static_cast<uint32_t*>(hist_.ensure((2 + later_places) * hn * 4 + 5 * 256 * 4));
+    // slot chunks: <= 1024 chunks of >= 4 blocks (bin_chunk_scan_kernel's loop, bin_offsets_kernel's rows)
+    const uint32_t bper = std::max<uint32_t>(4, (nblocks + 1023) / 1024), bchunks = (nblocks + bper - 1) / bper;
+    uint32_t* hist = static_cast<uint32_t*>(
+        hist_.ensure(((2 + later_places) * hn + 5 * 256 + 2 * (size_t)bchunks * 256 + 256) * 4));
     uint32_t* hoff = hist + hn;
     uint32_t* later = hist + 2 * hn;
     uint32_t* digit_cnt = later + later_places * hn;  // 2 x 256 counts, 2 x 256 offsets, 256 spare
+    uint32_t* bcsum = digit_cnt + 5 * 256;            // [chunk][bin] sums, then prefixes, then the bin totals
+    uint32_t* bcpre = bcsum + (size_t)bchunks * 256;
+    uint32_t* btotal = bcpre + (size_t)bchunks * 256;
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
                        Wt, wr0, Ws, nblocks, spt, later_places, hist, later, reinterpret_cast<uint4*>(bucket_sum),
                        nb * slot / 16, glen, gstep);
@@ -1982,10 +2060,11 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       hipLaunchKernelGGL(digit_scan_kernel, dim3(later_places), dim3(kBlock), 0, stream_, digit_cnt, digit_off);
       TA_HIP(hipGetLastError());
     }
-    size_t hscan_bytes = 0;
-    TA_HIP(rocprim::exclusive_scan(nullptr, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
-    void* hscan_tmp = hscan_tmp_.ensure(hscan_bytes);
-    TA_HIP(rocprim::exclusive_scan(hscan_tmp, hscan_bytes, hist, hoff, 0u, hn, rocprim::plus<uint32_t>(), stream_));
+    hipLaunchKernelGGL(bin_chunk_sums_kernel, dim3(bchunks), dim3(kBlock), 0, stream_, hist, nblocks, bper, bcsum);
+    hipLaunchKernelGGL(bin_chunk_scan_kernel, dim3(256), dim3(kBlock), 0, stream_, bcsum, bchunks, bcpre, btotal);
+    hipLaunchKernelGGL(bin_offsets_kernel, dim3(bchunks), dim3(kBlock), 0, stream_, hist, nblocks, bper, bcpre, btotal,
+                       hoff);
+    TA_HIP(hipGetLastError());
     // the scattered entries are fully sorted when the key has <= 8 bits; the
     // own onesweep passes ping-pong from the scatter's output and end in ents2
     uint64_t* dst = own_sort ? (places % 2 == 0 ? ents2 : ents) : (sort_begin < key_bits ? ents : ents2);
