@@ -36,17 +36,21 @@ def main():
                     help="N = P point groups x Q window groups: the slowest rank runs n/P points over the first "
                          "ceil(W/Q) windows, for Q in 1, 2, 4 and the window bits of --hybrid-c")
     ap.add_argument("--hybrid-c", type=int, nargs="+", default=[17, 19, 20])
+    ap.add_argument("--curve", default="bn254_g1", help="bn254_g1, bls12_381_g1 or bls12_381_g2")
     args = ap.parse_args()
     import torch
     from tachyon_amd import dist as D
     from tachyon_amd import msm as M
+    from tachyon_amd._lib import CURVE_INFO
     n = 1 << args.log_n
-    d_b = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    curve = args.curve
+    pb, sf = CURVE_INFO[curve]
+    d_b = torch.empty(n * pb, dtype=torch.uint8, device="cuda")
     d_s = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
-    M.gen_bases("bn254_g1", 1, n, 1024, d_b.data_ptr())
-    M.gen_scalars("bn254_fr", 1, n, d_s.data_ptr())
+    M.gen_bases(curve, 1, n, 1024, d_b.data_ptr())
+    M.gen_scalars(sf, 1, n, d_s.data_ptr())
     torch.cuda.synchronize()
-    m = M.VariableBaseMSMGpu("bn254_g1")
+    m = M.VariableBaseMSMGpu(curve)
     whole = best_ms(lambda: m.run(d_b, d_s, n), args.reps)
     if args.hybrid:
         for world in args.worlds:
@@ -55,7 +59,7 @@ def main():
                     continue
                 shard = n // (world // q)
                 for c in args.hybrid_c:
-                    W = D._windows_for("bn254_g1", c)
+                    W = D._windows_for(curve, c)
                     w1 = -(-W // q)
                     m.set_window_bits(c)
                     t = best_ms(lambda: m.run_window_range(d_b, d_s, 0, w1, shard), args.reps)
@@ -64,13 +68,13 @@ def main():
                     ph = {k: round(v, 3) for k, v in m.last_timings().items()}
                     m.set_profile(False)
                     m.set_window_bits(0)
-                    print(json.dumps({"log_n": args.log_n, "world": world, "point_groups": world // q,
+                    print(json.dumps({"curve": curve, "log_n": args.log_n, "world": world, "point_groups": world // q,
                                       "window_groups": q, "c": c, "windows_slowest_rank": w1, "points_per_rank": shard,
                                       "whole_ms": round(whole, 3), "rank_ms": round(t, 3),
                                       "efficiency": round(whole / (world * t), 3), "phases": ph}), flush=True)
         m.close()
         return
-    W = D._windows_for("bn254_g1", args.c)
+    W = D._windows_for(curve, args.c)
     for world in args.worlds:
         shard = n // world
         pts = best_ms(lambda: m.run(d_b, d_s, shard), args.reps)
