@@ -91,7 +91,7 @@ def parse():
                     help="N > 1 MSM partition: point shards (default), or window ranges with every rank holding "
                          "all points (c = 16: W = 16 windows; measured slower per rank, tools/split_probe.py), or "
                          "hybrid: N / Q point groups x Q window groups (--window-groups; c = --window-bits or 19); "
-                         "auto (default): points below 8 GPUs, hybrid with Q = 2 from 8")
+                         "auto (default): the hybrid where HYBRID_PLANS has a plan for (curve, N), else points")
     ap.add_argument("--window-groups", type=int, default=2, help="Q of --msm-split hybrid")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the configs[1]/[2] size sweeps (profiling runs: one MSM and one NTT size only)")
@@ -218,24 +218,35 @@ def synth_groth16_zkey(log_n, seed=SEED):
 
 
 def bench_bls(args, rank, world, barrier, dist, backend):
-    """BLS12-381 G1 and G2 MSMs at 2^k (BASELINE configs[3]): point shards per
-    rank + the all-gather of partials, device-resident inputs, as the headline."""
+    """BLS12-381 G1 and G2 MSMs at 2^k (BASELINE configs[3]): each rank's share
+    of one global input (point shards, or the hybrid of HYBRID_PLANS) + the
+    all-gather of partials, device-resident inputs, as the headline."""
     import torch
     from tachyon_amd import dist as D
     from tachyon_amd import msm as M
     out = {}
     n_total = 1 << args.bls_log_n
-    start, n = D.shard_range(n_total, rank, world)
+    parts = {}
     for curve, pb in (("bls12_381_g1", 96), ("bls12_381_g2", 192)):
+        split, start, n, wrange, split_c, p_groups, q_groups = msm_partition(args, curve, world, rank, n_total)
+        parts[curve] = (split if split != "hybrid" else f"hybrid {p_groups} point groups x {q_groups} window groups, "
+                        f"c = {split_c}")
         d_b = torch.empty(max(1, n) * pb, dtype=torch.uint8, device="cuda")
         d_s = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
         M.gen_bases(curve, SEED, n, 1 << 10, d_b.data_ptr(), start=start)  # this rank's slice of one input
         M.gen_scalars("bls12_381_fr", SEED, n, d_s.data_ptr(), start=start)
         torch.cuda.synchronize()
         msm = M.VariableBaseMSMGpu(curve)
+        if wrange is not None:
+            msm.set_window_bits(split_c)
+
+        def local_run():
+            if wrange is not None:
+                return msm.run_window_range(d_b, d_s, wrange[0], wrange[1], n)
+            return msm.run(d_b, d_s, n)
 
         def step():
-            return D.sharded_msm(curve, lambda: msm.run(d_b, d_s, n), device="cuda")
+            return D.sharded_msm(curve, local_run, device="cuda")
 
         ref = step()
         reps = max(2, min(args.steps, 3))
@@ -250,7 +261,8 @@ def bench_bls(args, rank, world, barrier, dist, backend):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         leg = out[curve.split("_")[-1]] = {"ms_per_msm": dt * 1e3, "scalars_per_s": n_total / dt,
-                                           "consistent": res == ref, "points_per_gpu": n}
+                                           "consistent": res == ref, "points_per_gpu": n,
+                                           "partition": parts[curve] if world > 1 else "single GPU"}
         if world == 1 and not args.no_sweep:
             # the per-rank shards of this MSM at N = 2, 4, 8 (prefixes of the same input) and the
             # point-shard projection built on them
@@ -264,7 +276,9 @@ def bench_bls(args, rank, world, barrier, dist, backend):
                     ts.append(time.perf_counter() - t0)
                 sw[str(k)] = {"ms": round(sorted(ts)[1] * 1e3, 3), "scalars_per_s": (1 << k) / sorted(ts)[1]}
             leg["shard_sweep"] = sw
-            leg["projected_scaling"] = project_msm_scaling(curve, args.bls_log_n, sw)
+            hybrid = {str(w): hybrid_rank_ms(msm, curve, d_b, d_s, n_total, w)
+                      for w in (2, 4, 8) if (curve, w) in HYBRID_PLANS}
+            leg["projected_scaling"] = project_msm_scaling(curve, args.bls_log_n, sw, hybrid)
         msm.close()
         if world == 1 and not args.no_cpu_baseline:
             # the reference's GPU-vs-CPU check (variable_base_msm_gpu_unittest.cc:25-78) at the timed
@@ -279,7 +293,8 @@ def bench_bls(args, rank, world, barrier, dist, backend):
         if world > 1:  # the sharded MSM must equal the unsharded one
             out[curve.split("_")[-1]]["consistent_with_1gpu"] = full_msm_equals(curve, n_total, res, rank, dist)
     out["workload"] = (f"BLS12-381 G1 and G2 VariableBaseMSM 2^{args.bls_log_n} (BASELINE configs[3]), "
-                       f"device-resident inputs, point shards x{world} + all-gather of partials")
+                       f"device-resident inputs" + (f", {world} ranks (partition per curve) + all-gather of partials"
+                                                    if world > 1 else ""))
     return out
 
 
@@ -333,12 +348,64 @@ def full_msm_equals(curve, n_total, sharded, rank, dist):
 # all-gather latency; both are ASSUMPTIONS (no multi-GPU box here), every other
 # term of a projection is measured in this run.
 XGMI_LINK_GBS = 76.0
-# --msm-split auto: point shards up to 4 GPUs, from 8 the hybrid partition (N/2
-# point groups x 2 window groups at c = 19) -- per slowest rank at 2^26 / 8
-# GPUs 11.45 ms vs 12.11 ms for the 2^23 point shard; at 4 GPUs 21.45 vs 21.40
-# (tools/split_probe.py --hybrid, profiles/r05c/hybrid_split_probe.jsonl)
-HYBRID_C = 19
-HYBRID_MIN_WORLD = 8
+# --msm-split auto: (curve, N) -> (window groups Q, window bits c) of the hybrid
+# partition (N/Q point groups x Q window groups), point shards elsewhere.  The
+# slowest rank on one MI355X (tools/split_probe.py --hybrid): BN254 2^26 at N =
+# 8 11.45 ms vs 12.11 for the 2^23 point shard, N = 4 21.45 vs 21.40 (points
+# kept) (profiles/r05c/hybrid_split_probe.jsonl); BLS12-381 2^24 G1 N = 4
+# 12.35 vs 12.65, N = 8 6.91 vs 7.02; G2 N = 4 31.16 vs 32.19, N = 8 17.21
+# vs 17.81 (profiles/r05m/)
+HYBRID_PLANS = {("bn254_g1", 8): (2, 19),
+                ("bls12_381_g1", 4): (2, 19), ("bls12_381_g1", 8): (2, 16),
+                ("bls12_381_g2", 4): (2, 19), ("bls12_381_g2", 8): (4, 16)}
+
+
+def msm_partition(args, curve, world, rank, n_total):
+    """This rank's share of the MSM: (split, start, count, window range or None,
+    c or 0, point groups, window groups) -- point shards, the window split or
+    the hybrid (auto: HYBRID_PLANS)."""
+    from tachyon_amd import dist as D
+    split = args.msm_split
+    q, c = HYBRID_PLANS.get((curve, world), (0, 0))
+    if split == "auto":
+        split = "hybrid" if q else "points"
+    elif split == "hybrid":  # forced: --window-groups, --window-bits (else the table's or 19)
+        q, c = args.window_groups, args.window_bits or c or 19
+    if world == 1:
+        split = "points"
+    if split == "points":
+        start, n = D.shard_range(n_total, rank, world)
+        return split, start, n, None, 0, world, 1
+    if split == "windows":
+        c = args.window_bits or 16
+        return split, 0, n_total, D.window_range(D._windows_for(curve, c), rank, world), c, 1, world
+    q = max(1, min(q, world))
+    p = world // q
+    if p * q != world:
+        raise SystemExit("--window-groups must divide the world size")
+    start, n = D.shard_range(n_total, rank // q, p)
+    return split, start, n, D.window_range(D._windows_for(curve, c), rank % q, q), c, p, q
+
+
+def hybrid_rank_ms(msm, curve, d_bases, d_scalars, n_total, world, reps=3):
+    """The slowest rank of HYBRID_PLANS[(curve, world)] on this GPU: n/P points
+    (a prefix of this run's input) over the first ceil(W/Q) c-bit windows."""
+    from tachyon_amd import dist as D
+    q, c = HYBRID_PLANS[(curve, world)]
+    m = n_total // (world // q)
+    w1 = -(-D._windows_for(curve, c) // q)
+    prev = getattr(msm, "window_bits", 0)
+    msm.set_window_bits(c)
+    try:
+        msm.run_window_range(d_bases, d_scalars, 0, w1, m)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            msm.run_window_range(d_bases, d_scalars, 0, w1, m)
+            ts.append(time.perf_counter() - t0)
+    finally:
+        msm.set_window_bits(prev)
+    return round(sorted(ts)[len(ts) // 2] * 1e3, 3)
 RCCL_SMALL_ALLGATHER_MS = 0.03
 
 
@@ -369,11 +436,11 @@ def combine_cost_ms(curve, world, reps=20):
 def project_msm_scaling(curve, log_n, sweep, hybrid=None):
     """Projection of the 2^log_n MSM onto N = 2, 4, 8 GPUs from THIS run's
     single-GPU times: point shards (the 2^(log_n - log N) entries of the
-    sweep, prefixes of the same input) and, where measured, the hybrid
-    partition's slowest rank (`hybrid[N]`: N/2 point groups x 2 window groups);
-    per rank T + the combine (host side measured here + the assumed RCCL
-    all-gather latency).  `plan` is the faster one -- the partition
-    --msm-split auto runs.  Efficiency = projected value / (N x the 1-GPU value)."""
+    sweep, prefixes of the same input) or, where HYBRID_PLANS has a plan for
+    (curve, N), the hybrid partition's slowest rank (`hybrid[N]`, measured
+    by hybrid_rank_ms) -- the partition --msm-split auto runs; per rank T +
+    the combine (host side measured here + the assumed RCCL all-gather
+    latency).  Efficiency = projected value / (N x the 1-GPU value)."""
     t1 = sweep[str(log_n)]["ms"]
     out = {"model": "t(N) = min(t_1gpu(2^log_n / N points), t_1gpu(hybrid rank)) (measured above) + combine "
                     f"(measured host side + {RCCL_SMALL_ALLGATHER_MS} ms assumed RCCL small all-gather)", "t1_ms": t1}
@@ -385,11 +452,12 @@ def project_msm_scaling(curve, log_n, sweep, hybrid=None):
         comb = combine_cost_ms(curve, world) + RCCL_SMALL_ALLGATHER_MS
         t_points = sweep[key]["ms"]
         t_hybrid = (hybrid or {}).get(str(world))
-        use_hybrid = t_hybrid is not None and world >= HYBRID_MIN_WORLD
+        use_hybrid = t_hybrid is not None and (curve, world) in HYBRID_PLANS
         t = (t_hybrid if use_hybrid else t_points) + comb
+        q, c = HYBRID_PLANS.get((curve, world), (0, 0))
         out[f"n{world}"] = {"shard_log_n": log_n - lg_world, "shard_ms": t_points,
                             "hybrid_rank_ms": t_hybrid,
-                            "plan": f"hybrid {world // 2} point groups x 2 window groups, c = {HYBRID_C}"
+                            "plan": f"hybrid {world // q} point groups x {q} window groups, c = {c}"
                                     if use_hybrid else "point shards",
                             "combine_ms": round(comb, 4), "ms": round(t, 3),
                             "scalars_per_s": (1 << log_n) / (t * 1e-3), "efficiency": round(t1 / (world * t), 3)}
@@ -542,22 +610,10 @@ def main():
     # W = 16 windows) -- per-rank cost at 2^26 / 8 ranks 14.4 vs 16.2 ms: the
     # split's recode of all n scalars per rank and its 2 x 2^26 additions
     # (vs 15 x 2^23 at the shard's c = 17) outweigh the smaller bucket set.
-    # The hybrid (N/2 point groups x 2 window groups, c = 19) sits between:
-    # 2^24 points over 7 windows per rank at N = 8, 11.45 vs 12.11 ms for the
-    # point shard (profiles/r05c), so auto picks it from 8 GPUs
-    split = args.msm_split
-    if split == "auto":
-        split = "hybrid" if world >= HYBRID_MIN_WORLD else "points"
-    if world == 1:
-        split = "points"
-    if split == "hybrid":  # P = N / Q point groups x Q window groups; this rank: point group p, window group q
-        q_groups = max(1, min(args.window_groups, world))
-        p_groups = world // q_groups
-        if p_groups * q_groups != world:
-            raise SystemExit("--window-groups must divide the world size")
-        start, n = D.shard_range(n_total, rank // q_groups, p_groups)
-    else:
-        start, n = D.shard_range(n_total, rank, world) if split == "points" else (0, n_total)
+    # The hybrid (N/Q point groups x Q window groups, HYBRID_PLANS) sits
+    # between: 2^24 points over 7 of 14 windows per rank at N = 8, 11.45 vs
+    # 12.11 ms for the point shard (profiles/r05c), so auto runs it at 8 GPUs
+    split, start, n, wrange, split_c, p_groups, q_groups = msm_partition(args, "bn254_g1", world, rank, n_total)
     d_bases = torch.empty(max(1, n) * 64, dtype=torch.uint8, device="cuda")
     d_scalars = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
     chunk = 1 << 10
@@ -567,12 +623,8 @@ def main():
     torch.cuda.synchronize()
 
     msm = M.VariableBaseMSMGpu("bn254_g1")
-    split_c = args.window_bits or (HYBRID_C if split == "hybrid" else 16)
-    if split == "windows":
-        w_lo, w_hi = D.window_range(D._windows_for("bn254_g1", split_c), rank, world)
-        msm.set_window_bits(split_c)
-    elif split == "hybrid":
-        w_lo, w_hi = D.window_range(D._windows_for("bn254_g1", split_c), rank % q_groups, q_groups)
+    if wrange is not None:
+        w_lo, w_hi = wrange
         msm.set_window_bits(split_c)
     elif args.window_bits:
         msm.set_window_bits(args.window_bits)
@@ -675,9 +727,9 @@ def main():
                    "windows_per_gpu": rank_windows,
                    "parallelism": (f"msm window ranges x{world} (every rank all points, {rank_windows} of {windows} "
                                    f"windows) + RCCL all-gather of partial points" if split == "windows" else
-                                   f"msm point groups x{world // max(1, (q_groups if split == 'hybrid' else 1))} x window "
-                                   f"groups x{q_groups if split == 'hybrid' else 1} ({rank_windows} of {windows} windows "
-                                   f"per rank) + RCCL all-gather of partial points" if split == "hybrid" else
+                                   f"msm point groups x{p_groups} x window groups x{q_groups} ({rank_windows} of "
+                                   f"{windows} windows per rank) + RCCL all-gather of partial points"
+                                   if split == "hybrid" else
                                    f"msm point shards x{world} + RCCL all-gather of partial points"
                                    + (f" (inside the library, {lib_comm.backend} communicator)" if lib_comm else ""))},
         "consistent_across_steps": consistent,
@@ -725,23 +777,10 @@ def main():
             sweep[str(k)] = {"ms": round(best * 1e3, 3), "scalars_per_s": m / best}
         sweep[str(args.log_n)] = {"ms": round(ms_per_step, 3), "scalars_per_s": value}
         out["msm_sweep"] = sweep
-        # the hybrid partition's slowest rank (N / 2 point groups x 2 window
-        # groups, c = 19: 2N^-1 of the points over the first 7 of 14 windows),
-        # the plan --msm-split auto runs from 8 GPUs (tools/split_probe.py
-        # --hybrid, profiles/r05c: 11.45 vs 12.11 ms per rank at N = 8)
-        hybrid = {}
-        for lg_world in (2, 3):
-            m = (1 << args.log_n) >> (lg_world - 1)
-            w1 = -(-D._windows_for("bn254_g1", HYBRID_C) // 2)
-            msm.set_window_bits(HYBRID_C)
-            msm.run_window_range(d_bases, d_scalars, 0, w1, m)
-            ts = []
-            for _ in range(3):
-                t0 = time.perf_counter()
-                msm.run_window_range(d_bases, d_scalars, 0, w1, m)
-                ts.append(time.perf_counter() - t0)
-            msm.set_window_bits(args.window_bits or 0)
-            hybrid[str(1 << lg_world)] = round(sorted(ts)[1] * 1e3, 3)
+        # the hybrid partition's slowest rank where auto runs it (HYBRID_PLANS:
+        # N = 8, 4 point groups x 2 window groups at c = 19)
+        hybrid = {str(w): hybrid_rank_ms(msm, "bn254_g1", d_bases, d_scalars, 1 << args.log_n, w)
+                  for w in (2, 4, 8) if ("bn254_g1", w) in HYBRID_PLANS}
         out["projected_scaling"] = {"msm": project_msm_scaling("bn254_g1", args.log_n, sweep, hybrid)}
 
     # ---- NonUniform(n, 1) test set (variable_base_msm_test_set.h:43-53), the set of the reference's

@@ -152,13 +152,22 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
                                                              uint32_t* __restrict__ later,
                                                              uint4* __restrict__ zero, size_t zero_n, uint32_t glen,
                                                              uint32_t gstep) {
-  __shared__ uint32_t cnt[3][256];
+  // cnt2: the third place's counts (key bits 16..23) in four copies, one per
+  // lane & 3, 264 words apart: those bits are the window (the same in every
+  // lane of a step) and the digit's top bits, a handful of values per wave --
+  // one copy gave up to 8 lanes per address in a 32-lane atomic group (8-way
+  // conflicts); with the copies on distinct banks a group spreads over 4x the
+  // addresses.  A wave-uniform value takes one atomic (c <= 16: the bits are
+  // the window alone).
+  constexpr uint32_t kCopy = 264;
+  __shared__ uint32_t cnt[2][256];
+  __shared__ uint32_t cnt2[4 * kCopy];
   const uint32_t t = threadIdx.x;
   // the bucket sums start as the identity (all-zero words): cleared here, not by a memset launch
   for (size_t i = (size_t)blockIdx.x * kBlock + t; i < zero_n; i += (size_t)nblocks * kBlock) zero[i] = uint4{0, 0, 0, 0};
   cnt[0][t] = 0;
   cnt[1][t] = 0;
-  cnt[2][t] = 0;
+  for (uint32_t j = t; j < 4 * kCopy; j += kBlock) cnt2[j] = 0;
   __syncthreads();
   for (uint32_t k = 0; k < spt; ++k) {
     const uint32_t i = blockIdx.x * spt * kBlock + k * kBlock + t;
@@ -168,23 +177,33 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
         // have equal bins): NonUniform inputs take one atomic per wave
         const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
         const uint64_t active = __ballot(1);
+        const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)active) - 1);
         if (__ballot(key == k0) == active) {
-          if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)active) - 1)) {
+          if (__lane_id() == leader) {
             const uint32_t m = (uint32_t)__popcll(active);
             atomicAdd(&cnt[0][k0 & 255], m);
             if (places > 0) atomicAdd(&cnt[1][(k0 >> 8) & 255], m);
-            if (places > 1) atomicAdd(&cnt[2][(k0 >> 16) & 255], m);
+            if (places > 1) atomicAdd(&cnt2[(k0 >> 16) & 255], m);
           }
         } else {
           atomicAdd(&cnt[0][key & 255], 1u);
           if (places > 0) atomicAdd(&cnt[1][(key >> 8) & 255], 1u);
-          if (places > 1) atomicAdd(&cnt[2][(key >> 16) & 255], 1u);
+          if (places > 1) {
+            const uint32_t b2 = (key >> 16) & 255, v0 = __builtin_amdgcn_readfirstlane(b2);
+            if (__ballot(b2 == v0) == active) {
+              if (__lane_id() == leader) atomicAdd(&cnt2[v0], (uint32_t)__popcll(active));
+            } else {
+              atomicAdd(&cnt2[(__lane_id() & 3) * kCopy + b2], 1u);
+            }
+          }
         }
       }, glen, gstep);
   }
   __syncthreads();
   hist[(size_t)blockIdx.x * 256 + t] = cnt[0][t];  // one coalesced 1 KiB row per block
-  for (uint32_t p = 1; p <= places; ++p) later[((size_t)(p - 1) * nblocks + blockIdx.x) * 256 + t] = cnt[p][t];
+  if (places > 0) later[(size_t)blockIdx.x * 256 + t] = cnt[1][t];
+  if (places > 1)
+    later[((size_t)nblocks + blockIdx.x) * 256 + t] = cnt2[t] + cnt2[kCopy + t] + cnt2[2 * kCopy + t] + cnt2[3 * kCopy + t];
 }
 
 // counts[q * 256 + bin] += the later-place counts of a chunk of recode blocks
