@@ -476,7 +476,10 @@ def project_ntt_scaling(log_n, t1_ms, reps=20):
     out = {"model": f"t(N) = rank 0's local stages (measured) + n/N^2 x 32 B per pair at {XGMI_LINK_GBS} GB/s "
                     f"per xGMI link (assumed) + {RCCL_SMALL_ALLGATHER_MS} ms", "t1_ms": t1_ms}
     for world in (2, 4, 8):
-        plan = FourStepNtt(log_n, world, 0)
+        # the split with the fewest pass launches (2^24: 2^8 x 2^16, one packed
+        # pass for the columns) -- local stages 0.282 / 0.545 ms at N = 8 / 4 vs
+        # 0.299 / 0.562 for 2^12 x 2^12 (profiles/r05o/ntt4_probe.jsonl)
+        plan = FourStepNtt(log_n, world, 0, log_r=FourStepNtt.split_log_r(log_n, world))
         m = plan.local_size
         x = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
         y = torch.empty_like(x)
@@ -501,7 +504,8 @@ def project_ntt_scaling(log_n, t1_ms, reps=20):
         # where it projects faster than one GPU, else the single device
         split = t_split < t1_ms
         t = t_split if split else t1_ms
-        out[f"n{world}"] = {"local_stages_ms": round(local, 4), "all_to_all_ms_model": round(a2a, 4),
+        out[f"n{world}"] = {"log_r": plan.log_r, "local_stages_ms": round(local, 4),
+                            "all_to_all_ms_model": round(a2a, 4),
                             "split_ms": round(t_split, 4),
                             "plan": "four-step" if split else "single GPU (the split projects slower)",
                             "ms": round(t, 4), "elems_per_s": (1 << log_n) / (t * 1e-3),
@@ -867,7 +871,8 @@ def main():
                               f"{nn * 32 // 4} B over one xGMI link, projected slower than one GPU"}
     if not args.no_ntt and world > 2:
         from tachyon_amd.ntt import FourStepNtt
-        plan = FourStepNtt(args.ntt_log_n, world, rank)  # its own stream; sharded_ntt orders on it
+        # its own stream (sharded_ntt orders on it); the split with the fewest passes
+        plan = FourStepNtt(args.ntt_log_n, world, rank, log_r=FourStepNtt.split_log_r(args.ntt_log_n, world))
         m = plan.local_size
         x = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
         M.gen_scalars("bn254_fr", SEED + 1, m, x.data_ptr(), start=rank * m)
@@ -891,8 +896,8 @@ def main():
         nn = 1 << args.ntt_log_n
         out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
                       "round_trip_ok": bool(ok.item()), "scaling": "strong",
-                      "mode": f"four-step sharded x{world}: local R/C-point NTTs + one RCCL all-to-all "
-                              f"({nn * 32 // world // world} B per rank pair)"}
+                      "mode": f"four-step sharded x{world}: local R/C-point NTTs (R = 2^{plan.log_r}) + one RCCL "
+                              f"all-to-all ({nn * 32 // world // world} B per rank pair)"}
         plan.close()
 
     if not args.no_ntt and world == 1:

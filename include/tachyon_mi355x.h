@@ -303,6 +303,17 @@ TACHYON_C_EXPORT int tachyon_mi355x_bn254_univariate_evaluation_domain_last_timi
 typedef struct tachyon_mi355x_bn254_ntt4 tachyon_mi355x_bn254_ntt4;
 TACHYON_C_EXPORT tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create(uint32_t log_n, uint32_t log_world,
                                                                             uint32_t rank, void* stream);
+/* The same plan with R = 2^log_r (1 <= log_r < log_n, R and C = n / R >= G):
+ * the layouts above with that R.  _split_log_r returns the split with the
+ * fewest pass launches (passes of <= 8 stages; ties: the larger R up to C),
+ * e.g. 2^24 -> R = 2^8, C = 2^16: one pass for the column NTTs (several
+ * columns per workgroup) and two for the rows, against 2 + 2 for 2^12 x 2^12.
+ * _log_rows returns a plan's log R. */
+TACHYON_C_EXPORT tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create_split(uint32_t log_n, uint32_t log_r,
+                                                                                  uint32_t log_world, uint32_t rank,
+                                                                                  void* stream);
+TACHYON_C_EXPORT uint32_t tachyon_mi355x_bn254_ntt4_log_rows(const tachyon_mi355x_bn254_ntt4* plan);
+TACHYON_C_EXPORT uint32_t tachyon_mi355x_ntt4_split_log_r(uint32_t log_n, uint32_t log_world);
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_destroy(tachyon_mi355x_bn254_ntt4* plan);
 TACHYON_C_EXPORT size_t tachyon_mi355x_bn254_ntt4_local_size(const tachyon_mi355x_bn254_ntt4* plan);
 TACHYON_C_EXPORT void tachyon_mi355x_bn254_ntt4_stage(tachyon_mi355x_bn254_ntt4* plan, int stage, int inverse,
@@ -313,7 +324,8 @@ TACHYON_C_EXPORT void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn2
  * input copy, the passes, a separate twiddle kernel) instead of the exchange's
  * twiddle and packing fused into the sub-transforms' passes; bit 1 = the
  * sub-transforms on the 8 x 32-bit-limb passes instead of their size's
- * default (29-bit up to 2^20).  Returns 0 for other values. */
+ * default (29-bit up to 2^20); bit 2 = one column per workgroup in one-pass
+ * sub-transforms (no packing).  Returns 0 for other values. */
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_ntt4_set_variant(tachyon_mi355x_bn254_ntt4* plan, int variant);
 
 /* ---- communicators and library-level sharded entry points ------------------

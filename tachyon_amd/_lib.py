@@ -107,6 +107,10 @@ SIGNATURES = [
     ("tachyon_mi355x_bn254_ntt4_create", vp, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp]),
     ("tachyon_mi355x_bn254_ntt4_destroy", None, [vp]),
     ("tachyon_mi355x_bn254_ntt4_local_size", sz, [vp]),
+    ("tachyon_mi355x_bn254_ntt4_create_split", vp, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                    vp]),
+    ("tachyon_mi355x_bn254_ntt4_log_rows", ctypes.c_uint32, [vp]),
+    ("tachyon_mi355x_ntt4_split_log_r", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
     ("tachyon_mi355x_bn254_ntt4_stage", None, [vp, i32, i32, vp, vp]),
     ("tachyon_mi355x_bn254_ntt4_synchronize", None, [vp]),
     ("tachyon_mi355x_bn254_ntt4_stream", vp, [vp]),

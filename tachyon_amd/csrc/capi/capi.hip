@@ -953,6 +953,18 @@ tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create(uint32_t log_n, uint
       new ntt::Ntt4Step<Bn254Fr>(log_n, log_world, rank, static_cast<hipStream_t>(stream))};
   GUARD_END
 }
+tachyon_mi355x_bn254_ntt4* tachyon_mi355x_bn254_ntt4_create_split(uint32_t log_n, uint32_t log_r, uint32_t log_world,
+                                                                 uint32_t rank, void* stream) {
+  GUARD_BEGIN
+  if (log_r == 0 || log_r >= log_n) throw std::runtime_error("tachyon_mi355x: ntt4 split needs 1 <= log_r < log_n");
+  return new tachyon_mi355x_bn254_ntt4{
+      new ntt::Ntt4Step<Bn254Fr>(log_n, log_world, rank, static_cast<hipStream_t>(stream), log_r)};
+  GUARD_END
+}
+uint32_t tachyon_mi355x_bn254_ntt4_log_rows(const tachyon_mi355x_bn254_ntt4* plan) { return plan->impl->log_rows(); }
+uint32_t tachyon_mi355x_ntt4_split_log_r(uint32_t log_n, uint32_t log_world) {
+  return ntt::ntt4_split_log_r(log_n, log_world);
+}
 void tachyon_mi355x_bn254_ntt4_destroy(tachyon_mi355x_bn254_ntt4* plan) {
   if (!plan) return;
   delete plan->impl;
@@ -1037,7 +1049,7 @@ int tachyon_mi355x_comm_rank(const tachyon_mi355x_comm* comm) { return comm->imp
 const char* tachyon_mi355x_comm_backend(const tachyon_mi355x_comm* comm) { return comm->impl->backend(); }
 
 int tachyon_mi355x_bn254_ntt4_set_variant(tachyon_mi355x_bn254_ntt4* plan, int variant) {
-  if (variant < 0 || variant > 3) return 0;
+  if (variant < 0 || variant > 7) return 0;
   GUARD_BEGIN plan->impl->set_variant(variant); GUARD_END
   return 1;
 }

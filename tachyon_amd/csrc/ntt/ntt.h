@@ -86,8 +86,10 @@ class NttDomain {
   // (dif29_pass_kernel), 0 = the 8 x 32-bit ones (dif_pass_kernel); the
   // default is 1 up to 2^20 and 0 above (DESIGN.md NTT round 4: fewer
   // instructions win while the clock holds, more multiplies per butterfly
-  // lower it at 2^22+); bit 1 (with bit 0) swizzles their LDS positions.
-  // Unknown values (or any bit on other fields): refused.
+  // lower it at 2^22+); bit 1 (with bit 0) swizzles their LDS positions;
+  // bit 2 (any field) keeps one batch entry per workgroup in one-pass
+  // transforms (no packing, pack_log).  Unknown values (or bits 0-1 on other
+  // fields): refused.
   bool set_variant(int v);
   int variant() const { return variant_; }
 
@@ -100,6 +102,7 @@ class NttDomain {
  private:
   void run(Fr* d_data, bool inverse, size_t batch, const Fr* src = nullptr, const FourStepTw<Fr>* fs = nullptr);
   void run29(Fr* d_data, bool inverse, size_t batch, const Fr* src = nullptr, const FourStepTw<Fr>* fs = nullptr);
+  uint32_t pack_log(size_t batch) const;
   void build_twiddles();
   void build_tables29();
   void ensure_tables32();
@@ -158,8 +161,9 @@ Fr field_from_u64(uint64_t v);
 namespace tachyon_amd::ntt {
 
 // Distributed four-step NTT (Bailey) over G = 2^log_world ranks, one process
-// per GPU: n = R * C with R = 2^floor(L/2), C = n / R, both
-// >= G.  Rank g owns
+// per GPU: n = R * C with R = 2^floor(L/2) (or 2^log_r when
+// given: ntt4_split_log_r picks the split with the fewest passes), C = n / R,
+// both >= G.  Rank g owns
 //   input   the columns c in [g C/G, (g+1) C/G) of the R x C row-major view
 //           of x, stored column by column: in[c_l * R + r] = x[C r + c]
 //   output  the rows k1 in [g R/G, (g+1) R/G) of X, stored row by row:
@@ -173,7 +177,7 @@ namespace tachyon_amd::ntt {
 template <class Fr>
 class Ntt4Step {
  public:
-  Ntt4Step(uint32_t log_n, uint32_t log_world, uint32_t rank, hipStream_t stream);
+  Ntt4Step(uint32_t log_n, uint32_t log_world, uint32_t rank, hipStream_t stream, uint32_t log_r = 0);
   ~Ntt4Step();
   Ntt4Step(const Ntt4Step&) = delete;
   Ntt4Step& operator=(const Ntt4Step&) = delete;
@@ -190,16 +194,17 @@ class Ntt4Step {
   void inverse_stage1(const Fr* in, Fr* send);
   void inverse_stage2(const Fr* recv, Fr* out);
   // A/B: bit 0 = the round-4 stages (copies, separate twiddle kernel), bit 1
-  // = the sub-transforms on the 32-bit passes
+  // = the sub-transforms on the 32-bit passes, bit 2 = no packing of one-pass
+  // sub-transforms (NttDomain variant bit 2)
   void set_variant(int v) {
     fused_ = !(v & 1);
-    const int sub = (v & 2) ? 0 : -1;
-    if (sub == 0) {
-      dom_r_->set_variant(0);
-      dom_c_->set_variant(0);
+    const int nopack = (v & 4) ? 4 : 0;
+    if (v & 2) {
+      dom_r_->set_variant(nopack);
+      dom_c_->set_variant(nopack);
     } else {
-      dom_r_->set_variant(dom_r_->log_size() <= 20 ? 1 : 0);
-      dom_c_->set_variant(dom_c_->log_size() <= 20 ? 1 : 0);
+      dom_r_->set_variant((dom_r_->log_size() <= 20 ? 1 : 0) | nopack);
+      dom_c_->set_variant((dom_c_->log_size() <= 20 ? 1 : 0) | nopack);
     }
   }
 
@@ -217,6 +222,12 @@ class Ntt4Step {
 };
 
 extern template class Ntt4Step<Bn254Fr>;
+
+// The R x C split with the fewest pass launches (ceil(log R / 8) + ceil(log C
+// / 8), passes of <= 8 stages) with R, C >= 2^log_world, ties to the larger R
+// up to C: 2^24 -> 2^8 x 2^16 (1 + 2 passes instead of 2 + 2 for 2^12 x
+// 2^12).  One-pass R-point transforms pack several columns per workgroup.
+uint32_t ntt4_split_log_r(uint32_t log_n, uint32_t log_world);
 
 // One process, several GPUs (round 4): the four-step plan above with one part
 // per entry of `devices` (ids may repeat -- logical devices sharing a GPU on

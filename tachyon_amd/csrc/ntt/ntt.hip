@@ -65,6 +65,9 @@ struct PassArgs {
   // the inverse stage 2's first pass): element k of batch entry b (the local
   // column c_l) times w_N^(+-(c0 + b) k), at its packed send / recv position
   FourStepTw<Fr> fs;
+  // single-pass transforms smaller than a tile: 2^pack batch entries per
+  // workgroup, set m = entry (blockIdx.y << pack) + m (0: one entry per blockIdx.y)
+  uint32_t pack;
 };
 
 // packed position of element k1 of local column c_l (twiddle_exchange_kernel's layout):
@@ -173,9 +176,11 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
   const uint32_t elems = M << k;
   const uint32_t b = blockIdx.x;
   // batch of independent contiguous transforms (the packed four-step
-  // layouts address the whole buffer themselves)
-  if (!(a.mode & kLoadTw4)) in += (size_t)blockIdx.y << L;
-  if (!(a.mode & kStoreTw4)) out += (size_t)blockIdx.y << L;
+  // layouts address the whole buffer themselves); with a.pack the workgroup's
+  // sets are 2^pack whole transforms, entries ybase + m
+  const uint32_t pk = a.pack, ybase = blockIdx.y << pk;
+  if (!(a.mode & kLoadTw4)) in += (size_t)ybase << L;
+  if (!(a.mode & kStoreTw4)) out += (size_t)ybase << L;
 
   // index(mid, m) of element m of the block's set, position mid in the set
   uint32_t hi_shift = L - a.s0;            // set stride in the hi dimension
@@ -198,11 +203,12 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
   for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
     uint32_t mid = e >> log_m, m = e & (M - 1);
     uint32_t i = index(mid, m);
+    const uint32_t ent = pk ? m : 0u;
     Fr v;
     if (a.mode & kLoadTw4) {
-      v = in[fs_packed(a.fs, i, blockIdx.y)] * fs_twiddle(a.fs, i, blockIdx.y);
+      v = in[fs_packed(a.fs, i, ybase + ent)] * fs_twiddle(a.fs, i, ybase + ent);
     } else {
-      v = in[i];
+      v = in[((size_t)ent << L) + i];
       if (a.mode & kLoadCoset) v = v * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
     }
     lds[e] = v;
@@ -242,11 +248,11 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
       uint32_t q = e >> log_m, m = e & (M - 1);
       uint32_t mid = bitrev(q, k);
       Fr v = lds[(mid << log_m) + m];
-      uint32_t o = (q << (L - k)) + r0 + m;
+      const uint32_t o = pk ? q : (q << (L - k)) + r0 + m, ent = pk ? m : 0u;
       if (a.mode & kStoreCoset) v = v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits]);
       else if (a.mode & kStoreScale) v = v * a.scale;
-      if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, blockIdx.y)] = (v * fs_twiddle(a.fs, o, blockIdx.y)).canonical();
-      else out[o] = v.canonical();
+      if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, ybase + ent)] = (v * fs_twiddle(a.fs, o, ybase + ent)).canonical();
+      else out[((size_t)ent << L) + o] = v.canonical();
     }
   }
 }
@@ -370,22 +376,25 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
   };
 
   // ---- load ----
-  const size_t batch_off = (size_t)blockIdx.y << L;
+  // (a.pack: the workgroup's sets are 2^pack whole transforms, entries ybase + m)
+  const uint32_t pk = a.pack, ybase = blockIdx.y << pk;
+  const size_t batch_off = (size_t)ybase << L;
   for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
     const uint32_t mid = e >> log_m, m = e & (M - 1);
     const uint32_t i = index(mid, m);
+    const uint32_t ent = pk ? m : 0u;
     F29 v;
     if constexpr (kFirst) {
       Bn254Fr x;
       if (a.mode & kLoadTw4) {
-        x = static_cast<const Bn254Fr*>(in_v)[fs_packed(a.fs, i, blockIdx.y)] * fs_twiddle(a.fs, i, blockIdx.y);
+        x = static_cast<const Bn254Fr*>(in_v)[fs_packed(a.fs, i, ybase + ent)] * fs_twiddle(a.fs, i, ybase + ent);
       } else {
-        x = static_cast<const Bn254Fr*>(in_v)[batch_off + i];
+        x = static_cast<const Bn254Fr*>(in_v)[batch_off + ((size_t)ent << L) + i];
         if (a.mode & kLoadCoset) x = x * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
       }
       v = fr29::from_words(x.v);
     } else {
-      v = static_cast<const F29*>(in_v)[batch_off + i];
+      v = static_cast<const F29*>(in_v)[batch_off + ((size_t)ent << L) + i];
     }
     lds29_store<kSwz>(lds, e, v);
   }
@@ -419,11 +428,11 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
       const uint32_t mid = bitrev(q, k);
       Bn254Fr v;
       fr29::to_canonical_words(lds29_load<kSwz>(lds, (mid << log_m) + m), v.v);
-      const uint32_t o = (q << (L - k)) + r0 + m;
+      const uint32_t o = pk ? q : (q << (L - k)) + r0 + m, ent = pk ? m : 0u;
       if (a.mode & kStoreCoset) v = (v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits])).canonical();
       else if (a.mode & kStoreScale) v = (v * a.scale).canonical();
-      if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, blockIdx.y)] = (v * fs_twiddle(a.fs, o, blockIdx.y)).canonical();
-      else out[o] = v;
+      if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, ybase + ent)] = (v * fs_twiddle(a.fs, o, ybase + ent)).canonical();
+      else out[((size_t)ent << L) + o] = v;
     }
   }
 }
@@ -751,11 +760,24 @@ void NttDomain<Fr>::ensure_tables32() {
 
 template <class Fr>
 bool NttDomain<Fr>::set_variant(int v) {
-  if (v < 0 || v > 3 || v == 2) return false;  // bit 1 (the LDS swizzle) modifies bit 0
-  if (v != 0 && !std::is_same_v<Fr, Bn254Fr>) return false;
+  if (v < 0 || v > 7 || (v & 3) == 2) return false;  // bit 1 (the LDS swizzle) modifies bit 0
+  if ((v & 3) != 0 && !std::is_same_v<Fr, Bn254Fr>) return false;
   variant_ = v;
   if (v & 1) build_tables29();
   return true;
+}
+
+// A one-pass transform (<= 8 stages) smaller than a tile of kMaxLdsElems: 2^p
+// batch entries per workgroup (the largest p with 2^p | batch and 2^(L + p)
+// elements in the tile) instead of one entry using 2^L / 4 of its 256 threads
+// -- the 2^8-point column NTTs of the four-step's 2^8 x 2^16 split.  Variant
+// bit 2 turns it off (A/B).
+template <class Fr>
+uint32_t NttDomain<Fr>::pack_log(size_t batch) const {
+  if (plan_.size() != 1 || batch < 2 || (variant_ & 4)) return 0;
+  uint32_t p = 0;
+  while (batch % (size_t(2) << p) == 0 && (n_ << (p + 1)) <= kMaxLdsElems) ++p;
+  return p;
 }
 
 template <class Fr>
@@ -838,8 +860,12 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch, const Fr* src_in
     // first pass: data (or src_in) -> scratch; middle: scratch in place; last: scratch -> data
     const Fr* src = (p == 0) ? (src_in ? src_in : d_data) : scratch;
     Fr* dst = ps.final_pass ? d_data : scratch;
-    uint32_t elems = (1u << ps.log_m) << ps.k;
-    uint32_t blocks = (uint32_t)(n_ / elems);
+    // a one-pass transform smaller than a tile: several batch entries per workgroup
+    a.pack = pack_log(batch);
+    if (a.pack) a.log_m = a.pack;
+    uint32_t elems = (1u << a.log_m) << ps.k;
+    uint32_t blocks = a.pack ? 1u : (uint32_t)(n_ / elems);
+    const uint32_t gy = (uint32_t)(batch >> a.pack);
     size_t lds = (size_t)elems * sizeof(Fr);
     // Shoup twiddles (64 B) in the passes whose stage tables are small and
     // cache-resident; Montgomery twiddles (32 B) where the tables stream from
@@ -859,22 +885,22 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch, const Fr* src_in
                                                                          : dif_pass_kernel<Fr, Tw, 3>;
       if (radix_ == 2 && (ntt_variant_ & 2)) kern = dif_pass_kernel<Fr, Tw, 2, false, 5>;
       allow(reinterpret_cast<const void*>(kern));
-      hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, tw, a);
+      hipLaunchKernelGGL(kern, dim3(blocks, gy), dim3(kBlock), lds, stream_, src, dst, tw, a);
     } else {
       auto kern = radix_ == 1 ? dif_pass_kernel<Fr, Fr, 1> : radix_ == 2 ? dif_pass_kernel<Fr, Fr, 2>
                                                                          : dif_pass_kernel<Fr, Fr, 3>;
       if (radix_ == 2 && (ntt_variant_ & 1)) kern = dif_pass_kernel<Fr, Fr, 2, true, 5>;
       allow(reinterpret_cast<const void*>(kern));
-      hipLaunchKernelGGL(kern, dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src, dst, twm, a);
+      hipLaunchKernelGGL(kern, dim3(blocks, gy), dim3(kBlock), lds, stream_, src, dst, twm, a);
     }
 #else
     // release schedule: radix-4 register steps (2 DIF stages per LDS round trip)
     if (lds > 64 * 1024) throw std::runtime_error("tachyon_mi355x: NTT pass tile above 64 KiB in a release build");
     if (shoup)
-      hipLaunchKernelGGL((dif_pass_kernel<Fr, Tw, 2>), dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src,
+      hipLaunchKernelGGL((dif_pass_kernel<Fr, Tw, 2>), dim3(blocks, gy), dim3(kBlock), lds, stream_, src,
                          dst, tw, a);
     else
-      hipLaunchKernelGGL((dif_pass_kernel<Fr, Fr, 2>), dim3(blocks, (uint32_t)batch), dim3(kBlock), lds, stream_, src,
+      hipLaunchKernelGGL((dif_pass_kernel<Fr, Fr, 2>), dim3(blocks, gy), dim3(kBlock), lds, stream_, src,
                          dst, twm, a);
 #endif
     TA_HIP(hipGetLastError());
@@ -931,19 +957,22 @@ void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch, const Fr* src_
       // first pass: data / src_in (32 B) -> scratch (36 B); middle: scratch in place; last: scratch -> data
       const void* src = (p == 0) ? static_cast<const void*>(src_in ? src_in : d_data) : scratch;
       void* dst = ps.final_pass ? static_cast<void*>(d_data) : scratch;
-      const uint32_t elems = (1u << ps.log_m) << ps.k;
-      const uint32_t blocks = (uint32_t)(n_ / elems);
+      a.pack = pack_log(batch);  // a one-pass transform smaller than a tile: several entries per workgroup
+      if (a.pack) a.log_m = a.pack;
+      const uint32_t elems = (1u << a.log_m) << ps.k;
+      const uint32_t blocks = a.pack ? 1u : (uint32_t)(n_ / elems);
+      const uint32_t gy = (uint32_t)(batch >> a.pack);
       // the 29-bit kernel's LDS planes are sized for kMaxLdsElems (tuning plans with larger tiles: 32-bit only)
       if (elems > kMaxLdsElems) throw std::runtime_error("tachyon_mi355x: 29-bit NTT pass tile above its LDS planes");
       const bool swz = (variant_ & 2) != 0;
       if (p == 0) {
         auto* k0 = swz ? &dif29_pass_kernel<true, true, fr29::TwMont29> : &dif29_pass_kernel<true, false, fr29::TwMont29>;
-        hipLaunchKernelGGL(k0, dim3(blocks, (uint32_t)batch), dim3(kBlock), 0, stream_, src, dst,
+        hipLaunchKernelGGL(k0, dim3(blocks, gy), dim3(kBlock), 0, stream_, src, dst,
                            Tw29Table<fr29::TwMont29>{tm, 0u}, a);
       } else {
         auto* k1 = swz ? &dif29_pass_kernel<false, true, fr29::TwShoup29>
                        : &dif29_pass_kernel<false, false, fr29::TwShoup29>;
-        hipLaunchKernelGGL(k1, dim3(blocks, (uint32_t)batch), dim3(kBlock), 0, stream_, src, dst,
+        hipLaunchKernelGGL(k1, dim3(blocks, gy), dim3(kBlock), 0, stream_, src, dst,
                            Tw29Table<fr29::TwShoup29>{ts, (uint32_t)split29_}, a);
       }
       TA_HIP(hipGetLastError());
@@ -992,13 +1021,15 @@ void NttDomain<Fr>::inverse_host(const Fr* in, size_t len, Fr* out) {
 }
 
 template <class Fr>
-Ntt4Step<Fr>::Ntt4Step(uint32_t log_n, uint32_t log_world, uint32_t rank, hipStream_t stream)
+Ntt4Step<Fr>::Ntt4Step(uint32_t log_n, uint32_t log_world, uint32_t rank, hipStream_t stream, uint32_t log_r)
     : log_n_(log_n), log_g_(log_world), rank_(rank), n_(size_t(1) << log_n), stream_(stream) {
   require_gpu();
-  log_r_ = log_n / 2;
+  log_r_ = log_r ? log_r : log_n / 2;
+  if (log_r_ >= log_n) throw std::runtime_error("tachyon_mi355x: four-step NTT needs 1 <= log R < log n");
   log_c_ = log_n - log_r_;
-  if (log_g_ > log_r_ || rank >= (1u << log_g_) || log_n > (uint32_t)Fr::Config::kTwoAdicity || log_n > 30)
-    throw std::runtime_error("tachyon_mi355x: four-step NTT needs R = 2^floor(L/2) >= world size");
+  if (log_g_ > log_r_ || log_g_ > log_c_ || rank >= (1u << log_g_) || log_n > (uint32_t)Fr::Config::kTwoAdicity ||
+      log_n > 30)
+    throw std::runtime_error("tachyon_mi355x: four-step NTT needs R, C >= world size");
   if (!stream_) {
     TA_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     own_stream_ = true;
@@ -1270,6 +1301,21 @@ template Bls381Fr root_of_unity<Bls381Fr>(uint32_t);
 template Bn254Fr field_from_u64<Bn254Fr>(uint64_t);
 template Bls381Fr field_from_u64<Bls381Fr>(uint64_t);
 template class Ntt4Step<Bn254Fr>;
+
+uint32_t ntt4_split_log_r(uint32_t log_n, uint32_t log_world) {
+  auto passes = [](uint32_t k) { return (k + kMaxPassStages - 1) / kMaxPassStages; };
+  uint32_t best = 0, best_cost = ~0u;
+  for (uint32_t r = std::max(1u, log_world); r < log_n; ++r) {
+    const uint32_t c = log_n - r;
+    if (c < log_world || r > c) continue;
+    const uint32_t cost = passes(r) + passes(c);
+    if (cost <= best_cost) {  // ties: the larger R (up to C)
+      best_cost = cost;
+      best = r;
+    }
+  }
+  return best ? best : log_n / 2;
+}
 template class NttMultiDevice<Bn254Fr>;
 
 }  // namespace tachyon_amd::ntt

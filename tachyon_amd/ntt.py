@@ -181,14 +181,15 @@ class Radix2EvaluationDomain:
 
 class FourStepNtt:
     """One rank's plan of the distributed four-step NTT (include/tachyon_mi355x.h,
-    tachyon_mi355x_bn254_ntt4_*).  n = 2^log_n = R*C, R = 2^floor(log_n/2).
+    tachyon_mi355x_bn254_ntt4_*).  n = 2^log_n = R*C, R = 2^floor(log_n/2), or
+    R = 2^log_r when given (split_log_r: the split with the fewest passes).
 
     Layouts (see input_indices / output_indices): rank r holds the columns
     [r C/G, (r+1) C/G) of the R x C view of x, column-major, and produces the
     rows [r R/G, (r+1) R/G) of X, row-major.  The inverse maps back.
     """
 
-    def __init__(self, log_n: int, world: int, rank: int, stream=None):
+    def __init__(self, log_n: int, world: int, rank: int, stream=None, log_r: int = None):
         """stream: a torch.cuda.Stream (or None for a new one).  The plan's
         kernels run on it; callers run the exchange and any tensor work between
         the stages under `with torch.cuda.stream(plan.torch_stream)` so that one
@@ -204,9 +205,14 @@ class FourStepNtt:
             raise ValueError("FourStepNtt needs a non-default torch.cuda.Stream")
         self.torch_stream = stream
         self.log_n, self.world, self.rank = log_n, world, rank
-        self._p = lib().tachyon_mi355x_bn254_ntt4_create(log_n, world.bit_length() - 1, rank, stream.cuda_stream)
+        if log_r:
+            self._p = lib().tachyon_mi355x_bn254_ntt4_create_split(log_n, log_r, world.bit_length() - 1, rank,
+                                                                   stream.cuda_stream)
+        else:
+            self._p = lib().tachyon_mi355x_bn254_ntt4_create(log_n, world.bit_length() - 1, rank, stream.cuda_stream)
         if not self._p:
             raise RuntimeError("four-step NTT plan creation failed")
+        self.log_r = lib().tachyon_mi355x_bn254_ntt4_log_rows(self._p)
         self.local_size = lib().tachyon_mi355x_bn254_ntt4_local_size(self._p)
 
     def close(self):
@@ -240,7 +246,8 @@ class FourStepNtt:
     def set_variant(self, variant: int):
         """A/B (same bytes): bit 0 = the round-4 stages (copy + passes +
         separate twiddle kernel) instead of the fused exchange; bit 1 = the
-        32-bit-limb passes for the sub-transforms."""
+        32-bit-limb passes for the sub-transforms; bit 2 = one column per
+        workgroup in one-pass sub-transforms (no packing)."""
         if not lib().tachyon_mi355x_bn254_ntt4_set_variant(self._p, variant):
             raise ValueError(f"unknown four-step variant {variant}")
 
@@ -248,20 +255,27 @@ class FourStepNtt:
         lib().tachyon_mi355x_bn254_ntt4_synchronize(self._p)
 
     @staticmethod
-    def input_indices(log_n: int, world: int, rank: int):
+    def split_log_r(log_n: int, world: int) -> int:
+        """log R of the split with the fewest pass launches (tachyon_mi355x_ntt4_split_log_r)."""
+        return lib().tachyon_mi355x_ntt4_split_log_r(log_n, world.bit_length() - 1)
+
+    @staticmethod
+    def input_indices(log_n: int, world: int, rank: int, log_r: int = None):
         """Global index of each local input element: in[c_l*R + r] = x[C*r + c]."""
         import numpy as np
-        R, C = 1 << (log_n // 2), 1 << (log_n - log_n // 2)
+        lr = log_r or log_n // 2
+        R, C = 1 << lr, 1 << (log_n - lr)
         cg = C // world
         c = rank * cg + np.arange(cg)[:, None]
         r = np.arange(R)[None, :]
         return (C * r + c).reshape(-1)
 
     @staticmethod
-    def output_indices(log_n: int, world: int, rank: int):
+    def output_indices(log_n: int, world: int, rank: int, log_r: int = None):
         """Global index of each local output element: out[k1_l*C + k2] = X[k1 + R*k2]."""
         import numpy as np
-        R, C = 1 << (log_n // 2), 1 << (log_n - log_n // 2)
+        lr = log_r or log_n // 2
+        R, C = 1 << lr, 1 << (log_n - lr)
         rg = R // world
         k1 = rank * rg + np.arange(rg)[:, None]
         k2 = np.arange(C)[None, :]

@@ -103,6 +103,32 @@ def test_four_step_simulated_ranks(log_n, world, variant):
     Every plan variant (the exchange's twiddle + packing fused into the
     sub-transforms' passes or the round-4 separate kernels; 29- or 32-bit
     passes) gives the same bytes."""
+    _four_step_round_trip(log_n, world, variant)
+
+
+@pytest.mark.parametrize("variant", [0, 2, 4, 6])
+@pytest.mark.parametrize("log_n,world,log_r", [(20, 8, 8), (16, 4, 8), (12, 2, 4), (10, 8, 3), (19, 2, 8),
+                                               (13, 8, 5), (11, 1, 2), (18, 4, 10)])
+def test_four_step_split(log_n, world, log_r, variant):
+    """Plans with R = 2^log_r != 2^floor(L/2) (tachyon_mi355x_bn254_ntt4_create_split;
+    2^8 x 2^16 is split_log_r's choice for 2^24): the one-pass column NTTs
+    pack 2^p columns per workgroup (variant bit 2 turns that off, same bytes),
+    every variant equal to the oracle's FFT slab and its own inverse."""
+    from tachyon_amd.ntt import FourStepNtt
+    if log_r == 8 and log_n >= 16:
+        assert FourStepNtt.split_log_r(log_n, world) in (8, log_n // 2)
+    _four_step_round_trip(log_n, world, variant, log_r)
+
+
+def test_four_step_split_choice():
+    """split_log_r: the fewest pass launches (passes of <= 8 stages), ties to the larger R up to C."""
+    from tachyon_amd.ntt import FourStepNtt
+    assert FourStepNtt.split_log_r(24, 8) == 8 and FourStepNtt.split_log_r(22, 4) == 8
+    assert FourStepNtt.split_log_r(20, 2) == 8 and FourStepNtt.split_log_r(16, 1) == 8
+    assert FourStepNtt.split_log_r(12, 8) == 6 and FourStepNtt.split_log_r(26, 8) == 13
+
+
+def _four_step_round_trip(log_n, world, variant, log_r=None):
     import torch
     from tachyon_amd.ntt import FourStepNtt
     n = 1 << log_n
@@ -112,7 +138,7 @@ def test_four_step_simulated_ranks(log_n, world, variant):
     X = X.reshape(n, 4)
     stream = torch.cuda.Stream()  # the plans and every tensor op below share it
     torch.cuda.set_stream(stream)
-    plans = [FourStepNtt(log_n, world, r, stream) for r in range(world)]
+    plans = [FourStepNtt(log_n, world, r, stream, log_r=log_r) for r in range(world)]
     for p in plans:
         p.set_variant(variant)
     m = n // world
@@ -132,24 +158,28 @@ def test_four_step_simulated_ranks(log_n, world, variant):
         torch.cuda.synchronize()
         return outs
 
-    ins = [torch.from_numpy(np.ascontiguousarray(x[FourStepNtt.input_indices(log_n, world, r)]).view(np.uint8)
-                            .reshape(-1)).cuda() for r in range(world)]
+    ins = [torch.from_numpy(np.ascontiguousarray(x[FourStepNtt.input_indices(log_n, world, r, log_r)])
+                            .view(np.uint8).reshape(-1)).cuda() for r in range(world)]
     outs = run(ins, False)
     for r in range(world):
-        assert outs[r].cpu().numpy().tobytes() == X[FourStepNtt.output_indices(log_n, world, r)].tobytes(), r
+        assert outs[r].cpu().numpy().tobytes() == X[FourStepNtt.output_indices(log_n, world, r, log_r)].tobytes(), r
     back = run(outs, True)
     for r in range(world):
         assert torch.equal(back[r], ins[r]), r
     torch.cuda.set_stream(torch.cuda.default_stream())
 
 
-def test_batched_transform_device():
-    """transform_batch_device == per-array transforms (the four-step's building block)."""
+@pytest.mark.parametrize("logn,batch,variant", [(10, 7, 1), (6, 12, 1), (6, 12, 0), (8, 64, 1), (8, 64, 5),
+                                               (3, 40, 1), (5, 7, 0), (1, 6, 1)])
+def test_batched_transform_device(logn, batch, variant):
+    """transform_batch_device == per-array transforms (the four-step's building
+    block), including one-pass sizes with several arrays per workgroup (batch
+    divisible by 2^p; odd batches unpacked; variant bit 2: packing off)."""
     import torch
-    logn, batch = 10, 7
     n = 1 << logn
     v = O.gen_scalars("bn254_fr", 555, n * batch).reshape(batch, n * 4)
     d = domain(n)
+    d.set_variant(variant)
     t = torch.from_numpy(v.view(np.uint8).reshape(-1).copy()).cuda()
     d.transform_batch_device(t.data_ptr(), batch)
     torch.cuda.synchronize()  # device-wide: covers the domain's own stream

@@ -2,9 +2,11 @@
 """A/B of the four-step NTT's local stages (rank 0 of an N-rank plan, the
 stages bench.py's project_ntt_scaling times) over the plan variants:
 bit 0 = the round-4 stages (input copy + passes + separate twiddle kernel),
-bit 1 = 32-bit-limb sub-transform passes.  Rounds alternate the variants.
+bit 1 = 32-bit-limb sub-transform passes, bit 2 = no packing of one-pass
+sub-transforms; --splits: log R of the plan (0 = floor(L/2), -1 =
+split_log_r's choice).  Rounds alternate the variants.
 
-  python tools/ntt4_probe.py --log-n 24 --worlds 2 4 8 --variants 0 1 2 3 --rounds 3
+  python tools/ntt4_probe.py --log-n 24 --worlds 2 4 8 --variants 0 1 2 3 --rounds 3 --splits 0 -1
 """
 import argparse
 import json
@@ -22,12 +24,14 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 1, 2, 3])
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--splits", type=int, nargs="+", default=[0])
     args = ap.parse_args()
     import torch
     from tachyon_amd import msm as M
     from tachyon_amd.ntt import FourStepNtt
-    for world in args.worlds:
-        plan = FourStepNtt(args.log_n, world, 0)
+    for world, split in [(w, sp) for w in args.worlds for sp in args.splits]:
+        log_r = FourStepNtt.split_log_r(args.log_n, world) if split < 0 else split or None
+        plan = FourStepNtt(args.log_n, world, 0, log_r=log_r)
         m = plan.local_size
         x = torch.empty(m * 32, dtype=torch.uint8, device="cuda")
         y = torch.empty_like(x)
@@ -60,8 +64,8 @@ def main():
                     plan.run_stage(2, False, y, x0)
                 s.synchronize()
                 ms = (time.perf_counter() - t0) / args.reps * 1e3
-                print(json.dumps({"log_n": args.log_n, "world": world, "variant": v, "round": rnd,
-                                  "local_stages_ms": round(ms, 4)}), flush=True)
+                print(json.dumps({"log_n": args.log_n, "world": world, "log_r": plan.log_r, "variant": v,
+                                  "round": rnd, "local_stages_ms": round(ms, 4)}), flush=True)
         plan.close()
 
 
