@@ -237,7 +237,7 @@ uint32_t ntt4_split_log_r(uint32_t log_n, uint32_t log_world);
 // that part g's input columns are one contiguous chunk, and the parts' output
 // rows come back as one R x C matrix transposed to natural order.  Everything
 // is enqueued on the primary stream and the parts' streams (events between
-// them).  G = |devices| is a power of two with R = 2^floor(log_n / 2) >= G.
+// them).  G = |devices| is a power of two, R x C = ntt4_split_log_r's split, R, C >= G.
 template <class Fr>
 class NttMultiDevice {
  public:

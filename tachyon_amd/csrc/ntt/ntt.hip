@@ -1136,9 +1136,10 @@ NttMultiDevice<Fr>::NttMultiDevice(uint32_t log_n, const std::vector<int>& devic
   const size_t G = devices.size();
   if (G < 2 || (G & (G - 1))) throw std::runtime_error("tachyon_mi355x: multi-device NTT needs 2^k >= 2 devices");
   log_g_ = (uint32_t)__builtin_ctzll(G);
-  log_r_ = log_n / 2;
+  log_r_ = ntt4_split_log_r(log_n, log_g_);  // the fewest pass launches (2^24: 2^8 x 2^16)
   log_c_ = log_n - log_r_;
-  if (log_g_ > log_r_) throw std::runtime_error("tachyon_mi355x: multi-device NTT needs R = 2^floor(L/2) >= devices");
+  if (log_g_ > log_r_ || log_g_ > log_c_)
+    throw std::runtime_error("tachyon_mi355x: multi-device NTT needs R, C >= devices");
   int count = 0, prev = 0;
   TA_HIP(hipGetDeviceCount(&count));
   for (int d : devices)
@@ -1163,7 +1164,7 @@ NttMultiDevice<Fr>::NttMultiDevice(uint32_t log_n, const std::vector<int>& devic
     TA_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     TA_HIP(hipEventCreateWithFlags(&p->ev1, hipEventDisableTiming));
     TA_HIP(hipEventCreateWithFlags(&p->ev2, hipEventDisableTiming));
-    p->plan = std::make_unique<Ntt4Step<Fr>>(log_n, log_g_, (uint32_t)g, p->stream);
+    p->plan = std::make_unique<Ntt4Step<Fr>>(log_n, log_g_, (uint32_t)g, p->stream, log_r_);
     const size_t m = n_ >> log_g_;
     p->in.ensure(m * sizeof(Fr));
     p->send.ensure(m * sizeof(Fr));
