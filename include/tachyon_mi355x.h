@@ -325,7 +325,9 @@ TACHYON_C_EXPORT void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn2
  * twiddle and packing fused into the sub-transforms' passes; bit 1 = the
  * sub-transforms on the 8 x 32-bit-limb passes instead of their size's
  * default (29-bit up to 2^20); bit 2 = one column per workgroup in one-pass
- * sub-transforms (no packing).  Returns 0 for other values. */
+ * sub-transforms (no packing); bit 3 = the exchange twiddles computed in the
+ * pass instead of read from the plan's precomputed table.  Returns 0 for other
+ * values. */
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_ntt4_set_variant(tachyon_mi355x_bn254_ntt4* plan, int variant);
 
 /* ---- communicators and library-level sharded entry points ------------------

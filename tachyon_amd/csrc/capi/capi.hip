@@ -1049,7 +1049,7 @@ int tachyon_mi355x_comm_rank(const tachyon_mi355x_comm* comm) { return comm->imp
 const char* tachyon_mi355x_comm_backend(const tachyon_mi355x_comm* comm) { return comm->impl->backend(); }
 
 int tachyon_mi355x_bn254_ntt4_set_variant(tachyon_mi355x_bn254_ntt4* plan, int variant) {
-  if (variant < 0 || variant > 7) return 0;
+  if (variant < 0 || variant > 15) return 0;
   GUARD_BEGIN plan->impl->set_variant(variant); GUARD_END
   return 1;
 }

@@ -42,6 +42,15 @@ struct FourStepTw {
   const Fr* lo = nullptr;
   const Fr* hi = nullptr;
   uint32_t bits = 0, log_n = 0, log_rg = 0, log_cg = 0, c0 = 0;
+  // BN254 Fr 29-bit passes: the rank's twiddles w_N^(+-(c0 + c_l) k1)
+  // precomputed in R'-form (fr29::TwMont29, entry c_l << log_r | k1): one
+  // 36-byte read and one product per element instead of two table reads and
+  // two Montgomery products (nullptr: computed in the pass)
+  const void* tab29 = nullptr;
+  uint32_t log_r = 0;
+  // 1: the row NTTs of the exchange (forward stage 2 reads, inverse stage 1
+  // writes the exchange layout directly: no transpose); 0: the column NTTs
+  uint32_t rows = 0;
 };
 
 template <class Fr>
@@ -195,9 +204,11 @@ class Ntt4Step {
   void inverse_stage2(const Fr* recv, Fr* out);
   // A/B: bit 0 = the round-4 stages (copies, separate twiddle kernel), bit 1
   // = the sub-transforms on the 32-bit passes, bit 2 = no packing of one-pass
-  // sub-transforms (NttDomain variant bit 2)
+  // sub-transforms (NttDomain variant bit 2), bit 3 = the exchange twiddles
+  // computed in the pass (no tab29)
   void set_variant(int v) {
     fused_ = !(v & 1);
+    no_table_ = (v & 8) != 0;
     const int nopack = (v & 4) ? 4 : 0;
     if (v & 2) {
       dom_r_->set_variant(nopack);
@@ -210,6 +221,7 @@ class Ntt4Step {
 
  private:
   bool fused_ = true;
+  bool no_table_ = false;
   uint32_t log_n_, log_g_, rank_, log_r_, log_c_;
   size_t n_;
   hipStream_t stream_ = nullptr;
@@ -219,6 +231,8 @@ class Ntt4Step {
   uint32_t pow_bits_ = 0;
   Fr w_;
   DeviceBuffer work_, w_lo_, w_hi_, wi_lo_, wi_hi_;
+  DeviceBuffer tab29_fwd_, tab29_inv_;  // FourStepTw::tab29 of the two directions (built on first use)
+  const void* exchange_table(bool inverse);
 };
 
 extern template class Ntt4Step<Bn254Fr>;

@@ -24,7 +24,15 @@ constexpr uint32_t kMaxPassStages = 8;
 // 1024/r2 1.95, 1024/r3 2.82 (half the threads idle), 512/r2 2.54 ms.
 constexpr uint32_t kMaxLdsElems = 1024;
 
-enum : uint32_t { kLoadCoset = 1, kStoreScale = 2, kStoreCoset = 4, kLoadTw4 = 8, kStoreTw4 = 16 };
+enum : uint32_t {
+  kLoadCoset = 1,
+  kStoreScale = 2,
+  kStoreCoset = 4,
+  kLoadTw4 = 8,
+  kStoreTw4 = 16,
+  kLoadXch = 32,
+  kStoreXch = 64
+};
 
 // Twiddle tables.  BN254 Fr butterflies multiply by a Shoup product
 // (Fp::mul_shoup, mont_asm.h shoup_mul_8): an entry is the plain twiddle and
@@ -70,11 +78,20 @@ struct PassArgs {
   uint32_t pack;
 };
 
-// packed position of element k1 of local column c_l (twiddle_exchange_kernel's layout):
-// ((h Cg + c_l) Rg + k1_l), h = k1 >> log_rg
+// The exchange layout of the fused stages: chunk h (n/G^2 elements, to / from
+// rank h) holds [k1_l][c_l], row-major -- so the row NTTs read (forward
+// stage 2) and write (inverse stage 1) Cg-element runs and need no transpose.
+// Column side: element k1 of local column c_l at (h Rg + k1_l) Cg + c_l =
+// k1 Cg + c_l (h = k1 >> log_rg).  (The unfused round-4 stages keep
+// twiddle_exchange_kernel's [c_l][k1_l] chunks and the transposes.)
 template <class Fr>
 __device__ __forceinline__ size_t fs_packed(const FourStepTw<Fr>& f, uint32_t k1, uint32_t c_l) {
-  return ((((size_t)(k1 >> f.log_rg) << f.log_cg) + c_l) << f.log_rg) + (k1 & ((1u << f.log_rg) - 1));
+  return ((size_t)k1 << f.log_cg) + c_l;
+}
+// Row side: element c (column, c = g Cg + c_l) of local row j at (g Rg + j) Cg + c_l
+template <class Fr>
+__device__ __forceinline__ size_t xch_pos(const FourStepTw<Fr>& f, uint32_t c, uint32_t j) {
+  return ((((size_t)(c >> f.log_cg) << f.log_rg) + j) << f.log_cg) + (c & ((1u << f.log_cg) - 1));
 }
 // w_N^((c0 + c_l) k1) from the two-level power tables of the four-step's root
 template <class Fr>
@@ -179,8 +196,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
   // layouts address the whole buffer themselves); with a.pack the workgroup's
   // sets are 2^pack whole transforms, entries ybase + m
   const uint32_t pk = a.pack, ybase = blockIdx.y << pk;
-  if (!(a.mode & kLoadTw4)) in += (size_t)ybase << L;
-  if (!(a.mode & kStoreTw4)) out += (size_t)ybase << L;
+  if (!(a.mode & (kLoadTw4 | kLoadXch))) in += (size_t)ybase << L;
+  if (!(a.mode & (kStoreTw4 | kStoreXch))) out += (size_t)ybase << L;
 
   // index(mid, m) of element m of the block's set, position mid in the set
   uint32_t hi_shift = L - a.s0;            // set stride in the hi dimension
@@ -207,6 +224,8 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
     Fr v;
     if (a.mode & kLoadTw4) {
       v = in[fs_packed(a.fs, i, ybase + ent)] * fs_twiddle(a.fs, i, ybase + ent);
+    } else if (a.mode & kLoadXch) {
+      v = in[xch_pos(a.fs, i, ybase + ent)];
     } else {
       v = in[((size_t)ent << L) + i];
       if (a.mode & kLoadCoset) v = v * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
@@ -252,6 +271,7 @@ __global__ __launch_bounds__(kBlock, kWaves) void dif_pass_kernel(const Fr* __re
       if (a.mode & kStoreCoset) v = v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits]);
       else if (a.mode & kStoreScale) v = v * a.scale;
       if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, ybase + ent)] = (v * fs_twiddle(a.fs, o, ybase + ent)).canonical();
+      else if (a.mode & kStoreXch) out[xch_pos(a.fs, o, ybase + ent)] = v.canonical();
       else out[((size_t)ent << L) + o] = v.canonical();
     }
   }
@@ -386,8 +406,17 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
     F29 v;
     if constexpr (kFirst) {
       Bn254Fr x;
+      if ((a.mode & kLoadTw4) && a.fs.tab29) {  // the precomputed R'-form twiddle: one product
+        const Bn254Fr raw = static_cast<const Bn254Fr*>(in_v)[fs_packed(a.fs, i, ybase + ent)];
+        const auto* t29 = static_cast<const fr29::TwMont29*>(a.fs.tab29);
+        v = fr29::tw_prod(fr29::from_words(raw.v), t29[((size_t)(ybase + ent) << a.fs.log_r) + i]);
+        lds29_store<kSwz>(lds, e, v);
+        continue;
+      }
       if (a.mode & kLoadTw4) {
         x = static_cast<const Bn254Fr*>(in_v)[fs_packed(a.fs, i, ybase + ent)] * fs_twiddle(a.fs, i, ybase + ent);
+      } else if (a.mode & kLoadXch) {
+        x = static_cast<const Bn254Fr*>(in_v)[xch_pos(a.fs, i, ybase + ent)];
       } else {
         x = static_cast<const Bn254Fr*>(in_v)[batch_off + ((size_t)ent << L) + i];
         if (a.mode & kLoadCoset) x = x * (a.load_lo[i & ((1u << a.pow_bits) - 1)] * a.load_hi[i >> a.pow_bits]);
@@ -422,16 +451,25 @@ __global__ __launch_bounds__(kBlock) void dif29_pass_kernel(const void* __restri
       out[index(mid, m)] = lds29_load<kSwz>(lds, e);
     }
   } else {
-    Bn254Fr* out = static_cast<Bn254Fr*>(out_v) + ((a.mode & kStoreTw4) ? 0 : batch_off);
+    Bn254Fr* out = static_cast<Bn254Fr*>(out_v) + ((a.mode & (kStoreTw4 | kStoreXch)) ? 0 : batch_off);
     for (uint32_t e = threadIdx.x; e < elems; e += kBlock) {
       const uint32_t q = e >> log_m, m = e & (M - 1);
       const uint32_t mid = bitrev(q, k);
       Bn254Fr v;
-      fr29::to_canonical_words(lds29_load<kSwz>(lds, (mid << log_m) + m), v.v);
       const uint32_t o = pk ? q : (q << (L - k)) + r0 + m, ent = pk ? m : 0u;
+      if ((a.mode & kStoreTw4) && a.fs.tab29) {  // the precomputed R'-form twiddle: one product
+        const auto* t29 = static_cast<const fr29::TwMont29*>(a.fs.tab29);
+        const F29 y = fr29::tw_prod(lds29_load<kSwz>(lds, (mid << log_m) + m),
+                                    t29[((size_t)(ybase + ent) << a.fs.log_r) + o]);
+        fr29::to_canonical_words(y, v.v);
+        out[fs_packed(a.fs, o, ybase + ent)] = v;
+        continue;
+      }
+      fr29::to_canonical_words(lds29_load<kSwz>(lds, (mid << log_m) + m), v.v);
       if (a.mode & kStoreCoset) v = (v * (a.store_lo[o & ((1u << a.pow_bits) - 1)] * a.store_hi[o >> a.pow_bits])).canonical();
       else if (a.mode & kStoreScale) v = (v * a.scale).canonical();
       if (a.mode & kStoreTw4) out[fs_packed(a.fs, o, ybase + ent)] = (v * fs_twiddle(a.fs, o, ybase + ent)).canonical();
+      else if (a.mode & kStoreXch) out[xch_pos(a.fs, o, ybase + ent)] = v;
       else out[((size_t)ent << L) + o] = v;
     }
   }
@@ -554,6 +592,20 @@ std::vector<Fr> host_powers(const Fr& base, const Fr& scale, size_t count) {
     p = p * base;
   }
   return out;
+}
+
+// FourStepTw::tab29: entry (c_l << log_r) + k1 = w_N^((c0 + c_l) k1) of this
+// rank (the direction's power tables in f) in R'-form (32 W mod p, W the
+// canonical Montgomery value: five doublings, as tw29_table_kernel)
+__global__ __launch_bounds__(kBlock) void fs_table29_kernel(FourStepTw<Bn254Fr> f, uint32_t log_r, size_t count,
+                                                            fr29::TwMont29* __restrict__ out) {
+  const size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= count) return;
+  const uint32_t c_l = (uint32_t)(j >> log_r), k1 = (uint32_t)(j & ((size_t(1) << log_r) - 1));
+  Bn254Fr x = fs_twiddle(f, k1, c_l).canonical();
+#pragma unroll
+  for (int i = 0; i < 5; ++i) x = (x + x).canonical();
+  out[j].w = fr29::from_words(x.v);
 }
 
 // out[c][r] = in[r][c] for a rows x cols row-major matrix, through 32 x 32 LDS tiles
@@ -854,8 +906,13 @@ void NttDomain<Fr>::run(Fr* d_data, bool inverse, size_t batch, const Fr* src_in
     }
     if (fs) {
       a.fs = *fs;
-      if (p == 0 && inverse) a.mode |= kLoadTw4;
-      if (ps.final_pass && !inverse) a.mode |= kStoreTw4;
+      if (fs->rows) {
+        if (p == 0 && !inverse) a.mode |= kLoadXch;
+        if (ps.final_pass && inverse) a.mode |= kStoreXch;
+      } else {
+        if (p == 0 && inverse) a.mode |= kLoadTw4;
+        if (ps.final_pass && !inverse) a.mode |= kStoreTw4;
+      }
     }
     // first pass: data (or src_in) -> scratch; middle: scratch in place; last: scratch -> data
     const Fr* src = (p == 0) ? (src_in ? src_in : d_data) : scratch;
@@ -951,8 +1008,13 @@ void NttDomain<Fr>::run29(Fr* d_data, bool inverse, size_t batch, const Fr* src_
       }
       if (fs) {
         a.fs = *fs;
-        if (p == 0 && inverse) a.mode |= kLoadTw4;
-        if (ps.final_pass && !inverse) a.mode |= kStoreTw4;
+        if (fs->rows) {
+          if (p == 0 && !inverse) a.mode |= kLoadXch;
+          if (ps.final_pass && inverse) a.mode |= kStoreXch;
+        } else {
+          if (p == 0 && inverse) a.mode |= kLoadTw4;
+          if (ps.final_pass && !inverse) a.mode |= kStoreTw4;
+        }
       }
       // first pass: data / src_in (32 B) -> scratch (36 B); middle: scratch in place; last: scratch -> data
       const void* src = (p == 0) ? static_cast<const void*>(src_in ? src_in : d_data) : scratch;
@@ -1070,12 +1132,39 @@ Ntt4Step<Fr>::~Ntt4Step() {
 // send layout (no separate twiddle kernel): two HBM round trips for R <= 2^16.
 // (Before round 5: a copy, the passes, and twiddle_exchange_kernel -- kept as
 // the unfused path, fused_ = false, for A/B.)
+// The exchange twiddles of one direction as FourStepTw::tab29, built on first
+// use when the column NTTs run on the 29-bit passes (nullptr otherwise: the
+// 32-bit passes compute them)
+template <class Fr>
+const void* Ntt4Step<Fr>::exchange_table(bool inverse) {
+  if constexpr (!std::is_same_v<Fr, Bn254Fr>) {
+    (void)inverse;
+    return nullptr;
+  } else {
+    if (!(dom_r_->variant() & 1) || no_table_) return nullptr;
+    DeviceBuffer& t = inverse ? tab29_inv_ : tab29_fwd_;
+    if (!t.capacity()) {
+      const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
+      const FourStepTw<Fr> f{inverse ? wi_lo_.as<Fr>() : w_lo_.as<Fr>(), inverse ? wi_hi_.as<Fr>() : w_hi_.as<Fr>(),
+                             pow_bits_, log_n_, log_rg, log_cg, rank_ << log_cg};
+      const size_t count = local_size();
+      auto* out = static_cast<fr29::TwMont29*>(t.ensure(count * sizeof(fr29::TwMont29)));
+      hipLaunchKernelGGL(fs_table29_kernel, dim3(ceil_div(count, kBlock)), dim3(kBlock), 0, stream_, f, log_r_, count,
+                         out);
+      TA_HIP(hipGetLastError());
+    }
+    return t.as<void>();
+  }
+}
+
 template <class Fr>
 void Ntt4Step<Fr>::forward_stage1(const Fr* in, Fr* send) {
   const size_t m = local_size();
   const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
   if (fused_) {
-    const FourStepTw<Fr> fs{w_lo_.as<Fr>(), w_hi_.as<Fr>(), pow_bits_, log_n_, log_rg, log_cg, rank_ << log_cg};
+    FourStepTw<Fr> fs{w_lo_.as<Fr>(), w_hi_.as<Fr>(), pow_bits_, log_n_, log_rg, log_cg, rank_ << log_cg};
+    fs.tab29 = exchange_table(false);
+    fs.log_r = log_r_;
     dom_r_->transform_device(in, send, false, size_t(1) << log_cg, &fs);
     return;
   }
@@ -1089,8 +1178,27 @@ void Ntt4Step<Fr>::forward_stage1(const Fr* in, Fr* send) {
 
 template <class Fr>
 void Ntt4Step<Fr>::forward_stage2(const Fr* recv, Fr* out) {
-  // recv = [c][k1_l] (C x Rg) -> out = [k1_l][c], then C-point NTTs on the rows
-  const uint32_t rows = 1u << log_c_, cols = 1u << (log_r_ - log_g_);
+  const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
+  if (fused_) {
+    // recv = G chunks [k1_l][c_l] (fs_packed): the C-point NTTs' first pass
+    // reads each local row k1_l as G runs of Cg elements (kLoadXch) -- no
+    // transpose.  A one-pass C NTT in place would read what other workgroups
+    // write: recv goes through the work buffer then.
+    FourStepTw<Fr> fs{};
+    fs.log_rg = log_rg;
+    fs.log_cg = log_cg;
+    fs.rows = 1;
+    const Fr* src = recv;
+    if (recv == out && dom_c_->plan().size() == 1) {
+      Fr* work = static_cast<Fr*>(work_.ensure(local_size() * sizeof(Fr)));
+      TA_HIP(hipMemcpyAsync(work, recv, local_size() * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+      src = work;
+    }
+    dom_c_->transform_device(src, out, false, size_t(1) << log_rg, &fs);
+    return;
+  }
+  // round 4: recv = [c][k1_l] (C x Rg) -> out = [k1_l][c], then C-point NTTs on the rows
+  const uint32_t rows = 1u << log_c_, cols = 1u << log_rg;
   hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(cols, 32), ceil_div(rows, 32)), dim3(kBlock), 0, stream_,
                      recv, out, rows, cols);
   TA_HIP(hipGetLastError());
@@ -1099,16 +1207,30 @@ void Ntt4Step<Fr>::forward_stage2(const Fr* recv, Fr* out) {
 
 template <class Fr>
 void Ntt4Step<Fr>::inverse_stage1(const Fr* in, Fr* send) {
-  // in = [k1_l][k2] (Rg x C): inverse C-point NTTs, then transpose to [c][k1_l] = G chunks [c_l][k1_l]
+  // in = [k1_l][k2] (Rg x C): inverse C-point NTTs on the rows
   const size_t m = local_size();
-  Fr* work = static_cast<Fr*>(work_.ensure(m * sizeof(Fr)));
-  const uint32_t rows = 1u << (log_r_ - log_g_), cols = 1u << log_c_;
+  const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
+  const uint32_t rows = 1u << log_rg, cols = 1u << log_c_;
   if (fused_) {
-    dom_c_->transform_device(in, work, true, rows, nullptr);  // out of place: no copy
-  } else {
-    TA_HIP(hipMemcpyAsync(work, in, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
-    dom_c_->inverse_device(work, rows);
+    // the last pass writes the exchange layout, G chunks [k1_l][c_l]
+    // (kStoreXch) -- no transpose; in place (in == send) through the work buffer
+    FourStepTw<Fr> fs{};
+    fs.log_rg = log_rg;
+    fs.log_cg = log_cg;
+    fs.rows = 1;
+    if (in == send) {
+      Fr* work = static_cast<Fr*>(work_.ensure(m * sizeof(Fr)));
+      dom_c_->transform_device(in, work, true, rows, &fs);
+      TA_HIP(hipMemcpyAsync(send, work, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+    } else {
+      dom_c_->transform_device(in, send, true, rows, &fs);
+    }
+    return;
   }
+  // round 4: a copy, the inverse passes, then the transpose to [c][k1_l] = G chunks [c_l][k1_l]
+  Fr* work = static_cast<Fr*>(work_.ensure(m * sizeof(Fr)));
+  TA_HIP(hipMemcpyAsync(work, in, m * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
+  dom_c_->inverse_device(work, rows);
   hipLaunchKernelGGL(transpose_kernel<Fr>, dim3(ceil_div(cols, 32), ceil_div(rows, 32)), dim3(kBlock), 0, stream_,
                      work, send, rows, cols);
   TA_HIP(hipGetLastError());
@@ -1119,7 +1241,9 @@ void Ntt4Step<Fr>::inverse_stage2(const Fr* recv, Fr* out) {
   const size_t m = local_size();
   const uint32_t log_cg = log_c_ - log_g_, log_rg = log_r_ - log_g_;
   if (fused_) {  // the unpack and w_n^-(c k1) in the first pass's load
-    const FourStepTw<Fr> fs{wi_lo_.as<Fr>(), wi_hi_.as<Fr>(), pow_bits_, log_n_, log_rg, log_cg, rank_ << log_cg};
+    FourStepTw<Fr> fs{wi_lo_.as<Fr>(), wi_hi_.as<Fr>(), pow_bits_, log_n_, log_rg, log_cg, rank_ << log_cg};
+    fs.tab29 = exchange_table(true);
+    fs.log_r = log_r_;
     dom_r_->transform_device(recv, out, true, size_t(1) << log_cg, &fs);
     return;
   }

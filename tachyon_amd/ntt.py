@@ -247,7 +247,8 @@ class FourStepNtt:
         """A/B (same bytes): bit 0 = the round-4 stages (copy + passes +
         separate twiddle kernel) instead of the fused exchange; bit 1 = the
         32-bit-limb passes for the sub-transforms; bit 2 = one column per
-        workgroup in one-pass sub-transforms (no packing)."""
+        workgroup in one-pass sub-transforms (no packing); bit 3 = the
+        exchange twiddles computed in the pass (no precomputed table)."""
         if not lib().tachyon_mi355x_bn254_ntt4_set_variant(self._p, variant):
             raise ValueError(f"unknown four-step variant {variant}")
 

@@ -106,14 +106,16 @@ def test_four_step_simulated_ranks(log_n, world, variant):
     _four_step_round_trip(log_n, world, variant)
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4, 6])
+@pytest.mark.parametrize("variant", [0, 2, 4, 6, 8, 12])
 @pytest.mark.parametrize("log_n,world,log_r", [(20, 8, 8), (16, 4, 8), (12, 2, 4), (10, 8, 3), (19, 2, 8),
                                                (13, 8, 5), (11, 1, 2), (18, 4, 10)])
 def test_four_step_split(log_n, world, log_r, variant):
     """Plans with R = 2^log_r != 2^floor(L/2) (tachyon_mi355x_bn254_ntt4_create_split;
     2^8 x 2^16 is split_log_r's choice for 2^24): the one-pass column NTTs
-    pack 2^p columns per workgroup (variant bit 2 turns that off, same bytes),
-    every variant equal to the oracle's FFT slab and its own inverse."""
+    pack 2^p columns per workgroup (variant bit 2 turns that off, same bytes;
+    bit 3: the exchange twiddles computed in the pass instead of the plan's
+    precomputed 29-bit table), every variant equal to the oracle's FFT slab
+    and its own inverse."""
     from tachyon_amd.ntt import FourStepNtt
     if log_r == 8 and log_n >= 16:
         assert FourStepNtt.split_log_r(log_n, world) in (8, log_n // 2)
