@@ -115,18 +115,33 @@ def test_four_step_2_25(world):
     """The distributed four-step plan at 2^25 (R = 2^12, C = 2^13) with
     `world` simulated ranks on one GPU: each rank's slab equals the oracle's
     FFT, and the inverse returns every rank's input."""
+    _four_step_full(25, world, None)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [4, 8])
+def test_four_step_2_24_split(world):
+    """The bench's plan for 2^24 (split_log_r: R = 2^8, C = 2^16 -- packed
+    one-pass column NTTs, the precomputed exchange twiddles, the
+    transpose-free exchange layout) with `world` simulated ranks on one GPU:
+    every slab equals the oracle's FFT, the inverse returns the input."""
+    from tachyon_amd.ntt import FourStepNtt
+    assert FourStepNtt.split_log_r(24, world) == 8
+    _four_step_full(24, world, 8)
+
+
+def _four_step_full(log_n, world, log_r):
     import torch
     from tachyon_amd.ntt import FourStepNtt
-    log_n = 25
     n = 1 << log_n
-    x = O.gen_scalars("bn254_fr", 5125 + world, n).reshape(n, 4)
+    x = O.gen_scalars("bn254_fr", 5100 + log_n + world, n).reshape(n, 4)
     X = x.copy().reshape(-1)
     O.fft_np(X)
     X = X.reshape(n, 4)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     try:
-        plans = [FourStepNtt(log_n, world, r, stream) for r in range(world)]
+        plans = [FourStepNtt(log_n, world, r, stream, log_r=log_r) for r in range(world)]
         chunk = (n // world // world) * 32
 
         def run(inputs, inverse):
@@ -140,11 +155,12 @@ def test_four_step_2_25(world):
             torch.cuda.synchronize()
             return outs
 
-        ins = [torch.from_numpy(np.ascontiguousarray(x[FourStepNtt.input_indices(log_n, world, r)]).view(np.uint8)
-                                .reshape(-1)).cuda() for r in range(world)]
+        ins = [torch.from_numpy(np.ascontiguousarray(x[FourStepNtt.input_indices(log_n, world, r, log_r)])
+                                .view(np.uint8).reshape(-1)).cuda() for r in range(world)]
         outs = run(ins, False)
         for r in range(world):
-            assert outs[r].cpu().numpy().tobytes() == X[FourStepNtt.output_indices(log_n, world, r)].tobytes(), r
+            want = X[FourStepNtt.output_indices(log_n, world, r, log_r)].tobytes()
+            assert outs[r].cpu().numpy().tobytes() == want, r
         back = run(outs, True)
         for r in range(world):
             assert torch.equal(back[r], ins[r]), r
