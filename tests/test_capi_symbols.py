@@ -94,3 +94,26 @@ def test_circom_prover_device_list_parsing():
         r = subprocess.run([exe, "--zkey", "a", "--wtns", "b", "--proof", "c", "--public", "d", "--devices", bad],
                            capture_output=True, text=True, timeout=60)
         assert r.returncode == 1 and "usage:" in r.stderr + r.stdout, (bad, r.returncode, r.stderr)
+
+
+def test_four_step_split_rule_on_the_host(libpath):
+    """tachyon_mi355x_ntt4_split_log_r is host logic (no GPU call): the R x C
+    split with the fewest pass launches (passes of <= 8 stages), R and C >=
+    the world, ties to the larger R up to C -- the rule the bench's four-step
+    leg, its projection and the multi-device domain follow."""
+    from tachyon_amd._lib import lib
+
+    def passes(k):
+        return (k + 7) // 8
+
+    for log_n in range(2, 29):
+        for lg in range(0, 4):
+            r = lib().tachyon_mi355x_ntt4_split_log_r(log_n, lg)
+            if 2 * lg > log_n:
+                assert r == log_n // 2  # no valid split: the default, which the plan then refuses
+                continue
+            c = log_n - r
+            assert lg <= r <= c, (log_n, lg, r)
+            best = min(passes(x) + passes(log_n - x) for x in range(max(1, lg), log_n) if lg <= log_n - x and x <= log_n - x)
+            assert passes(r) + passes(c) == best, (log_n, lg, r)
+    assert lib().tachyon_mi355x_ntt4_split_log_r(24, 3) == 8
