@@ -48,6 +48,7 @@ def main():
             p.set_profile(False)
             print(json.dumps({"log_n": args.log_n, "c_a": ca, "c_lh": clh, "c_b2": cb2, "variant": var, "round": rnd,
                               "median_ms": round(sorted(ts)[len(ts) // 2], 3), "min_ms": round(min(ts), 3),
+                              "mean_ms": round(sum(ts) / len(ts), 3), "reps_ms": [round(t, 3) for t in ts],
                               "phases": {k: round(v, 3) for k, v in ph.items()}}), flush=True)
     p.close()
 
