@@ -452,7 +452,8 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ct
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule).
  * Every accepted variant computes the same MSM; returns 0 (nothing changed)
- * for bits outside 0x7FFFBF (bits 0-22 but 6). */
+ * for bits outside 0xFFFFBF (bits 0-23 but 6; bit 23: two-level window sums
+ * for the G2 / BLS12-381 G1 / FIPS reductions, measured slower). */
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
  * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total,

@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0x7FFFBF;  // bits 0-22 except 6 (21: a debug check, not a schedule)
+constexpr int kMsmVariantMask = 0xFFFFBF;  // bits 0-23 except 6 (21: a debug check, not a schedule)
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair

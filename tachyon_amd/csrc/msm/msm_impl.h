@@ -1440,6 +1440,52 @@ __global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_segment
   Ar::store(out, t, acc);
 }
 
+// Two-level window sums with one lane per point (the pair kernels below
+// explain the scheme): level 1 A_j, R_j per L1-bucket segment without fix-up,
+// level 2 sum_j j R_j with 0-based weights, out = sum_j A_j + L1 sum_j j R_j.
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_seg1_kernel(
+    const XYZZ<typename Curve::F>* __restrict__ bucket_sum, unsigned W, unsigned B, unsigned L,
+    XYZZ<typename Curve::F>* __restrict__ out_a, XYZZ<typename Curve::F>* __restrict__ out_r) {
+  const uint32_t S = B / L;
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= W * S) return;
+  const uint32_t w = t / S, j = t - w * S;
+  const size_t b0 = (size_t)w * B + (size_t)j * L;
+  typename Ar::A R = Ar::zero(), acc = Ar::zero();
+  for (int k = (int)L - 1; k >= 0; --k) {
+    R = Ar::add(R, Ar::load(bucket_sum, b0 + k));
+    acc = Ar::add(acc, R);
+  }
+  Ar::store(out_a, t, acc);
+  Ar::store(out_r, t, R);
+}
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_seg2_kernel(
+    const XYZZ<typename Curve::F>* __restrict__ in, unsigned W, unsigned S, unsigned L2,
+    XYZZ<typename Curve::F>* __restrict__ out) {
+  const uint32_t S2 = S / L2;
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= W * S2) return;
+  const uint32_t w = t / S2, q = t - w * S2;
+  const size_t b0 = (size_t)w * S + (size_t)q * L2;
+  typename Ar::A R = Ar::zero(), acc = Ar::zero();
+  for (int k = (int)L2 - 1; k >= 0; --k) {  // acc before R: weights k, not k + 1
+    acc = Ar::add(acc, R);
+    R = Ar::add(R, Ar::load(in, b0 + k));
+  }
+  acc = Ar::add(acc, small_mul_ar<Ar>(R, q * L2));
+  Ar::store(out, t, acc);
+}
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, AccWaves<Curve>::value) void window_combine_kernel(
+    const XYZZ<typename Curve::F>* __restrict__ a, const XYZZ<typename Curve::F>* __restrict__ b, unsigned W,
+    unsigned m, XYZZ<typename Curve::F>* __restrict__ out) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= W) return;
+  Ar::store(out, t, Ar::add(Ar::load(a, t), small_mul_ar<Ar>(Ar::load(b, t), m)));
+}
+
 // The G2 reductions with a lane pair per point (acc_pair.h): the one-lane
 // XYZZ<Fq2> additions hold two points and their temporaries (BLS12-381:
 // 220-460 spilled VGPRs per kernel, 21 ms of a 2^24 MSM); split by component
@@ -1558,6 +1604,73 @@ __global__ __launch_bounds__(kBlock, 2) void window_segment_pair_kernel(const XY
   }
   acc = Ar::add(acc, Ar::small_mul(R, j * L, h != 0), h != 0);
   Ar::store(reinterpret_cast<Fb*>(out), t, h, acc);
+}
+
+// Two-level window sums (G2 lane pairs, round 5).  sum_b (b + 1) B_b over a
+// window's B buckets in segments of L1: level 1 gives each segment j its local
+// weighted sum A_j = sum_k (k + 1) B_{j L1 + k} and plain sum R_j with no
+// (j L1) R_j fix-up; level 2 prices all fix-ups at once, sum_j j R_j, by the
+// same running sums over the R_j (0-based weights, segments of L2 with the
+// small fix-up of the one-level kernel); the window is sum_j A_j + L1 sum_j j
+// R_j.  Per bucket ~2 + 3 / L1 additions instead of 2 + (the ~log2(B)
+// doublings and adds of a fix-up) / L, and with L1 = 16 four times the threads
+// of L = 64.  Measured slower (set_variant bit 23, see the window sums in
+// enqueue): the trees over the partial sums add more than the fix-ups cost.
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, 2) void window_seg1_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+                                                                  unsigned W, unsigned B, unsigned L,
+                                                                  XYZZ<typename Curve::F>* __restrict__ out_a,
+                                                                  XYZZ<typename Curve::F>* __restrict__ out_r) {
+  using Fb = typename Ar::Fb;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t S = B / L;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W * S) return;
+  const uint32_t w = t / S, j = t - w * S;
+  const Fb* bs = reinterpret_cast<const Fb*>(bucket_sum);
+  const size_t b0 = (size_t)w * B + (size_t)j * L;
+  typename Ar::A R = Ar::zero(h != 0), acc = R;
+  for (int k = (int)L - 1; k >= 0; --k) {
+    R = Ar::add(R, Ar::load(bs, b0 + k, h), h != 0);
+    acc = Ar::add(acc, R, h != 0);
+  }
+  Ar::store(reinterpret_cast<Fb*>(out_a), t, h, acc);
+  Ar::store(reinterpret_cast<Fb*>(out_r), t, h, R);
+}
+// level 2: out[w S2 + q] = sum_{k < L2} (q L2 + k) R_{w S + q L2 + k}
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, 2) void window_seg2_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
+                                                                  unsigned W, unsigned S, unsigned L2,
+                                                                  XYZZ<typename Curve::F>* __restrict__ out) {
+  using Fb = typename Ar::Fb;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t S2 = S / L2;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W * S2) return;
+  const uint32_t w = t / S2, q = t - w * S2;
+  const Fb* src = reinterpret_cast<const Fb*>(in);
+  const size_t b0 = (size_t)w * S + (size_t)q * L2;
+  typename Ar::A R = Ar::zero(h != 0), acc = R;
+  for (int k = (int)L2 - 1; k >= 0; --k) {  // acc before R: weights k, not k + 1
+    acc = Ar::add(acc, R, h != 0);
+    R = Ar::add(R, Ar::load(src, b0 + k, h), h != 0);
+  }
+  acc = Ar::add(acc, Ar::small_mul(R, q * L2, h != 0), h != 0);
+  Ar::store(reinterpret_cast<Fb*>(out), t, h, acc);
+}
+// out[w] = a[w] + m b[w]
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, 2) void window_combine_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ a,
+                                                                     const XYZZ<typename Curve::F>* __restrict__ b,
+                                                                     unsigned W, unsigned m,
+                                                                     XYZZ<typename Curve::F>* __restrict__ out) {
+  using Fb = typename Ar::Fb;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W) return;
+  const typename Ar::A x = Ar::load(reinterpret_cast<const Fb*>(a), t, h);
+  const typename Ar::A y = Ar::load(reinterpret_cast<const Fb*>(b), t, h);
+  Ar::store(reinterpret_cast<Fb*>(out), t, h, Ar::add(x, Ar::small_mul(y, m, h != 0), h != 0));
 }
 
 template <class Curve, class Ar = FipsPairArith<Curve>>
@@ -2355,6 +2468,90 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   }
 
   // ---- window sums ----
+  // Two-level window sums (window_seg1/2 + combine) under set_variant bit 23,
+  // for the G2 lane pairs and the one-lane BLS12-381 G1 / FIPS reductions: an
+  // A/B that lost -- BLS12-381 G2 2^24 109.0 vs 106.2 ms (reduction 16.3 vs
+  // 13.7), BN254 G2 2^20 6.6 vs 5.15 ms (2.18 vs 0.95), Groth16 2^20 12.8 vs
+  // 11.4 ms (profiles/r05w/): the extra launches of two binary trees over
+  // W x B/16 and W x B/1024 partial sums cost more than the fix-ups they save.
+  // The one-level kernels (per-segment (jL) R fix-up) stay the default.
+  using WinKernel1 = void (*)(const Point*, unsigned, unsigned, unsigned, Point*, Point*);
+  using WinKernel2 = void (*)(const Point*, unsigned, unsigned, unsigned, Point*);
+  using WinKernelC = void (*)(const Point*, const Point*, unsigned, unsigned, Point*);
+  WinKernel1 seg1 = nullptr;
+  WinKernel2 seg2 = nullptr;
+  WinKernelC comb = nullptr;
+  if constexpr (kG2) {
+    if (pair_reduce) {
+      using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
+      if (pair_limb_ && !(variant_ & (1 << 22))) {
+        seg1 = &window_seg1_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        seg2 = &window_seg2_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        comb = &window_combine_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+      } else {
+        seg1 = &window_seg1_pair_kernel<Curve, FipsPairArith<Curve>>;
+        seg2 = &window_seg2_pair_kernel<Curve, FipsPairArith<Curve>>;
+        comb = &window_combine_pair_kernel<Curve, FipsPairArith<Curve>>;
+      }
+    }
+  } else {
+    bool fips = true;
+    if constexpr (std::is_same_v<Curve, Bn254G1>) fips = !acc29_;  // the 29-bit raw path below
+    if constexpr (std::is_same_v<Curve, Bls381G1>) {
+      if (acc28_ && !(variant_ & (1 << 22))) {
+        seg1 = &window_seg1_kernel<Curve, Limb28Arith>;
+        seg2 = &window_seg2_kernel<Curve, Limb28Arith>;
+        comb = &window_combine_kernel<Curve, Limb28Arith>;
+        fips = false;
+      }
+    }
+    if (fips) {
+      seg1 = &window_seg1_kernel<Curve, FipsArith<Curve>>;
+      seg2 = &window_seg2_kernel<Curve, FipsArith<Curve>>;
+      comb = &window_combine_kernel<Curve, FipsArith<Curve>>;
+    }
+  }
+  if (seg1 && (variant_ & (1 << 23)) && !tree_reduce_) {
+    const unsigned L1 = std::min(16u, B), S1 = B / L1;
+    const unsigned L2 = std::min(64u, S1), S2 = S1 / L2;
+    // A_j, R_j (W S1 each), level-2 sums (W S2), two tree ping-pong halves, the two window sums
+    const size_t tmp = (size_t)W * ((S1 + 1) / 2 + 1);
+    Point* segA = static_cast<Point*>(
+        seg_a_.ensure(((size_t)2 * W * S1 + (size_t)W * S2 + 2 * tmp + 2 * W) * sizeof(Point)));
+    Point* segR = segA + (size_t)W * S1;
+    Point* seg2o = segR + (size_t)W * S1;
+    Point* tA = seg2o + (size_t)W * S2;
+    Point* tB = tA + tmp;
+    Point* winA = tB + tmp;
+    Point* winB = winA + W;
+    hipLaunchKernelGGL(seg1, dim3(grid_for(lanes * (size_t)W * S1)), dim3(kBlock), 0, stream_, bucket_sum, W, B, L1,
+                       segA, segR);
+    hipLaunchKernelGGL(seg2, dim3(grid_for(lanes * (size_t)W * S2)), dim3(kBlock), 0, stream_, segR, W, S1, L2, seg2o);
+    TA_HIP(hipGetLastError());
+    // binary trees (win_reduce) of the W x S arrays down to one point per window
+    auto tree = [&](Point* src, unsigned S, Point* dst) {
+      Point* cur = src;
+      Point* bufs[2] = {tA, tB};
+      int k = 0;
+      while (S > 1) {
+        const unsigned S_out = (S + 1) / 2;
+        Point* o = (S_out == 1) ? dst : bufs[k];
+        hipLaunchKernelGGL(win_reduce, dim3(grid_for(lanes * (size_t)W * S_out)), dim3(kBlock), 0, stream_, cur, W, S,
+                           2u, o);
+        TA_HIP(hipGetLastError());
+        cur = o;
+        k ^= 1;
+        S = S_out;
+      }
+      if (cur != dst) TA_HIP(hipMemcpyAsync(dst, cur, W * sizeof(Point), hipMemcpyDeviceToDevice, stream_));
+    };
+    tree(segA, S1, winA);
+    tree(seg2o, S2, winB);
+    hipLaunchKernelGGL(comb, dim3(grid_for(lanes * (size_t)W)), dim3(kBlock), 0, stream_, winA, winB, W, L1, d_windows);
+    TA_HIP(hipGetLastError());
+    if (profile_) TA_HIP(hipEventRecord(ev_[5], stream_));
+    return;
+  }
   if (tree_reduce_) {
     // segments of L buckets, workgroup trees of kWinBlock nodes, launches until one node per window
     unsigned L = plan.seg_tree, log_l = 0;

@@ -65,11 +65,13 @@ def test_msm_golden_bn254_g1_variants(variant):
                                            ("bn254_g2", 1 << 22), ("bls12_381_g2", 1 << 22),
                                            ("bls12_381_g2", 0),
                                            ("bls12_381_g2", 32768), ("bls12_381_g2", 65536 | (1 << 20)),
-                                           ("bls12_381_g2", 1 << 20)])
+                                           ("bls12_381_g2", 1 << 20), ("bn254_g2", 1 << 23),
+                                           ("bls12_381_g2", 1 << 23)])
 def test_msm_golden_g2_lane_pair(curve, variant):
     """The G2 accumulations and reductions: a lane pair per point over the
     limb fields (the default: BN254 9 x 29-bit, BLS12-381 14 x 28-bit), the
-    FIPS pair (bit 20), the FIPS pair reductions (bit 22),
+    FIPS pair (bit 20), the FIPS pair reductions (bit 22), the two-level
+    window sums instead of the per-segment fix-ups (bit 23, an A/B),
     the one-lane kernel (set_variant bit 15) and, for BLS12-381, the FIPS pair
     with out-of-line 12-limb products (bit 16) -- golden edge cases, a
     random set, a repeated base (doublings inside one bucket) and P, -P
@@ -393,7 +395,7 @@ def test_msm_schedule_variants_agree(curve, logn):
                     assert s["acc28"] == limb, (hex(v), s)
                 else:  # BN254 G2: the pair over 29-bit limbs; bit 20 the FIPS pair
                     assert s["acc29"] == limb, (hex(v), s)
-        for bad in (64, 1 << 23):
+        for bad in (64, 1 << 24):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
@@ -423,7 +425,9 @@ def _neg_point(curve, p: bytes) -> bytes:
 @pytest.mark.parametrize("curve,variant", [("bn254_g1", 0), ("bn254_g1", 262144), ("bn254_g2", 0),
                                            ("bn254_g2", 1 << 22), ("bls12_381_g1", 0), ("bls12_381_g1", 1 << 22),
                                            ("bls12_381_g2", 0), ("bls12_381_g2", 1 << 22),
-                                           ("bls12_381_g2", 32768)])
+                                           ("bls12_381_g2", 32768), ("bls12_381_g1", 1 << 23),
+                                           ("bls12_381_g2", 1 << 23), ("bn254_g2", 1 << 23),
+                                           ("bn254_g1", 262144 | (1 << 23))])
 def test_msm_reduction_edge_cases(curve, variant):
     """Inputs that drive the chain join and the window sums through their
     special cases: every base the same point (equal bucket pieces and equal
