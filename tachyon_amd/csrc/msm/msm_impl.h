@@ -2008,6 +2008,14 @@ hipError_t onesweep_pass(unsigned cfg, const uint64_t* in, uint64_t* out, uint32
     case 3:
       return onesweep_pass_cfg<MsmOnesweep<1024, 12, R::match>>(in, out, size, bit, end_bit, digit_offsets,
                                                                   offsets_tmp, lookback, block_id, s);
+#ifdef TACHYON_TUNING_KNOBS  // more tile shapes for A/B (TACHYON_ONESWEEP_CFG=4, 5; tuning builds only)
+    case 4:
+      return onesweep_pass_cfg<MsmOnesweep<1024, 16, R::match>>(in, out, size, bit, end_bit, digit_offsets,
+                                                                  offsets_tmp, lookback, block_id, s);
+    case 5:
+      return onesweep_pass_cfg<MsmOnesweep<512, 16, R::match>>(in, out, size, bit, end_bit, digit_offsets,
+                                                                 offsets_tmp, lookback, block_id, s);
+#endif
     default:
       return onesweep_pass_cfg<MsmOnesweep<1024, 8, R::match>>(in, out, size, bit, end_bit, digit_offsets,
                                                                  offsets_tmp, lookback, block_id, s);
@@ -2655,6 +2663,9 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   static constexpr uint32_t kSpt[] = {kRecodeSpt, 1, 4, 3};
   recode_spt_ = kSpt[(variant_ >> 8) & 3];  // bits 8-9: scalars per thread of the fused recode
   sort_cfg_ = (variant_ >> 4) & 3;  // bits 4-5: onesweep tile shape
+#ifdef TACHYON_TUNING_KNOBS
+  if (const char* e = getenv("TACHYON_ONESWEEP_CFG")) sort_cfg_ = (unsigned)std::clamp(atoi(e), 0, 5);
+#endif
   rocprim_hist_ = (variant_ & 1024) != 0;  // bit 10: rocPRIM's own digit histogram pass (A/B)
   wide_stage_ = (variant_ & 2048) != 0;    // bit 11: 8-byte LDS staging in the recode scatter (A/B)
   tree_reduce_ = (variant_ & 4096) != 0;   // bit 12: window sums by workgroup trees (A/B)
