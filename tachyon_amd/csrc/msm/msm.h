@@ -266,7 +266,7 @@ class MsmGpu {
   hipStream_t copy_stream_ = nullptr;
   hipEvent_t copy_done_ = nullptr;
   std::vector<hipEvent_t> chunk_ev_;  // host-resident pipeline: chunk k uploaded
-  DeviceBuffer hist_, hscan_tmp_;
+  DeviceBuffer hist_;
   DeviceBuffer norm_in_, norm_out_, norm_prefix_;  // affine_bases
   DeviceBuffer maxlen_, lofs_;  // lofs_: every join level's output offsets
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket

@@ -2932,7 +2932,7 @@ template <class Curve>
 size_t MsmGpu<Curve>::held_bytes() const {
   const DeviceBuffer* bufs[] = {&ents_,  &ents2_, &sort_tmp_, &scan_tmp_, &start_, &end_,
                                 &cnt_,   &off_a_, &off_b_, &part_a_, &part_b_,  &seg_a_,    &seg_b_, &buckets_,
-                                &hist_, &hscan_tmp_, &lofs_};
+                                &hist_, &lofs_};
   size_t s = 0;
   for (const DeviceBuffer* b : bufs) s += b->capacity();
   return s;
