@@ -352,11 +352,12 @@ XGMI_LINK_GBS = 76.0
 # partition (N/Q point groups x Q window groups), point shards elsewhere.  The
 # slowest rank on one MI355X (tools/split_probe.py --hybrid): BN254 2^26 at N =
 # 8 11.45 ms vs 12.11 for the 2^23 point shard, N = 4 21.45 vs 21.40 (points
-# kept) (profiles/r05c/hybrid_split_probe.jsonl); BLS12-381 2^24 G1 N = 4
-# 12.35 vs 12.65, N = 8 6.91 vs 7.02; G2 N = 4 31.16 vs 32.19, N = 8 17.21
-# vs 17.81 (profiles/r05m/)
+# kept) (profiles/r05c/hybrid_split_probe.jsonl); BLS12-381 2^24 G2 N = 4
+# 31.16 vs 32.19, N = 8 17.21 vs 17.81 (profiles/r05m/), and again in the
+# bench projections of three boxes (r05p/r05r/r05z: G2 hybrid 1-5 % faster);
+# BLS12-381 G1's hybrid (P2 x Q2 c = 19 at 4, P4 x Q2 c = 16 at 8) came out
+# within noise of the point shard there (-2 .. +4 %), so G1 keeps point shards
 HYBRID_PLANS = {("bn254_g1", 8): (2, 19),
-                ("bls12_381_g1", 4): (2, 19), ("bls12_381_g1", 8): (2, 16),
                 ("bls12_381_g2", 4): (2, 19), ("bls12_381_g2", 8): (4, 16)}
 
 
