@@ -451,9 +451,36 @@ struct Fp {
 
   // Montgomery -> canonical integer (ToBigInt, prime_field_fallback.h:166-169)
   TA_HD Fp from_mont() const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // device: the Montgomery reduction alone (N rounds of one digit and N
+    // multiply-adds: 64 v_mad_u64_u32 for 8 limbs, against 128 for the
+    // product by 1 through the asm multiply, whose zero limbs it cannot
+    // skip) -- the MSM recode runs this once per scalar in each of its two
+    // passes.  For x < 2p: (x + m p) / 2^(32N) <= p, and = p only for x = p.
+    uint32_t t[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) t[i] = v[i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint32_t k = t[0] * Cfg::kInv32;
+      uint64_t s = (uint64_t)k * Cfg::kP32[0] + t[0];
+#pragma unroll
+      for (int j = 1; j < N; ++j) {
+        s = (uint64_t)k * Cfg::kP32[j] + ((uint64_t)t[j] + (s >> 32));
+        t[j - 1] = (uint32_t)s;
+      }
+      t[N - 1] = (uint32_t)(s >> 32);
+    }
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r.v[i] = t[i];
+    reduce_once(r.v);
+    return r;
+#else
     Fp one_plain = zero();
     one_plain.v[0] = 1;
     return ((*this) * one_plain).canonical();
+#endif
   }
   // canonical integer (< p) -> Montgomery (lazy on device)
   TA_HD Fp to_mont() const {
