@@ -60,7 +60,13 @@ def pmc_traffic(kernel):
     passes (profiles/<round>/pmc_traffic.json, written by tools/profile_round.sh
     from separate FETCH_SIZE / WRITE_SIZE runs of this bench command); None if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")))
+    import re
+
+    def order(f):  # r05z < r05aa < r05ab (spreadsheet-column order of the run suffix)
+        m = re.fullmatch(r"r(\d+)([a-z]*)", os.path.basename(os.path.dirname(f)))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, f)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), key=order)
     for f in reversed(files):
         try:
             t = json.load(open(f))
