@@ -416,6 +416,21 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_window_range_affine(int curve, void
  * every failure of this library does). */
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_batch_affine(int curve, void* ctx, const void* bases, size_t len,
                                                         const void* scalars, size_t count, void* out_affine);
+/* Fixed-base folding (bases known ahead, e.g. a proving key; an extension,
+ * no reference counterpart -- the result is the same MSM).  _plan_windows:
+ * W for `size` points under the context's window bits.  _fold_bases: from
+ * `size` device-resident affine bases, `fold` x `size` affine points into
+ * out_bases (device): copy k = 2^(k c W / fold) * P_i.  _folded_affine: the
+ * MSM of `size` device scalars over such a table (same size, same window
+ * bits), with W / fold window sums instead of W.  Both return 1, or 0
+ * (nothing written) when fold does not divide W or a pointer is not device
+ * memory. */
+TACHYON_C_EXPORT unsigned tachyon_mi355x_msm_gpu_plan_windows(int curve, const void* ctx, size_t size);
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_fold_bases(int curve, void* ctx, const void* bases, size_t size,
+                                                      unsigned fold, void* out_bases);
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_folded_affine(int curve, void* ctx, const void* folded_bases,
+                                                         const void* scalars, size_t size, unsigned fold,
+                                                         void* out_affine);
 /* Contexts for the C++ plugin boundary (include/tachyon_mi355x_msm.h):
  * VariableBaseMSMGpu<Point>(mem_pool, stream) (variable_base_msm_gpu.h:16-18)
  * over any of the four groups, its work on `stream` (hipStream_t; NULL = a
@@ -592,10 +607,14 @@ TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_sharded(tachyon_mi355x_groth1
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                          size_t count, void* out_h);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on);
-/* A/B: variant 1 runs A and the witness + h MSM as two MSMs (round 4); 0
- * (default) as one grouped MSM over their own bases (one recode / sort /
- * accumulation / reduction; single-device proofs).  Same proof; returns 0
- * for other values. */
+/* A/B: variant bit 0 runs A and the witness + h MSM as two MSMs (round 4);
+ * clear (default) as one grouped MSM over their own bases (one recode / sort
+ * / accumulation / reduction; single-device proofs).  Bits 1-3 pick the fold
+ * of the G2 B query (a table of its points times 2^(k c W / F), built on the
+ * first proof; _msm_gpu_fold_bases), bits 4-6 the fold of the grouped G1
+ * MSM's bases: 0 the default (B2 16 copies, G1 4), k = 1..5 2^(k-1) copies (1 =
+ * none), each lowered to the largest power of two dividing the MSM's window
+ * count.  Same proof for every variant; returns 0 for other values. */
 TACHYON_C_EXPORT int tachyon_mi355x_groth16_set_variant(tachyon_mi355x_groth16_prover* prover, int variant);
 /* Window bits of the proof's MSMs (0 = each MSM's size default): A (and B in
  * G1), the merged witness + h MSM, B in G2.  Tuning / A/B; the proof is the

@@ -123,6 +123,9 @@ SIGNATURES = [
     ("tachyon_mi355x_msm_gpu_affine", None, [i32, vp, vp, vp, sz, vp]),
     ("tachyon_mi355x_msm_gpu_window_range_affine", None, [i32, vp, vp, vp, sz, ctypes.c_uint, ctypes.c_uint, vp]),
     ("tachyon_mi355x_msm_gpu_batch_affine", i32, [i32, vp, vp, sz, vp, sz, vp]),
+    ("tachyon_mi355x_msm_gpu_plan_windows", ctypes.c_uint, [i32, vp, sz]),
+    ("tachyon_mi355x_msm_gpu_fold_bases", i32, [i32, vp, vp, sz, ctypes.c_uint, vp]),
+    ("tachyon_mi355x_msm_gpu_folded_affine", i32, [i32, vp, vp, vp, sz, ctypes.c_uint, vp]),
     ("tachyon_mi355x_msm_gpu_create", vp, [i32, vp]),
     ("tachyon_mi355x_msm_gpu_destroy", None, [i32, vp]),
     ("tachyon_mi355x_msm_gpu_run", i32, [i32, vp, vp, sz, vp, sz, i32, vp]),

@@ -164,6 +164,14 @@ void msm_window_range_out(void* ctx, const void* bases, const void* scalars, siz
   memcpy(out, &a, sizeof(a));
 }
 
+template <class Curve>
+void msm_folded_out(void* ctx, const void* folded_bases, const void* scalars, size_t n, unsigned fold, void* out) {
+  using F = typename Curve::F;
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  Affine<F> a = c->impl.run_folded(folded_bases, scalars, n, fold).to_affine();
+  memcpy(out, &a, sizeof(a));
+}
+
 // `count` MSMs over the same device-resident bases in one launch sequence
 // (MsmGpu::run_batch): count affine results ((0, 0) = identity)
 template <class Curve>
@@ -412,6 +420,25 @@ int tachyon_mi355x_msm_gpu_batch_affine(int curve, void* ctx, const void* bases,
                                         size_t count, void* out_affine) {
   if (!is_device_pointer(bases)) return 0;
   GUARD_BEGIN CURVE_DISPATCH(curve, msm_batch_out<C>(ctx, bases, len, scalars, count, out_affine)) GUARD_END
+  return 1;
+}
+unsigned tachyon_mi355x_msm_gpu_plan_windows(int curve, const void* ctx, size_t size) {
+  GUARD_BEGIN CURVE_DISPATCH(curve, return static_cast<const MsmCtx<C>*>(ctx)->impl.plan_windows(size)) GUARD_END
+  return 0;
+}
+int tachyon_mi355x_msm_gpu_fold_bases(int curve, void* ctx, const void* bases, size_t size, unsigned fold,
+                                      void* out_bases) {
+  if (fold == 0 || !is_device_pointer(bases) || !is_device_pointer(out_bases)) return 0;
+  if (tachyon_mi355x_msm_gpu_plan_windows(curve, ctx, size) % fold != 0) return 0;  // refused, nothing written
+  GUARD_BEGIN CURVE_DISPATCH(curve, static_cast<MsmCtx<C>*>(ctx)->impl.fold_bases(bases, size, fold, out_bases))
+  GUARD_END
+  return 1;
+}
+int tachyon_mi355x_msm_gpu_folded_affine(int curve, void* ctx, const void* folded_bases, const void* scalars,
+                                         size_t size, unsigned fold, void* out_affine) {
+  if (fold == 0 || !is_device_pointer(folded_bases) || !is_device_pointer(scalars)) return 0;
+  if (fold > 1 && tachyon_mi355x_msm_gpu_plan_windows(curve, ctx, size) % fold != 0) return 0;
+  GUARD_BEGIN CURVE_DISPATCH(curve, msm_folded_out<C>(ctx, folded_bases, scalars, size, fold, out_affine)) GUARD_END
   return 1;
 }
 void* tachyon_mi355x_msm_gpu_create(int curve, void* stream) {

@@ -294,7 +294,7 @@ void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, i
 }
 
 int tachyon_mi355x_groth16_set_variant(tachyon_mi355x_groth16_prover* prover, int variant) {
-  if (variant < 0 || variant > 1) return 0;
+  if (!BnProver::valid_variant(variant)) return 0;
   GUARD_BEGIN
   PROVER_DISPATCH(prover, impl->set_variant(variant));
   for (auto& p : prover->bn_dev) p->set_variant(variant);

@@ -99,8 +99,18 @@ class Groth16Prover {
   // window bits of the proof's MSMs (0 = each MSM's default): A (and B in G1),
   // the merged witness + h MSM, B in G2 -- tuning and A/B only
   // A/B: bit 0 = A and the witness + h MSM as two MSMs (round 4) instead of
-  // one grouped MSM (MsmGpu::run_groups, one process one device)
+  // one grouped MSM (MsmGpu::run_groups, one process one device); bits 1-3 =
+  // the fold of the G2 B MSM's fixed bases (MsmGpu::run_folded), bits 4-6 the
+  // fold of the grouped G1 MSM's (run_groups_folded): 0 the default (kB2Fold
+  // / kG1Fold), k = 1..5 2^(k-1) copies at most (1 = none); valid_variant checks
+  static bool valid_variant(int v) { return v >= 0 && v < 128 && ((v >> 1) & 7) <= 5 && ((v >> 4) & 7) <= 5; }
   void set_variant(int v) { variant_ = v; }
+  unsigned b2_fold() const { return fold_of((variant_ >> 1) & 7, kB2Fold); }
+  unsigned g1_fold() const { return fold_of((variant_ >> 4) & 7, kG1Fold); }
+  // (the largest power of two up to these that divides the MSM's W).
+  // profiles/r05ai: B2 x16 + G1 x4 10.06 ms per 2^20 proof, B2 x8 10.13, B2
+  // x4 10.33, G1 x2 10.34, no tables 11.11; r05ah: both x8 10.27, G1 x8 10.41
+  static constexpr unsigned kB2Fold = 16, kG1Fold = 4;
   int variant() const { return variant_; }
   void set_msm_window_bits(unsigned c_a, unsigned c_lh, unsigned c_b2) {
     c_a_ = c_a;
@@ -111,6 +121,7 @@ class Groth16Prover {
   hipStream_t stream() const { return stream_; }
 
  private:
+  static unsigned fold_of(unsigned sel, unsigned dflt) { return sel == 0 ? dflt : 1u << (sel - 1); }
   void init_device_state();
   void build_groups();
   Key key_;  // host copy: verifying-key points and the query heads used on the host
@@ -126,6 +137,11 @@ class Groth16Prover {
   std::unique_ptr<msm::MsmGpu<G1>> msm1_;
   std::unique_ptr<msm::MsmGpu<G2>> msm2_;
   DeviceBuffer a1_, b1_, lh1_, b2_;              // query points (lh1 = C1 | H1)
+  DeviceBuffer b2_fold_;                         // the G2 B query's fold table (built on first use)
+  size_t b2_fold_lo_ = 0, b2_fold_len_ = 0;      // ... over b2 + 1 + [lo, lo + len)
+  unsigned b2_fold_f_ = 0, b2_fold_c_ = 0;       // ... its fold and window bits (0: none built)
+  DeviceBuffer g1_fold_;                         // the grouped G1 MSM's fold table (gbases_, first use)
+  unsigned g1_fold_f_ = 0, g1_fold_c_ = 0;
   DeviceBuffer lh_;                              // scalars of the merged MSM: witness | h
   DeviceBuffer row_a_, row_b_, col_, val_;       // CSR of the A and B matrices
   DeviceBuffer full_, abc_;                      // witness, 3 x n work vectors

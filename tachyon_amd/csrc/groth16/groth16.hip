@@ -429,7 +429,27 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
       TA_HIP(hipSetDevice(device));
       auto tb = Clock::now();
       msm2_->set_force_window_bits(c_b2_);
-      if (q_len) acc_b2 = msm2_->run(b2 + 1 + q_lo, d_full + 1 + q_lo, q_len);
+      // the B2 query is fixed: a fold table (built once per shard / window
+      // bits, the first proof's cost) halves the G2 window sums and their
+      // host Horner on the proof's critical path
+      // (the largest power of two up to the chosen fold that divides W)
+      unsigned fold = b2_fold();
+      if (q_len)
+        while (fold > 1 && msm2_->plan_windows(q_len) % fold != 0) fold >>= 1;
+      if (q_len && fold > 1) {
+        if (b2_fold_f_ != fold || b2_fold_c_ != c_b2_ || b2_fold_lo_ != q_lo || b2_fold_len_ != q_len) {
+          b2_fold_f_ = 0;
+          void* tab = b2_fold_.ensure((size_t)fold * q_len * sizeof(Affine<F2>));
+          msm2_->fold_bases(b2 + 1 + q_lo, q_len, fold, tab);
+          b2_fold_f_ = fold;
+          b2_fold_c_ = c_b2_;
+          b2_fold_lo_ = q_lo;
+          b2_fold_len_ = q_len;
+        }
+        acc_b2 = msm2_->run_folded(b2_fold_.as<Affine<F2>>(), d_full + 1 + q_lo, q_len, fold);
+      } else if (q_len) {
+        acc_b2 = msm2_->run(b2 + 1 + q_lo, d_full + 1 + q_lo, q_len);
+      }
       timings_.msm_b2 = ms_since(tb);
     } catch (...) {
       g2_error = std::current_exception();
@@ -464,7 +484,22 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   msm1_->set_force_window_bits(c_a_);
   if (grouped) {
     // groups: [A | pad], [witness + h, first glen], [the rest | pad]
-    const auto r = msm1_->run_groups(gbases_.as<Affine<F1>>(), gscalars_.as<Fr>(), glen_, 3);
+    // the group bases are fixed too: their fold table (built on first use)
+    unsigned f1 = g1_fold();
+    while (f1 > 1 && msm1_->batch_windows(glen_) % f1 != 0) f1 >>= 1;
+    std::vector<P1> r;
+    if (f1 > 1) {
+      if (g1_fold_f_ != f1 || g1_fold_c_ != c_a_) {
+        g1_fold_f_ = 0;
+        void* tab = g1_fold_.ensure((size_t)f1 * 3 * glen_ * sizeof(Affine<F1>));
+        msm1_->fold_bases_groups(gbases_.as<Affine<F1>>(), glen_, 3, f1, tab);
+        g1_fold_f_ = f1;
+        g1_fold_c_ = c_a_;
+      }
+      r = msm1_->run_groups_folded(g1_fold_.as<Affine<F1>>(), gscalars_.as<Fr>(), glen_, 3, f1);
+    } else {
+      r = msm1_->run_groups(gbases_.as<Affine<F1>>(), gscalars_.as<Fr>(), glen_, 3);
+    }
     out.a = r[0];
     out.lh = r[1] + r[2];
   } else {

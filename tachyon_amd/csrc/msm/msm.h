@@ -191,6 +191,27 @@ class MsmGpu {
   // affine points (valid until the next call).  Form 0 returns `bases` as is.
   const Aff* affine_bases(const void* bases, size_t n, int form);
 
+  // Fixed bases (a proving key's): with the plan's W windows of c bits and a
+  // fold F dividing W, fold_bases builds F copies of the n bases, copy k =
+  // 2^(k c W / F) P_i (device, F n affine points), and run_folded adds window
+  // w's digit to copy w / (W / F) in key window w mod (W / F): the same n W
+  // entries, W / F window sums -- 1 / F of the bucket reduction and of the
+  // host Horner.  Both take device-resident arrays; the plan (forced c or the
+  // size's default) must be the same for both calls.
+  void fold_bases(const void* bases, size_t n, unsigned fold, void* out);
+  Point run_folded(const void* folded_bases, const void* scalars, size_t n, unsigned fold);
+  // The same for run_groups: the table of the count x len bases (window bits
+  // of a batch of len-point MSMs, batch_window_bits), then the grouped MSMs
+  // over it (device scalars); copy k of the whole array at k count len.
+  void fold_bases_groups(const void* bases, size_t len, size_t count, unsigned fold, void* out);
+  std::vector<Point> run_groups_folded(const void* folded_bases, const void* scalars, size_t len, size_t count,
+                                       unsigned fold);
+  unsigned plan_windows(size_t n) const;  // W of the plan for n points
+  unsigned batch_windows(size_t len) const {  // W of run_batch / run_groups over len-point MSMs
+    const unsigned c = batch_window_bits(len);
+    return (Fr::Config::kModulusBits + 1 + c - 1) / c;
+  }
+
   static Point combine_windows(const std::vector<Point>& window_sums, unsigned c);
   // Mixed additions per second (G/s) of this curve's accumulation field code
   // in registers on the current device -- no gathers, no run logic: the VALU
@@ -223,7 +244,9 @@ class MsmGpu {
 
  private:
   unsigned batch_window_bits(size_t len) const;
-  std::vector<Point> run_batch_impl(const void* bases, const void* scalars, size_t len, size_t count, bool distinct);
+  std::vector<Point> run_batch_impl(const void* bases, const void* scalars, size_t len, size_t count, bool distinct,
+                                    unsigned fold = 1);
+  void fold_bases_c(const void* bases, size_t n, unsigned fold, void* out, unsigned c);
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
   Point run_host_pipelined(const void* bases, const void* scalars, size_t n, size_t chunks);
   size_t work_bytes(size_t n) const;
@@ -276,6 +299,7 @@ class MsmGpu {
   unsigned range_begin_ = 0, range_end_ = ~0u;  // window range of the next run_windows
   unsigned batch_ = 1;                           // MSMs in the next run_windows (run_batch)
   bool batch_distinct_ = false;                  // ... each over its own bases (run_groups)
+  unsigned fold_ = 1;                            // base copies of the next run_windows (run_folded)
 };
 
 extern template class MsmGpu<Bn254G1>;

@@ -51,9 +51,14 @@ template <class Fr, class Emit>
 // glen > 0 (a batch of MSMs, run_batch / run_groups): scalar i belongs to
 // MSM g = i / glen, its windows are g * wr .. g * wr + wr - 1 of the key space
 // and its base index is i - g * gstep (gstep = glen: the MSMs share one base
-// array; gstep = 0: MSM g has its own bases at [g glen, (g+1) glen))
+// array; gstep = 0: MSM g has its own bases at [g glen, (g+1) glen)).
+// fold_w > 0 (run_folded: F = W / fold_w copies of the bases, copy k =
+// 2^(k c fold_w) P): window w goes to key window w mod fold_w (of MSM g's
+// block g fold_w in a batch) and to copy w / fold_w, base index
+// vi + (w / fold_w) fold_n (fold_n = the length of one copy).
 __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsigned c, unsigned W, unsigned w0,
-                                              unsigned wr, Emit emit, uint32_t glen = 0, uint32_t gstep = 0) {
+                                              unsigned wr, Emit emit, uint32_t glen = 0, uint32_t gstep = 0,
+                                              uint32_t fold_w = 0, uint32_t fold_n = 0) {
   constexpr int N = Fr::N;
   Fr s = scalar.from_mont();
   uint32_t limbs[N];
@@ -64,7 +69,7 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
   uint32_t gw = 0, vi = i;
   if (glen) {
     const uint32_t g = i / glen;
-    gw = g * wr;
+    gw = g * (fold_w ? fold_w : wr);
     vi = i - g * gstep;
   }
   uint32_t carry = 0;
@@ -85,7 +90,12 @@ __device__ __forceinline__ void recode_scalar(const Fr& scalar, uint32_t i, unsi
       key = coeff;  // top digit, carry folded in, non-negative
       sign = 0;
     }
-    if (w >= w0) emit(w - w0, ((gw + w - w0) << c) | key, vi | sign);
+    if (fold_w) {
+      const uint32_t part = w / fold_w;
+      emit(w, ((gw + w - part * fold_w) << c) | key, (vi + part * fold_n) | sign);
+    } else if (w >= w0) {
+      emit(w - w0, ((gw + w - w0) << c) | key, vi | sign);
+    }
   }
 }
 
@@ -96,12 +106,14 @@ __device__ __forceinline__ uint32_t entry_val(uint64_t e) { return (uint32_t)e; 
 template <class Fr>
 __global__ __launch_bounds__(kBlock) void recode_kernel(const Fr* __restrict__ scalars, uint32_t n,
                                                         unsigned c, unsigned W, unsigned w0, unsigned wr,
-                                                        uint64_t* __restrict__ ents, uint32_t glen, uint32_t gstep) {
+                                                        uint64_t* __restrict__ ents, uint32_t glen, uint32_t gstep,
+                                                        uint32_t fold_w, uint32_t fold_n) {
   uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   recode_scalar(
       scalars[i], i, c, W, w0, wr,
-      [&](unsigned w, uint32_t key, uint32_t val) { ents[(size_t)w * n + i] = make_entry(key, val); }, glen, gstep);
+      [&](unsigned w, uint32_t key, uint32_t val) { ents[(size_t)w * n + i] = make_entry(key, val); }, glen, gstep,
+      fold_w, fold_n);
 }
 
 // Recode fused with the first radix pass (key bits 0..7), in two launches:
@@ -151,7 +163,7 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
                                                              uint32_t* __restrict__ hist,
                                                              uint32_t* __restrict__ later,
                                                              uint4* __restrict__ zero, size_t zero_n, uint32_t glen,
-                                                             uint32_t gstep) {
+                                                             uint32_t gstep, uint32_t fold_w, uint32_t fold_n) {
   // cnt2: the third place's counts (key bits 16..23) in four copies, one per
   // lane & 3, 264 words apart: those bits are the window (the same in every
   // lane of a step) and the digit's top bits, a handful of values per wave --
@@ -197,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void recode_hist_kernel(const Fr* __restric
             }
           }
         }
-      }, glen, gstep);
+      }, glen, gstep, fold_w, fold_n);
   }
   __syncthreads();
   hist[(size_t)blockIdx.x * 256 + t] = cnt[0][t];  // one coalesced 1 KiB row per block
@@ -316,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
                                                                 const uint32_t* __restrict__ hist,
                                                                 const uint32_t* __restrict__ off,
                                                                 uint64_t* __restrict__ ents, uint32_t glen,
-                                                                uint32_t gstep) {
+                                                                uint32_t gstep, uint32_t fold_w, uint32_t fold_n) {
   // the block's entries are binned in LDS first, then written out bin run by
   // bin run, so consecutive lanes store to consecutive addresses
   extern __shared__ uint64_t lds_u64[];
@@ -355,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void recode_scatter_kernel(const Fr* __rest
         } else {
           lents[p] = make_entry(key, val);
         }
-      }, glen, gstep);
+      }, glen, gstep, fold_w, fold_n);
   }
   __syncthreads();
   const uint32_t total = loff[255] + cur[255];
@@ -417,6 +429,27 @@ __global__ __launch_bounds__(kBlock) void points_to_affine_kernel(const F* __res
       a = {p[0] * (p[2] * dinv).sqr(), p[1] * dinv};
     }
     out[i] = a.canonical();
+  }
+}
+
+// Folded bases (MsmGpu::fold_bases): copy k of point i = 2^(k shift) P_i as
+// XYZZ (x, y, zz, zzz words) at out[(k n + i) * 4], by k shift doublings of
+// one thread; points_to_affine_kernel (form 3) then normalises them.  A
+// one-time table build (a proving key's), not a per-MSM pass.
+template <class F>
+__global__ __launch_bounds__(kBlock) void fold_points_kernel(const Affine<F>* __restrict__ in, size_t n, unsigned fold,
+                                                             unsigned shift, F* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  XYZZ<F> p = XYZZ<F>::from_affine(in[i]);
+  for (unsigned k = 0; k < fold; ++k) {
+    if (k > 0)
+      for (unsigned d = 0; d < shift; ++d) p = p.dbl();
+    F* o = out + ((size_t)k * n + i) * 4;
+    o[0] = p.x;
+    o[1] = p.y;
+    o[2] = p.zz;
+    o[3] = p.zzz;
   }
 }
 
@@ -2071,9 +2104,12 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // shared bases (run_batch: batch_ MSMs of n / batch_ points each, MSM g's
   // windows g Ws .. g Ws + Ws - 1 in the key space)
   const unsigned Ws = plan.active(), Wt = plan.windows, wr0 = plan.w_begin, B = plan.buckets, c = plan.c;
-  const unsigned W = Ws * batch_;
+  // (a fold: Wt / fold_ key windows over fold_ copies of the bases, run_windows checked it)
+  const unsigned W = (fold_ > 1 ? Wt / fold_ : Ws) * batch_;
+  const uint32_t fold_w = fold_ > 1 ? Wt / fold_ : 0u;
   const uint32_t glen = batch_ > 1 ? (uint32_t)(n / batch_) : 0u;
   const uint32_t gstep = batch_distinct_ ? 0u : glen;  // shared bases (run_batch) or one array per MSM (run_groups)
+  const uint32_t fold_n = gstep ? glen : (uint32_t)n;   // points per fold copy
   const size_t entries = n * Ws;
   const size_t nb = (size_t)W * B;
   if (n >= (size_t(1) << 31)) throw std::runtime_error("tachyon_mi355x: MSM size must be < 2^31 per device");
@@ -2188,7 +2224,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     uint32_t* btotal = bcpre + (size_t)bchunks * 256;
     hipLaunchKernelGGL(recode_hist_kernel<Fr>, dim3(nblocks), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
                        Wt, wr0, Ws, nblocks, spt, later_places, hist, later, reinterpret_cast<uint4*>(bucket_sum),
-                       nb * slot / 16, glen, gstep);
+                       nb * slot / 16, glen, gstep, fold_w, fold_n);
     TA_HIP(hipGetLastError());
     if (later_places > 0) {
       digit_off = digit_cnt + 2 * 256;
@@ -2216,10 +2252,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       scatter_lds_set_[narrow ? 1 : 0] = true;
     }
     hipLaunchKernelGGL(scatter, dim3(nblocks), dim3(kBlock), scatter_lds, stream_, d_scalars, (uint32_t)n, c, Wt, wr0,
-                       Ws, nblocks, spt, hist, hoff, dst, glen, gstep);
+                       Ws, nblocks, spt, hist, hoff, dst, glen, gstep, fold_w, fold_n);
   } else {
     hipLaunchKernelGGL(recode_kernel<Fr>, dim3(grid_for(n)), dim3(kBlock), 0, stream_, d_scalars, (uint32_t)n, c,
-                       Wt, wr0, Ws, ents, glen, gstep);
+                       Wt, wr0, Ws, ents, glen, gstep, fold_w, fold_n);
   }
   TA_HIP(hipGetLastError());
   // every bucket without an entry stays the identity (the fused recode clears them)
@@ -2691,7 +2727,10 @@ void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n
   pair_acc_ = !(variant_ & 32768);
   pair_inline_ = !(variant_ & 65536);
   if (plan_out) *plan_out = plan;
-  const unsigned nwin = plan.active() * batch_;  // window sums (per MSM of a batch, run_batch)
+  if (fold_ > 1 && (plan.w_begin != 0 || plan.w_end != plan.windows || plan.windows % fold_ != 0))
+    throw std::runtime_error("tachyon_mi355x: an MSM fold must divide the plan's window count (all windows)");
+  // window sums (per MSM of a batch, run_batch; W / fold of a folded run)
+  const unsigned nwin = (fold_ > 1 ? plan.windows / fold_ : plan.active()) * batch_;
   out->assign(nwin, Point::zero());
   if (n == 0 || plan.active() == 0) return;
   if (profile_) TA_HIP(hipEventRecord(ev_[0], stream_));
@@ -3021,6 +3060,70 @@ const typename MsmGpu<Curve>::Aff* MsmGpu<Curve>::affine_bases(const void* bases
   return out;
 }
 
+template <class Curve>
+unsigned MsmGpu<Curve>::plan_windows(size_t n) const {
+  return MsmPlan::make(n, Fr::Config::kModulusBits, force_c_).windows;
+}
+
+// The fold table of n device-resident bases: copy k = 2^(k c W / fold) P for
+// the plan of n points (forced c or the size's default), fold x n affine
+// points into `out` (device).
+template <class Curve>
+void MsmGpu<Curve>::fold_bases(const void* bases, size_t n, unsigned fold, void* out) {
+  fold_bases_c(bases, n, fold, out, MsmPlan::make(n, Fr::Config::kModulusBits, force_c_).c);
+}
+
+// ... for run_groups_folded / run_batch_folded: count x len bases (the group
+// arrays back to back), the window bits of a batch of len-point MSMs
+template <class Curve>
+void MsmGpu<Curve>::fold_bases_groups(const void* bases, size_t len, size_t count, unsigned fold, void* out) {
+  fold_bases_c(bases, len * count, fold, out, batch_window_bits(len));
+}
+
+template <class Curve>
+void MsmGpu<Curve>::fold_bases_c(const void* bases, size_t n, unsigned fold, void* out, unsigned c) {
+  require_gpu();
+  if (!is_device_pointer(bases) || !is_device_pointer(out))
+    throw std::runtime_error("tachyon_mi355x: fold_bases takes device-resident bases and output");
+  const MsmPlan plan = MsmPlan::make(n, Fr::Config::kModulusBits, c);
+  if (fold < 1 || plan.windows % fold != 0)
+    throw std::runtime_error("tachyon_mi355x: an MSM fold must divide the plan's window count");
+  if (n == 0) return;
+  const unsigned shift = plan.c * (plan.windows / fold);
+  const size_t total = (size_t)fold * n;
+  F* xyzz = static_cast<F*>(norm_in_.ensure(total * 4 * sizeof(F)));
+  F* prefix = static_cast<F*>(norm_prefix_.ensure(total * sizeof(F)));
+  hipLaunchKernelGGL(detail::fold_points_kernel<F>, dim3(ceil_div(n, detail::kBlock)), dim3(detail::kBlock), 0,
+                     stream_, static_cast<const Aff*>(bases), n, fold, shift, xyzz);
+  constexpr uint32_t kChunk = 16;
+  hipLaunchKernelGGL(detail::points_to_affine_kernel<F>, dim3(ceil_div(ceil_div(total, kChunk), detail::kBlock)),
+                     dim3(detail::kBlock), 0, stream_, xyzz, 3, static_cast<Aff*>(out), prefix, total, kChunk);
+  TA_HIP(hipGetLastError());
+  TA_HIP(hipStreamSynchronize(stream_));
+}
+
+// The MSM of n scalars over a fold table (fold_bases of the same n, same
+// window bits): W / fold window sums instead of W.
+template <class Curve>
+typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_folded(const void* folded_bases, const void* scalars, size_t n,
+                                                        unsigned fold) {
+  last_divisions_ = 1;
+  if (fold <= 1) return run(folded_bases, scalars, n);
+  if (!is_device_pointer(folded_bases) || !is_device_pointer(scalars))
+    throw std::runtime_error("tachyon_mi355x: a folded MSM takes device-resident bases and scalars");
+  if (memory_divisions(n, 0) != 1)
+    throw std::runtime_error("tachyon_mi355x: a folded MSM must fit the device in one piece");
+  struct Reset {
+    unsigned& f;
+    ~Reset() { f = 1; }
+  } reset{fold_};
+  fold_ = fold;
+  std::vector<Point> ws;
+  MsmPlan plan;
+  run_windows(folded_bases, scalars, n, &ws, &plan);
+  return combine_windows(ws, plan.c);
+}
+
 // `count` MSMs over the same `len` device-resident bases in one recode, sort,
 // accumulation and reduction: MSM g's scalars are scalars[g len, (g+1) len)
 // (device or host; zero scalars pad shorter ones), its windows a block of
@@ -3069,15 +3172,28 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_groups(const void*
   return run_batch_impl(bases, scalars, len, count, true);
 }
 
+// run_groups over a fold table of the count x len bases (fold_bases_groups)
+template <class Curve>
+std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_groups_folded(const void* folded_bases,
+                                                                            const void* scalars, size_t len,
+                                                                            size_t count, unsigned fold) {
+  if (!is_device_pointer(folded_bases))
+    throw std::runtime_error("tachyon_mi355x: a folded MSM takes a device-resident fold table");
+  return run_batch_impl(folded_bases, scalars, len, count, true, fold);
+}
+
 template <class Curve>
 std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch_impl(const void* bases, const void* scalars,
-                                                                         size_t len, size_t count, bool distinct) {
+                                                                         size_t len, size_t count, bool distinct,
+                                                                         unsigned fold) {
   std::vector<Point> res(count, Point::zero());
   if (count == 0 || len == 0) return res;
-  if (count == 1) {
+  if (count == 1 && fold <= 1) {
     res[0] = run(bases, scalars, len);
     return res;
   }
+  if (fold > 1 && !is_device_pointer(scalars))
+    throw std::runtime_error("tachyon_mi355x: a folded MSM batch takes device-resident scalars");
   if (!is_device_pointer(bases)) throw std::runtime_error("tachyon_mi355x: run_batch needs device-resident bases");
   const size_t total = len * count;
   if (total >= (size_t(1) << 31) || count > 4096)
@@ -3090,18 +3206,20 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch_impl(const v
       m->batch_ = 1;
       m->batch_distinct_ = false;
       m->force_c_ = c;
+      m->fold_ = 1;
     }
   } reset{this, force_c_};
   force_c_ = batch_window_bits(len);
   batch_distinct_ = distinct;
   batch_ = (unsigned)count;
+  fold_ = std::max(1u, fold);
   last_divisions_ = 1;
   std::vector<Point> ws;
   MsmPlan plan;
   run_windows(bases, scalars, total, &ws, &plan);
   // each MSM's Horner combination of its windows on the host (W c doublings
   // apiece), spread over a few host threads for larger batches
-  const unsigned Ws = plan.active();
+  const unsigned Ws = fold_ > 1 ? plan.windows / fold_ : plan.active();  // window sums per MSM
   auto combine = [&](size_t g0, size_t g1) {
     for (size_t g = g0; g < g1; ++g) {
       std::vector<Point> one(ws.begin() + g * Ws, ws.begin() + (g + 1) * Ws);

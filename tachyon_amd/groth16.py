@@ -149,8 +149,10 @@ class Groth16Prover:
             raise ValueError(f"device ids out of range: {ids}")
 
     def set_variant(self, variant: int):
-        """A/B: 1 = A and the witness + h MSM as two MSMs (round 4), 0 = one
-        grouped MSM (default); same proof."""
+        """A/B: bit 0 = A and the witness + h MSM as two MSMs (round 4), clear =
+        one grouped MSM (default); bits 1-3 = the G2 B query's fold table,
+        bits 4-6 the grouped G1 MSM's (0 = the default, B2 16 copies and G1 4;
+        k = 1..5: up to 2^(k-1) copies, 1 = none); same proof."""
         if not lib().tachyon_mi355x_groth16_set_variant(self._h, variant):
             raise ValueError(f"unknown Groth16 variant {variant}")
 

@@ -109,6 +109,31 @@ class VariableBaseMSMGpu:
         del ks
         return [out.raw[g * self.point_bytes:(g + 1) * self.point_bytes] for g in range(count)]
 
+    def plan_windows(self, n: int) -> int:
+        """W of the plan for n points under this context's window bits."""
+        return lib().tachyon_mi355x_msm_gpu_plan_windows(self.curve_id, self._ctx, n)
+
+    def fold_bases(self, d_bases, n: int, fold: int, d_out):
+        """Fixed-base table for run_folded: `fold` x n affine points into the
+        device buffer d_out, copy k = 2^(k c W / fold) P_i (device tensors or
+        pointers) -- tachyon_mi355x_msm_gpu_fold_bases."""
+        pb = d_bases if isinstance(d_bases, int) else d_bases.data_ptr()
+        po = d_out if isinstance(d_out, int) else d_out.data_ptr()
+        if not isinstance(d_out, int) and d_out.numel() * d_out.element_size() < fold * n * self.point_bytes:
+            raise ValueError("d_out shorter than fold x n points")
+        if not lib().tachyon_mi355x_msm_gpu_fold_bases(self.curve_id, self._ctx, pb, n, fold, po):
+            raise ValueError(f"fold {fold} refused (must divide W = {self.plan_windows(n)}; device arrays only)")
+
+    def run_folded(self, d_folded, d_scalars, n: int, fold: int) -> bytes:
+        """The MSM of n device scalars over a fold_bases table (same n, same
+        window bits); affine bytes -- tachyon_mi355x_msm_gpu_folded_affine."""
+        pb = d_folded if isinstance(d_folded, int) else d_folded.data_ptr()
+        ps = d_scalars if isinstance(d_scalars, int) else d_scalars.data_ptr()
+        out = ctypes.create_string_buffer(self.point_bytes)
+        if not lib().tachyon_mi355x_msm_gpu_folded_affine(self.curve_id, self._ctx, pb, ps, n, fold, out):
+            raise ValueError(f"fold {fold} refused (must divide W = {self.plan_windows(n)}; device arrays only)")
+        return out.raw
+
     def run_window_range(self, bases, scalars, w_begin: int, w_end: int, n=None) -> bytes:
         """The windows [w_begin, w_end) of the MSM only: sum_w 2^(c w) S_w
         (affine).  Ranges tiling [0, W) add up to run(); see

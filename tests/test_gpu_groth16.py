@@ -73,6 +73,12 @@ def test_synthetic_parity(curve, log_n, num_public, seed):
     # default grouped MSM: the same proofs; then forced window bits
     prover.set_variant(1)
     assert list(prover.prove(fb)) == list(OG.prove(zk, full, h=h))
+    # the fixed-base fold tables of the G2 B MSM (variant bits 1-3) and the
+    # grouped G1 MSM (bits 4-6): none (18), two copies each (36), B2 sixteen
+    # and G1 eight (74); the default is B2 eight, G1 four (where they divide W)
+    for v in (18, 36, 74):
+        prover.set_variant(v)
+        assert list(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == want_zk, v
     prover.set_variant(0)
     prover.set_msm_window_bits(5, 6, 7)
     assert list(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == want_zk
@@ -119,6 +125,9 @@ def test_configs4_size_parity():
     assert tuple(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == tuple(OG.prove_np(zkey, full, r, s))
     prover.set_variant(1)  # the round-4 separate A and witness + h MSMs: the same proof
     assert tuple(prover.prove(fb)) == tuple(OG.prove_np(zkey, full))
+    for v in (18, 36, 74):  # fold tables off, two copies each, B2 x16 + G1 x8 (default: B2 x8, G1 x4)
+        prover.set_variant(v)
+        assert tuple(prover.prove(fb)) == tuple(OG.prove_np(zkey, full)), v
     prover.close()
 
 
