@@ -122,6 +122,10 @@ class Groth16Prover {
 
  private:
   static unsigned fold_of(unsigned sel, unsigned dflt) { return sel == 0 ? dflt : 1u << (sel - 1); }
+  struct FoldTable;
+  template <class G>
+  XYZZ<typename G::F> fixed_msm(msm::MsmGpu<G>& msm, FoldTable& tab, const Affine<typename G::F>* bases,
+                                const Fr* scalars, size_t len, unsigned fold, unsigned c);
   void init_device_state();
   void build_groups();
   Key key_;  // host copy: verifying-key points and the query heads used on the host
@@ -137,9 +141,15 @@ class Groth16Prover {
   std::unique_ptr<msm::MsmGpu<G1>> msm1_;
   std::unique_ptr<msm::MsmGpu<G2>> msm2_;
   DeviceBuffer a1_, b1_, lh1_, b2_;              // query points (lh1 = C1 | H1)
-  DeviceBuffer b2_fold_;                         // the G2 B query's fold table (built on first use)
-  size_t b2_fold_lo_ = 0, b2_fold_len_ = 0;      // ... over b2 + 1 + [lo, lo + len)
-  unsigned b2_fold_f_ = 0, b2_fold_c_ = 0;       // ... its fold and window bits (0: none built)
+  // fold tables of the fixed queries (built on first use): the table, and
+  // the bases / length / fold / window bits it was built for (fold 0: none)
+  struct FoldTable {
+    DeviceBuffer buf;
+    const void* src = nullptr;
+    size_t len = 0;
+    unsigned fold = 0, c = 0;
+  };
+  FoldTable b2_tab_, a_tab_, b1_tab_, lh_tab_;   // G2 B; A, B in G1, witness + h (ungrouped / shards)
   DeviceBuffer g1_fold_;                         // the grouped G1 MSM's fold table (gbases_, first use)
   unsigned g1_fold_f_ = 0, g1_fold_c_ = 0;
   DeviceBuffer lh_;                              // scalars of the merged MSM: witness | h

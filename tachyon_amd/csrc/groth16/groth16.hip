@@ -368,6 +368,30 @@ void Groth16Prover<G1, G2>::witness_map(const Fr* d_full, Fr* d_h) {
   if (d_h != abc) TA_HIP(hipMemcpyAsync(d_h, abc, n_ * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
 }
 
+// An MSM over fixed proving-key bases (the caller set the window bits c):
+// over a fold table of `fold` copies (MsmGpu::fold_bases, the largest power
+// of two up to `fold` dividing the plan's W), built on first use and kept
+// while the bases, length and window bits stay; a plain MSM for fold 1.
+template <class G1, class G2>
+template <class G>
+XYZZ<typename G::F> Groth16Prover<G1, G2>::fixed_msm(msm::MsmGpu<G>& msm, FoldTable& tab,
+                                                     const Affine<typename G::F>* bases, const Fr* scalars,
+                                                     size_t len, unsigned fold, unsigned c) {
+  if (len == 0) return XYZZ<typename G::F>::zero();
+  while (fold > 1 && msm.plan_windows(len) % fold != 0) fold >>= 1;
+  if (fold <= 1) return msm.run(bases, scalars, len);
+  if (tab.fold != fold || tab.c != c || tab.src != bases || tab.len != len) {
+    tab.fold = 0;
+    void* t = tab.buf.ensure((size_t)fold * len * sizeof(Affine<typename G::F>));
+    msm.fold_bases(bases, len, fold, t);
+    tab.fold = fold;
+    tab.c = c;
+    tab.src = bases;
+    tab.len = len;
+  }
+  return msm.run_folded(tab.buf.template as<void>(), scalars, len, fold);
+}
+
 template <class G1, class G2>
 ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t count, bool with_b1, uint32_t rank,
                                                       uint32_t world) {
@@ -430,26 +454,9 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
       auto tb = Clock::now();
       msm2_->set_force_window_bits(c_b2_);
       // the B2 query is fixed: a fold table (built once per shard / window
-      // bits, the first proof's cost) halves the G2 window sums and their
+      // bits, the first proof's cost) shrinks the G2 window sums and their
       // host Horner on the proof's critical path
-      // (the largest power of two up to the chosen fold that divides W)
-      unsigned fold = b2_fold();
-      if (q_len)
-        while (fold > 1 && msm2_->plan_windows(q_len) % fold != 0) fold >>= 1;
-      if (q_len && fold > 1) {
-        if (b2_fold_f_ != fold || b2_fold_c_ != c_b2_ || b2_fold_lo_ != q_lo || b2_fold_len_ != q_len) {
-          b2_fold_f_ = 0;
-          void* tab = b2_fold_.ensure((size_t)fold * q_len * sizeof(Affine<F2>));
-          msm2_->fold_bases(b2 + 1 + q_lo, q_len, fold, tab);
-          b2_fold_f_ = fold;
-          b2_fold_c_ = c_b2_;
-          b2_fold_lo_ = q_lo;
-          b2_fold_len_ = q_len;
-        }
-        acc_b2 = msm2_->run_folded(b2_fold_.as<Affine<F2>>(), d_full + 1 + q_lo, q_len, fold);
-      } else if (q_len) {
-        acc_b2 = msm2_->run(b2 + 1 + q_lo, d_full + 1 + q_lo, q_len);
-      }
+      acc_b2 = fixed_msm(*msm2_, b2_tab_, b2 + 1 + q_lo, d_full + 1 + q_lo, q_len, b2_fold(), c_b2_);
       timings_.msm_b2 = ms_since(tb);
     } catch (...) {
       g2_error = std::current_exception();
@@ -502,12 +509,13 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     }
     out.a = r[0];
     out.lh = r[1] + r[2];
-  } else {
-    out.a = q_len ? msm1_->run(a1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
+  } else {  // (the multi-rank shards, and variant bit 0: fold tables per MSM)
+    out.a = fixed_msm(*msm1_, a_tab_, a1 + 1 + q_lo, d_full + 1 + q_lo, q_len, g1_fold(), c_a_);
   }
   timings_.msm_a = ms_since(t2);
   t2 = Clock::now();
-  out.b1 = (with_b1 && q_len) ? msm1_->run(b1 + 1 + q_lo, d_full + 1 + q_lo, q_len) : P1::zero();
+  out.b1 = with_b1 ? fixed_msm(*msm1_, b1_tab_, b1 + 1 + q_lo, d_full + 1 + q_lo, q_len, g1_fold(), c_a_)
+                   : P1::zero();
   timings_.msm_b1 = ms_since(t2);
   t2 = Clock::now();
   // witness (l) and h MSMs merged; h_coefficients.size() == h_g1_query.size()
@@ -516,7 +524,7 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     size_t lh_lo = 0;
     const size_t lh_len = shard(nw + n_, &lh_lo);
     msm1_->set_force_window_bits(c_lh_);
-    out.lh = lh_len ? msm1_->run(lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len) : P1::zero();
+    out.lh = fixed_msm(*msm1_, lh_tab_, lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len, g1_fold(), c_lh_);
   }
   timings_.msm_l = grouped ? 0.f : ms_since(t2);
   timings_.msm_h = 0;
