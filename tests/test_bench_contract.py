@@ -16,7 +16,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def newest_bench_line():
     # newest round tag first (file mtimes are the checkout's); the 1-GPU
     # default-run lines only (multi-rank rehearsals carry no CPU baseline)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line*.json")))
+    import re
+
+    def order(f):  # run order: r05z < r05aa < r05ab (as bench.pmc_traffic)
+        m = re.fullmatch(r"r(\d+)([a-z]*)", os.path.basename(os.path.dirname(f)))
+        return (int(m.group(1)), len(m.group(2)), m.group(2), f) if m else (-1, 0, "", f)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bench_line*.json")), key=order)
     if not files:
         pytest.skip("no committed bench line")
     for path in reversed(files):
@@ -54,3 +60,18 @@ def test_bench_cli_parses_without_gpu():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], capture_output=True, text=True,
                          timeout=120)
     assert out.returncode == 0 and "--gpus" in out.stdout and "--steps" in out.stdout
+
+
+def test_pmc_traffic_takes_the_newest_run(tmp_path, monkeypatch):
+    """bench.pmc_traffic reads the newest committed profile in run order
+    (r05z < r05aa < r05ab: spreadsheet-column suffixes), not the
+    lexicographically last directory."""
+    import json
+    import bench
+    for run, gb in (("r05y", 1.0), ("r05z", 2.0), ("r05ab", 3.0), ("r04zz", 9.0)):
+        d = tmp_path / "profiles" / run
+        d.mkdir(parents=True)
+        (d / "pmc_traffic.json").write_text(json.dumps({"k": {"traffic_bytes": gb * 1e9}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    traffic, src, _ = bench.pmc_traffic("k")
+    assert traffic == 3.0 and src.endswith("r05ab/pmc_traffic.json")
