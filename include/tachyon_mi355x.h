@@ -467,8 +467,9 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ct
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule).
  * Every accepted variant computes the same MSM; returns 0 (nothing changed)
- * for bits outside 0xFFFFBF (bits 0-23 but 6; bit 23: two-level window sums
- * for the G2 / BLS12-381 G1 / FIPS reductions, measured slower). */
+ * for bits outside 0x1FFFFBF (bits 0-24 but 6; bit 23: two-level window sums
+ * for the G2 / BLS12-381 G1 / FIPS reductions, measured slower; bit 24: the
+ * G2 window segment sums in two passes). */
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
  * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total,

@@ -28,7 +28,7 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0xFFFFBF;  // bits 0-23 except 6 (21: a debug check, not a schedule)
+constexpr int kMsmVariantMask = 0x1FFFFBF;  // bits 0-24 except 6 (21: a debug check, not a schedule)
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
@@ -221,11 +221,12 @@ class MsmGpu {
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
   // kernel-variant bits for in-process A/B tuning (0 = default)
-  // A/B tuning knobs (bits 0-5, 7-20 and 22 -- the FIPS reductions instead of
-  // the limb-field ones; see run_windows) and bit 21, a debug
-  // check (the small-MSM chain flags vs the accumulation's).  Every variant
-  // computes the same MSM; bit 6 (once a wrong-result gather-locality
-  // experiment) and anything above bit 22 are refused.
+  // A/B tuning knobs (bits 0-5, 7-20, 22 -- the FIPS reductions instead of
+  // the limb-field ones; see run_windows --, 23 two-level and 24 two-pass
+  // window sums) and bit 21, a debug check (the small-MSM chain flags vs the
+  // accumulation's).  Every variant computes the same MSM; bit 6 (once a
+  // wrong-result gather-locality experiment) and anything above bit 24 are
+  // refused.
   void set_variant(int v) {
     if (v < 0 || (v & ~kMsmVariantMask)) throw std::runtime_error("tachyon_mi355x: unknown MSM variant bits");
     variant_ = v;
@@ -290,6 +291,7 @@ class MsmGpu {
   hipEvent_t copy_done_ = nullptr;
   std::vector<hipEvent_t> chunk_ev_;  // host-resident pipeline: chunk k uploaded
   DeviceBuffer hist_;
+  DeviceBuffer rsum_;  // the two-pass G2 window sums' suffix sums (set_variant bit 24)
   DeviceBuffer norm_in_, norm_out_, norm_prefix_;  // affine_bases
   DeviceBuffer maxlen_, lofs_;  // lofs_: every join level's output offsets
   uint32_t* h_max_ = nullptr;  // pinned read-back of the largest bucket

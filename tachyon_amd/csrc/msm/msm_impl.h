@@ -1706,6 +1706,67 @@ __global__ __launch_bounds__(kBlock, 2) void window_combine_pair_kernel(const XY
   Ar::store(reinterpret_cast<Fb*>(out), t, h, Ar::add(x, Ar::small_mul(y, m, h != 0), h != 0));
 }
 
+// The window segment sums in two passes (G2 lane pairs, set_variant bit 24):
+// window_segment_pair_kernel holds R, the running sum and a loaded bucket
+// (three G2 points, ~540 VGPRs of state for BLS12-381, spilled at the
+// two-wave cap).  Pass 1 keeps R and the loaded bucket only and stores every
+// suffix sum R_k = sum_{k' >= k} B_{j L + k'} of its segment; pass 2 sums a
+// segment's stored R_k (the running sum's value), pass 3 adds the (j L) R_0
+// fix-up -- the same segment sums, with two points live in each loop.
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, 2) void window_rsum_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+                                                                  unsigned W, unsigned B, unsigned L,
+                                                                  XYZZ<typename Curve::F>* __restrict__ rs) {
+  using Fb = typename Ar::Fb;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t S = B / L;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W * S) return;
+  const uint32_t w = t / S, j = t - w * S;
+  const Fb* bs = reinterpret_cast<const Fb*>(bucket_sum);
+  Fb* out = reinterpret_cast<Fb*>(rs);
+  const size_t b0 = (size_t)w * B + (size_t)j * L;
+  typename Ar::A R = Ar::zero(h != 0);
+  for (int k = (int)L - 1; k >= 0; --k) {
+    R = Ar::add(R, Ar::load(bs, b0 + k, h), h != 0);
+    Ar::store(out, b0 + k, h, R);
+  }
+}
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, 2) void window_rsum_total_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ rs,
+                                                                        unsigned W, unsigned B, unsigned L,
+                                                                        XYZZ<typename Curve::F>* __restrict__ out) {
+  using Fb = typename Ar::Fb;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t S = B / L;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W * S) return;
+  const uint32_t w = t / S, j = t - w * S;
+  const Fb* src = reinterpret_cast<const Fb*>(rs);
+  const size_t b0 = (size_t)w * B + (size_t)j * L;
+  typename Ar::A acc = Ar::load(src, b0, h);
+  for (uint32_t k = 1; k < L; ++k) acc = Ar::add(acc, Ar::load(src, b0 + k, h), h != 0);
+  Ar::store(reinterpret_cast<Fb*>(out), t, h, acc);
+}
+// pass 3: the (j L) R_0 fix-ups, out[t] += (j L) rs[segment start] (apart,
+// so the summing loop above keeps the scalar multiplication's registers free)
+template <class Curve, class Ar>
+__global__ __launch_bounds__(kBlock, 2) void window_rsum_fix_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ rs,
+                                                                      unsigned W, unsigned B, unsigned L,
+                                                                      XYZZ<typename Curve::F>* __restrict__ out) {
+  using Fb = typename Ar::Fb;
+  const uint32_t h = threadIdx.x & 1u;
+  const uint32_t S = B / L;
+  const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) >> 1;
+  if (t >= W * S) return;
+  const uint32_t w = t / S, j = t - w * S;
+  if (j == 0) return;  // (both lanes of the pair)
+  const typename Ar::A fix = Ar::small_mul(Ar::load(reinterpret_cast<const Fb*>(rs), (size_t)w * B + (size_t)j * L, h),
+                                           j * L, h != 0);
+  Fb* o = reinterpret_cast<Fb*>(out);
+  Ar::store(o, t, h, Ar::add(Ar::load(o, t, h), fix, h != 0));
+}
+
 template <class Curve, class Ar = FipsPairArith<Curve>>
 __global__ __launch_bounds__(kBlock, 2) void reduce_uniform_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ in,
                                                                      unsigned W, unsigned S_in, unsigned K2,
@@ -2394,6 +2455,7 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   auto* seg_reduce = &seg_reduce_kernel<Curve>;
   auto* win_segment = &window_segment_kernel<Curve>;
   auto* win_reduce = &reduce_uniform_kernel<Curve>;
+  decltype(win_segment) rsum_pass1 = nullptr, rsum_pass2 = nullptr, rsum_fix = nullptr;  // G2 two-pass sums (bit 24)
   if constexpr (kG2) {
     if (pair_reduce) {
       using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
@@ -2401,10 +2463,16 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
         seg_reduce = &seg_reduce_pair_kernel<Curve, LimbPairArith<LimbPol>>;
         win_segment = &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol>>;
         win_reduce = &reduce_uniform_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        rsum_pass1 = &window_rsum_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        rsum_pass2 = &window_rsum_total_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        rsum_fix = &window_rsum_fix_pair_kernel<Curve, LimbPairArith<LimbPol>>;
       } else {
         seg_reduce = &seg_reduce_pair_kernel<Curve>;
         win_segment = &window_segment_pair_kernel<Curve>;
         win_reduce = &reduce_uniform_pair_kernel<Curve>;
+        rsum_pass1 = &window_rsum_pair_kernel<Curve, FipsPairArith<Curve>>;
+        rsum_pass2 = &window_rsum_total_pair_kernel<Curve, FipsPairArith<Curve>>;
+        rsum_fix = &window_rsum_fix_pair_kernel<Curve, FipsPairArith<Curve>>;
       }
     }
   }
@@ -2647,8 +2715,18 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   }
   Point* seg_a = static_cast<Point*>(seg_a_.ensure((size_t)W * S * sizeof(Point)));
   Point* seg_b = static_cast<Point*>(seg_b_.ensure((size_t)W * S * sizeof(Point)));
-  hipLaunchKernelGGL(win_segment, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, bucket_sum, W, B,
-                     plan.seg, seg_a);
+  if (rsum_pass1 && (variant_ & (1 << 24))) {  // the two-pass segment sums (G2 lane pairs, A/B)
+    Point* rs = static_cast<Point*>(rsum_.ensure((size_t)W * B * sizeof(Point)));
+    hipLaunchKernelGGL(rsum_pass1, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, bucket_sum, W, B,
+                       plan.seg, rs);
+    hipLaunchKernelGGL(rsum_pass2, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, rs, W, B, plan.seg,
+                       seg_a);
+    hipLaunchKernelGGL(rsum_fix, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, rs, W, B, plan.seg,
+                       seg_a);
+  } else {
+    hipLaunchKernelGGL(win_segment, dim3(grid_for(lanes * (size_t)W * S)), dim3(kBlock), 0, stream_, bucket_sum, W, B,
+                       plan.seg, seg_a);
+  }
   TA_HIP(hipGetLastError());
   Point* s_cur = seg_a;
   Point* s_nxt = seg_b;
@@ -3100,6 +3178,9 @@ void MsmGpu<Curve>::fold_bases_c(const void* bases, size_t n, unsigned fold, voi
                      dim3(detail::kBlock), 0, stream_, xyzz, 3, static_cast<Aff*>(out), prefix, total, kChunk);
   TA_HIP(hipGetLastError());
   TA_HIP(hipStreamSynchronize(stream_));
+  // a one-time build: its XYZZ staging (4 x the table) is not kept
+  norm_in_.release();
+  norm_prefix_.release();
 }
 
 // The MSM of n scalars over a fold table (fold_bases of the same n, same

@@ -66,7 +66,8 @@ def test_msm_golden_bn254_g1_variants(variant):
                                            ("bls12_381_g2", 0),
                                            ("bls12_381_g2", 32768), ("bls12_381_g2", 65536 | (1 << 20)),
                                            ("bls12_381_g2", 1 << 20), ("bn254_g2", 1 << 23),
-                                           ("bls12_381_g2", 1 << 23)])
+                                           ("bls12_381_g2", 1 << 23), ("bn254_g2", 1 << 24),
+                                           ("bls12_381_g2", 1 << 24), ("bls12_381_g2", (1 << 24) | (1 << 22))])
 def test_msm_golden_g2_lane_pair(curve, variant):
     """The G2 accumulations and reductions: a lane pair per point over the
     limb fields (the default: BN254 9 x 29-bit, BLS12-381 14 x 28-bit), the
@@ -395,7 +396,7 @@ def test_msm_schedule_variants_agree(curve, logn):
                     assert s["acc28"] == limb, (hex(v), s)
                 else:  # BN254 G2: the pair over 29-bit limbs; bit 20 the FIPS pair
                     assert s["acc29"] == limb, (hex(v), s)
-        for bad in (64, 1 << 24):
+        for bad in (64, 1 << 25):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
     finally:
@@ -427,7 +428,8 @@ def _neg_point(curve, p: bytes) -> bytes:
                                            ("bls12_381_g2", 0), ("bls12_381_g2", 1 << 22),
                                            ("bls12_381_g2", 32768), ("bls12_381_g1", 1 << 23),
                                            ("bls12_381_g2", 1 << 23), ("bn254_g2", 1 << 23),
-                                           ("bn254_g1", 262144 | (1 << 23))])
+                                           ("bn254_g1", 262144 | (1 << 23)), ("bn254_g2", 1 << 24),
+                                           ("bls12_381_g2", 1 << 24)])
 def test_msm_reduction_edge_cases(curve, variant):
     """Inputs that drive the chain join and the window sums through their
     special cases: every base the same point (equal bucket pieces and equal
