@@ -2760,6 +2760,16 @@ template <class Curve>
 void MsmGpu<Curve>::run_windows(const void* bases, const void* scalars, size_t n, std::vector<Point>* out,
                                 MsmPlan* plan_out) {
   MsmPlan plan = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_, range_begin_, range_end_);
+  // G2: running-sum segments twice the G1 rule's length -- a G2 fix-up costs
+  // more against the latency-bound loop (BLS12-381 G2 2^24 reduction 13.7 ->
+  // 13.0 ms at L = 128, BN254 G2 2^22 1.75 -> 1.64 ms at L = 32;
+  // profiles/r05am, r05an)
+  if constexpr (std::is_same_v<Curve, Bn254G2> || std::is_same_v<Curve, Bls381G2>) {
+#ifdef TACHYON_TUNING_KNOBS
+    if (!getenv("TACHYON_MSM_SEG"))
+#endif
+      plan.seg = std::min(plan.buckets, std::min(128u, plan.seg * 2));
+  }
   switch (variant_ & 3) {  // accumulation chunk experiments
     case 1: plan.K = std::min(2048u, plan.K * 2); break;
     case 2: plan.K = std::min(2048u, plan.K * 4); break;
