@@ -97,7 +97,7 @@ def parse():
                     help="N > 1 MSM partition: point shards (default), or window ranges with every rank holding "
                          "all points (c = 16: W = 16 windows; measured slower per rank, tools/split_probe.py), or "
                          "hybrid: N / Q point groups x Q window groups (--window-groups; c = --window-bits or 19); "
-                         "auto (default): the hybrid where HYBRID_PLANS has a plan for (curve, N), else points")
+                         "auto (default): the library's plan (tachyon_mi355x_msm_shard_plan), hybrid or points")
     ap.add_argument("--window-groups", type=int, default=2, help="Q of --msm-split hybrid")
     ap.add_argument("--no-sweep", action="store_true",
                     help="skip the configs[1]/[2] size sweeps (profiling runs: one MSM and one NTT size only)")
@@ -223,9 +223,9 @@ def synth_groth16_zkey(log_n, seed=SEED):
     return b"".join(parts), full
 
 
-def bench_bls(args, rank, world, barrier, dist, backend):
+def bench_bls(args, rank, world, barrier, dist, backend, lib_comm=None):
     """BLS12-381 G1 and G2 MSMs at 2^k (BASELINE configs[3]): each rank's share
-    of one global input (point shards, or the hybrid of HYBRID_PLANS) + the
+    of one global input (the library's partition: point shards or the hybrid) + the
     all-gather of partials, device-resident inputs, as the headline."""
     import torch
     from tachyon_amd import dist as D
@@ -234,7 +234,7 @@ def bench_bls(args, rank, world, barrier, dist, backend):
     n_total = 1 << args.bls_log_n
     parts = {}
     for curve, pb in (("bls12_381_g1", 96), ("bls12_381_g2", 192)):
-        split, start, n, wrange, split_c, p_groups, q_groups = msm_partition(args, curve, world, rank, n_total)
+        split, start, n, wrange, split_c, p_groups, q_groups, shard = msm_partition(args, curve, world, rank, n_total)
         parts[curve] = (split if split != "hybrid" else f"hybrid {p_groups} point groups x {q_groups} window groups, "
                         f"c = {split_c}")
         d_b = torch.empty(max(1, n) * pb, dtype=torch.uint8, device="cuda")
@@ -252,6 +252,8 @@ def bench_bls(args, rank, world, barrier, dist, backend):
             return msm.run(d_b, d_s, n)
 
         def step():
+            if lib_comm is not None and shard is not None:  # the library's sharded entry (as the headline)
+                return msm.run_sharded_plan(lib_comm, shard, d_b, d_s)
             return D.sharded_msm(curve, local_run, device="cuda")
 
         ref = step()
@@ -269,6 +271,8 @@ def bench_bls(args, rank, world, barrier, dist, backend):
         leg = out[curve.split("_")[-1]] = {"ms_per_msm": dt * 1e3, "scalars_per_s": n_total / dt,
                                            "consistent": res == ref, "points_per_gpu": n,
                                            "partition": parts[curve] if world > 1 else "single GPU"}
+        if world == 1:
+            leg.update(msm_rooflines(msm, curve, d_b, d_s, n, pb))
         if world == 1 and not args.no_sweep:
             # the per-rank shards of this MSM at N = 2, 4, 8 (prefixes of the same input) and the
             # point-shard projection built on them
@@ -283,7 +287,7 @@ def bench_bls(args, rank, world, barrier, dist, backend):
                 sw[str(k)] = {"ms": round(sorted(ts)[1] * 1e3, 3), "scalars_per_s": (1 << k) / sorted(ts)[1]}
             leg["shard_sweep"] = sw
             hybrid = {str(w): hybrid_rank_ms(msm, curve, d_b, d_s, n_total, w)
-                      for w in (2, 4, 8) if (curve, w) in HYBRID_PLANS}
+                      for w in (2, 4, 8) if hybrid_plan(curve, w)}
             leg["projected_scaling"] = project_msm_scaling(curve, args.bls_log_n, sw, hybrid)
         msm.close()
         if world == 1 and not args.no_cpu_baseline:
@@ -302,6 +306,68 @@ def bench_bls(args, rank, world, barrier, dist, backend):
                        f"device-resident inputs" + (f", {world} ranks (partition per curve) + all-gather of partials"
                                                     if world > 1 else ""))
     return out
+
+
+# the in-register madd ceiling's field per curve (tachyon_mi355x_msm_madd_ceiling):
+# BN254 G1 29-bit limbs, BLS12-381 G1 28-bit, the G2 lane pairs over the same limbs
+CEILING_FIELD = {"bn254_g1": 29, "bls12_381_g1": 28, "bn254_g2": 29, "bls12_381_g2": 28}
+
+
+def acc_kernel_name(curve, schedule):
+    """The accumulation kernel the last run launched (rocprofv3's short name)."""
+    if schedule["acc29"]:
+        return "seg_acc29_kernel"
+    if schedule["acc28"]:
+        return "seg_acc28_kernel"
+    if schedule["lane_pair"]:
+        return "seg_acc_pair_limb_kernel"
+    return "seg_acc_kernel"
+
+
+def msm_rooflines(msm, curve, d_b, d_s, n, point_bytes, reps=3):
+    """HBM and VALU rooflines of an MSM's bucket accumulation (the dominant
+    kernel), as the headline's: achieved = n x (affine base + 32-B scalar)
+    algorithmic bytes / the kernel's HIP-event time; VALU = n x W mixed
+    additions / that time against the in-register madd ceiling of the same
+    field code measured in this run; traffic from the newest committed PMC
+    passes that profiled this kernel (profiles/*/pmc_traffic.json)."""
+    from tachyon_amd import msm as M
+    msm.set_profile(True)
+    prof = []
+    for _ in range(reps):
+        msm.run(d_b, d_s, n)
+        prof.append(msm.last_timings())
+    msm.set_profile(False)
+    launches = max(1, int(prof[0]["acc_launches"]))
+    acc_ms = sorted(p["acc"] for p in prof)[len(prof) // 2] / launches
+    kernel = acc_kernel_name(curve, msm.last_schedule())
+    c, windows = M.plan(curve, n)
+    if msm.window_bits:
+        from tachyon_amd import dist as D
+        c, windows = msm.window_bits, D._windows_for(curve, msm.window_bits)
+    algo = n / launches * (point_bytes + 32)
+    gbs = algo / (acc_ms * 1e-3) / 1e9
+    traffic, src, raw = pmc_traffic(kernel)
+    gmadd = n * windows / launches / (acc_ms * 1e-3) / 1e9
+    try:
+        peak = msm.madd_ceiling(CEILING_FIELD[curve])
+        peak_src = "measured in this run"
+    except Exception as e:  # noqa: BLE001 -- a diagnostic
+        peak, peak_src = 0.0, f"not measured ({e})"
+    return {
+        "phase_ms": {k: round(sorted(p[k] for p in prof)[len(prof) // 2], 4) for k in prof[0]},
+        "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_unit": "GB per launch", "traffic_source": src,
+                     "traffic_fetch_raw": raw, "kernel": kernel, "kernel_ms": acc_ms,
+                     "algorithmic_bytes_per_launch": algo,
+                     "note": f"n x ({point_bytes} B affine base + 32 B scalar) per launch / the accumulation's "
+                             f"HIP-event time (SURVEY 8(d)'s per-point bytes for this group)"},
+        "valu_roofline": {"bound": "valu", "kernel": kernel, "achieved": gmadd, "peak": peak,
+                          "peak_source": peak_src, "unit": "G mixed additions/s",
+                          "frac": (gmadd / peak) if peak else None, "window_bits": c, "windows": windows,
+                          "note": "n x W mixed additions per launch / the launch's time; peak = the same field "
+                                  "code's madd chain in registers (no gathers, no run logic), whole chip, this box"},
+    }
 
 
 def stream_copy_gbs(nbytes=1 << 31, reps=5):
@@ -354,51 +420,87 @@ def full_msm_equals(curve, n_total, sharded, rank, dist):
 # all-gather latency; both are ASSUMPTIONS (no multi-GPU box here), every other
 # term of a projection is measured in this run.
 XGMI_LINK_GBS = 76.0
-# --msm-split auto: (curve, N) -> (window groups Q, window bits c) of the hybrid
-# partition (N/Q point groups x Q window groups), point shards elsewhere.  The
-# slowest rank on one MI355X (tools/split_probe.py --hybrid): BN254 2^26 at N =
-# 8 11.45 ms vs 12.11 for the 2^23 point shard, N = 4 21.45 vs 21.40 (points
-# kept) (profiles/r05c/hybrid_split_probe.jsonl); BLS12-381 2^24 G2 N = 4
-# 31.16 vs 32.19, N = 8 17.21 vs 17.81 (profiles/r05m/), and again in the
-# bench projections of three boxes (r05p/r05r/r05z: G2 hybrid 1-5 % faster);
-# BLS12-381 G1's hybrid (P2 x Q2 c = 19 at 4, P4 x Q2 c = 16 at 8) came out
-# within noise of the point shard there (-2 .. +4 %), so G1 keeps point shards
-HYBRID_PLANS = {("bn254_g1", 8): (2, 19),
-                ("bls12_381_g2", 4): (2, 19), ("bls12_381_g2", 8): (4, 16)}
+def hybrid_plan(curve, world):
+    """(window groups Q, window bits c) of the hybrid point x window partition
+    the LIBRARY runs for (curve, world) -- tachyon_mi355x_msm_shard_plan, the
+    table of measured plans in capi.hip (BN254 G1 at 8 ranks, BLS12-381 G2 at
+    4 and 8) -- or None where it keeps point shards."""
+    from tachyon_amd import msm as M
+    s = M.shard_plan(curve, 1 << 20, world, 0)
+    return (s.window_groups, s.window_bits) if s.window_groups > 1 else None
+
+
+def hybrid_plans():
+    """{(curve, N): (Q, c)} of hybrid_plan over the curves and N = 2, 4, 8."""
+    out = {}
+    for curve in ("bn254_g1", "bn254_g2", "bls12_381_g1", "bls12_381_g2"):
+        for world in (2, 4, 8):
+            h = hybrid_plan(curve, world)
+            if h:
+                out[(curve, world)] = h
+    return out
 
 
 def msm_partition(args, curve, world, rank, n_total):
     """This rank's share of the MSM: (split, start, count, window range or None,
-    c or 0, point groups, window groups) -- point shards, the window split or
-    the hybrid (auto: HYBRID_PLANS)."""
+    c or 0, point groups, window groups, shard) -- auto: the library's plan
+    (tachyon_mi355x_msm_shard_plan: point shards or the hybrid); forced point
+    shards / hybrid (--window-groups, --window-bits) / window split.  `shard`
+    is the tachyon_mi355x_msm_shard the library's sharded entry takes (None for
+    the window split, which combines in Python)."""
     from tachyon_amd import dist as D
+    from tachyon_amd import msm as M
+    from tachyon_amd._lib import MsmShard
     split = args.msm_split
-    q, c = HYBRID_PLANS.get((curve, world), (0, 0))
-    if split == "auto":
-        split = "hybrid" if q else "points"
-    elif split == "hybrid":  # forced: --window-groups, --window-bits (else the table's or 19)
-        q, c = args.window_groups, args.window_bits or c or 19
     if world == 1:
         split = "points"
+    if split == "auto":
+        s = M.shard_plan(curve, n_total, world, rank)
+        if s.window_groups > 1:
+            return ("hybrid", s.start, s.count, (s.w_begin, s.w_end), s.window_bits, s.point_groups,
+                    s.window_groups, s)
+        return "points", s.start, s.count, None, 0, world, 1, s
     if split == "points":
         start, n = D.shard_range(n_total, rank, world)
-        return split, start, n, None, 0, world, 1
+        return split, start, n, None, 0, world, 1, MsmShard(start, n, world, 1, 0, 0, 0)
     if split == "windows":
         c = args.window_bits or 16
-        return split, 0, n_total, D.window_range(D._windows_for(curve, c), rank, world), c, 1, world
+        return split, 0, n_total, D.window_range(D._windows_for(curve, c), rank, world), c, 1, world, None
+    q, c = args.window_groups, args.window_bits or (hybrid_plan(curve, world) or (0, 19))[1]
     q = max(1, min(q, world))
     p = world // q
     if p * q != world:
         raise SystemExit("--window-groups must divide the world size")
     start, n = D.shard_range(n_total, rank // q, p)
-    return split, start, n, D.window_range(D._windows_for(curve, c), rank % q, q), c, p, q
+    w0, w1 = D.window_range(D._windows_for(curve, c), rank % q, q)
+    return split, start, n, (w0, w1), c, p, q, MsmShard(start, n, p, q, c, w0, w1)
+
+
+def lib_communicator(world, backend):
+    """The library communicator the multi-rank legs exchange through
+    (TACHYON_BENCH_COMM): rccl (default with the nccl backend) -- the
+    library's own RCCL communicator over xGMI; host (default under gloo) --
+    host-staged through this process group's collectives; torch -- none (the
+    Python combine, tachyon_amd.dist).  Returns (LibComm or None, label)."""
+    from tachyon_amd import dist as D
+    if world == 1:
+        return None, "single GPU"
+    kind = os.environ.get("TACHYON_BENCH_COMM", "rccl" if backend == "nccl" else "host")
+    if kind == "torch":
+        return None, "torch.distributed (Python combine)"
+    if kind == "rccl" and backend == "nccl":
+        try:
+            return D.LibComm.rccl(), "library rccl communicator"
+        except Exception as e:  # noqa: BLE001 -- recorded in the line, the host-staged one stands in
+            return D.LibComm.from_process_group(), f"library host-staged communicator (rccl init failed: {e})"
+    return D.LibComm.from_process_group(), "library host-staged communicator"
 
 
 def hybrid_rank_ms(msm, curve, d_bases, d_scalars, n_total, world, reps=3):
-    """The slowest rank of HYBRID_PLANS[(curve, world)] on this GPU: n/P points
+    """The slowest rank of hybrid_plan(curve, world) on this GPU: n/P points
     (a prefix of this run's input) over the first ceil(W/Q) c-bit windows."""
     from tachyon_amd import dist as D
-    q, c = HYBRID_PLANS[(curve, world)]
+    q, c = hybrid_plan(curve, world)
     m = n_total // (world // q)
     w1 = -(-D._windows_for(curve, c) // q)
     prev = getattr(msm, "window_bits", 0)
@@ -443,7 +545,7 @@ def combine_cost_ms(curve, world, reps=20):
 def project_msm_scaling(curve, log_n, sweep, hybrid=None):
     """Projection of the 2^log_n MSM onto N = 2, 4, 8 GPUs from THIS run's
     single-GPU times: point shards (the 2^(log_n - log N) entries of the
-    sweep, prefixes of the same input) or, where HYBRID_PLANS has a plan for
+    sweep, prefixes of the same input) or, where hybrid_plan has a plan for
     (curve, N), the hybrid partition's slowest rank (`hybrid[N]`, measured
     by hybrid_rank_ms) -- the partition --msm-split auto runs; per rank T +
     the combine (host side measured here + the assumed RCCL all-gather
@@ -459,9 +561,10 @@ def project_msm_scaling(curve, log_n, sweep, hybrid=None):
         comb = combine_cost_ms(curve, world) + RCCL_SMALL_ALLGATHER_MS
         t_points = sweep[key]["ms"]
         t_hybrid = (hybrid or {}).get(str(world))
-        use_hybrid = t_hybrid is not None and (curve, world) in HYBRID_PLANS
+        plan = hybrid_plan(curve, world)
+        use_hybrid = t_hybrid is not None and plan is not None
         t = (t_hybrid if use_hybrid else t_points) + comb
-        q, c = HYBRID_PLANS.get((curve, world), (0, 0))
+        q, c = plan or (0, 0)
         out[f"n{world}"] = {"shard_log_n": log_n - lg_world, "shard_ms": t_points,
                             "hybrid_rank_ms": t_hybrid,
                             "plan": f"hybrid {world // q} point groups x {q} window groups, c = {c}"
@@ -521,7 +624,7 @@ def project_ntt_scaling(log_n, t1_ms, reps=20):
     return out
 
 
-def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backend=None):
+def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backend=None, lib_comm=None):
     """Groth16 prove (witness map + 4 G1 MSMs + 1 G2 MSM, NoZK) on a synthetic
     2^k-constraint key; the witness is host memory as in prover_main.cc.  With
     N ranks (BASELINE configs[4] "1 and 8 GPUs") every rank runs the witness
@@ -533,14 +636,22 @@ def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backen
     zkey, full = synth_groth16_zkey(args.groth16_log_n)
     prover = Groth16Prover(zkey)
     setup_s = time.perf_counter() - t0
+    # the proving key's setup step: the fold tables of this rank's shard of the
+    # fixed queries (memory-aware, tachyon_mi355x_groth16_prepare), timed apart
+    t_fold = time.perf_counter()
+    fold_bytes = prover.prepare(rank, world)
+    fold_setup_s = time.perf_counter() - t_fold
+    folds = prover.folds()
 
     def step():
         if world == 1:
             return prover.prove(full)
+        if lib_comm is not None:  # partials, all-gather and assembly inside the library
+            return prover.prove_sharded(full, comm=lib_comm)
         return prover.prove_sharded(full, device="cuda" if backend == "nccl" else None)
 
     t_first = time.perf_counter()
-    ref = step()  # (builds the fold tables of the fixed G2 B and grouped G1 queries)
+    ref = step()
     first_ms = (time.perf_counter() - t_first) * 1e3
     step()  # a second untimed proof: the first timed one still ran ~0.7 ms slow after one (profiles/r05k)
     reps = max(2, min(args.steps, 5))
@@ -574,16 +685,60 @@ def bench_groth16(args, rank=0, world=1, barrier=lambda: None, dist=None, backen
            "constraints": 1 << args.groth16_log_n,
            "num_vars": prover.num_vars,
            "mode": "NoZK, host-resident witness, device-resident proving key with fixed-base fold tables "
-                   "(16 copies of the G2 B query, 4 of the grouped G1 ones, built by the first, untimed proof)",
+                   "built in the key's setup step (prepare: up to 16 copies of the G2 B query and 4 of the "
+                   "grouped G1 ones, as the device memory allows)",
            "first_proof_ms": round(first_ms, 1),
+           "fold_setup_s": round(fold_setup_s, 3), "fold_table_bytes": fold_bytes, "folds": folds,
            "consistent": proof == ref, "equals_cpu_oracle": equals_oracle, "phase_ms": phases,
            "setup_s": round(setup_s, 1),
            "workload": f"synthetic circom zkey, 2^{args.groth16_log_n} constraints, 2+2 A/B terms per row "
                        f"(BASELINE configs[4] shape; seeded points, no trapdoor)"}
+    if world == 1:
+        out["msm_rooflines"] = groth16_msm_rooflines(prover, phases)
     if world > 1:
         out["consistent_with_1gpu"] = consistent_1gpu
         out["mode"] += f"; witness map on every rank, MSM point shards x{world} + one all-gather of partials"
     prover.close()
+    return out
+
+
+def groth16_msm_rooflines(prover, phases):
+    """Per-MSM rooflines of one profiled proof (phase times are whole MSMs:
+    recode, sort, accumulation and reduction on the host clock): the B-in-G2
+    MSM over num_vars - 1 points (128 B base + 32 B scalar) and the grouped
+    G1 MSM (A over num_vars - 1 points + the merged witness + h MSM over
+    num_witness + n points, 64 + 32 B each); VALU = points x W mixed
+    additions / the phase time against the madd ceilings of the same fields."""
+    from tachyon_amd import msm as M
+    m, npub, n = prover.num_vars, prover.num_public, prover.domain_size
+    q = m - 1
+    nlh = (m - npub - 1) + n
+    out = {}
+    for key, curve, points, pbytes, ms, lg_len in (
+            ("b2_g2", "bn254_g2", q, 128, phases.get("msm_b2", 0.0), None),
+            ("a_lh_g1_grouped", "bn254_g1", q + nlh, 64, phases.get("msm_a", 0.0), max(q, (nlh + 1) // 2))):
+        if not ms or points <= 0:
+            continue
+        if lg_len is None:
+            c, W = M.plan(curve, points)
+        else:  # run_groups' window bits (MsmGpu::batch_window_bits) over glen-point groups
+            lg = max(1, (lg_len - 1).bit_length())
+            c = max(M.plan(curve, lg_len)[0], min(lg + 1, 8) if lg <= 13 else 10)
+            W = -(-255 // c)
+        gbs = points * (pbytes + 32) / (ms * 1e-3) / 1e9
+        gmadd = points * W / (ms * 1e-3) / 1e9
+        ctx = M.VariableBaseMSMGpu(curve)
+        try:
+            peak = ctx.madd_ceiling(CEILING_FIELD[curve])
+        finally:
+            ctx.close()
+        out[key] = {"points": points, "ms": ms, "window_bits": c, "windows": W,
+                    "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": gbs / HBM_PEAK_GBS},
+                    "valu_roofline": {"bound": "valu", "achieved": gmadd, "peak": peak,
+                                      "unit": "G mixed additions/s", "frac": gmadd / peak if peak else None}}
+    out["note"] = ("whole-MSM phase times of one profiled proof (host clock; the fold tables cut the window "
+                   "sums, not the n x W additions), so these fractions sit below the accumulation kernel's own")
     return out
 
 
@@ -626,10 +781,11 @@ def main():
     # W = 16 windows) -- per-rank cost at 2^26 / 8 ranks 14.4 vs 16.2 ms: the
     # split's recode of all n scalars per rank and its 2 x 2^26 additions
     # (vs 15 x 2^23 at the shard's c = 17) outweigh the smaller bucket set.
-    # The hybrid (N/Q point groups x Q window groups, HYBRID_PLANS) sits
+    # The hybrid (N/Q point groups x Q window groups, hybrid_plan) sits
     # between: 2^24 points over 7 of 14 windows per rank at N = 8, 11.45 vs
     # 12.11 ms for the point shard (profiles/r05c), so auto runs it at 8 GPUs
-    split, start, n, wrange, split_c, p_groups, q_groups = msm_partition(args, "bn254_g1", world, rank, n_total)
+    split, start, n, wrange, split_c, p_groups, q_groups, shard = msm_partition(args, "bn254_g1", world, rank,
+                                                                                   n_total)
     d_bases = torch.empty(max(1, n) * 64, dtype=torch.uint8, device="cuda")
     d_scalars = torch.empty(max(1, n) * 32, dtype=torch.uint8, device="cuda")
     chunk = 1 << 10
@@ -650,24 +806,19 @@ def main():
             return msm.run_window_range(d_bases, d_scalars, w_lo, w_hi, n)
         return msm.run(d_bases, d_scalars, n)
 
-    # N > 1 point shards: the library's sharded entry (local partial, all-gather,
-    # group sum in rank order inside libtachyon_mi355x) over a communicator:
-    # TACHYON_BENCH_COMM=host (default) -- the host-staged one whose exchange is
-    # this process group's collective (torch.distributed over RCCL / gloo);
-    # rccl -- the library's own RCCL communicator; torch -- the Python
-    # combine (tachyon_amd.dist.sharded_msm)
-    comm_kind = os.environ.get("TACHYON_BENCH_COMM", "host")
-    lib_comm = None
-    if world > 1 and split == "points" and comm_kind != "torch":
-        lib_comm = D.LibComm.rccl() if (comm_kind == "rccl" and backend == "nccl") else D.LibComm.from_process_group()
+    # N > 1: the library's sharded entry over a library communicator -- this
+    # rank's part of the partition (point shard or hybrid point group x window
+    # range), the all-gather of the partials and their group sum inside
+    # libtachyon_mi355x (tachyon_mi355x_msm_gpu_sharded_plan_affine); RCCL by
+    # default (lib_communicator); the window split and TACHYON_BENCH_COMM=torch
+    # combine in Python (tachyon_amd.dist)
+    lib_comm, comm_label = lib_communicator(world, backend)
 
     def step():
         if split == "windows":
             return D.window_split_msm("bn254_g1", msm, d_bases, d_scalars, n, split_c, device="cuda")
-        if split == "hybrid":  # every (point group, window range) partial, summed on every rank
-            return D.sharded_msm("bn254_g1", local_run, device="cuda")
         if lib_comm is not None:
-            return msm.run_sharded(lib_comm, d_bases, d_scalars, n)
+            return msm.run_sharded_plan(lib_comm, shard, d_bases, d_scalars)
         return D.sharded_msm("bn254_g1", local_run, device="cuda")
 
     for _ in range(args.warmup):
@@ -746,8 +897,9 @@ def main():
                                    f"msm point groups x{p_groups} x window groups x{q_groups} ({rank_windows} of "
                                    f"{windows} windows per rank) + RCCL all-gather of partial points"
                                    if split == "hybrid" else
-                                   f"msm point shards x{world} + RCCL all-gather of partial points"
-                                   + (f" (inside the library, {lib_comm.backend} communicator)" if lib_comm else ""))},
+                                   f"msm point shards x{world} + RCCL all-gather of partial points")
+                                  + (f"; exchange: {comm_label}" if world > 1 else ""),
+                   "communicator": (lib_comm.backend if lib_comm else comm_label)},
         "consistent_across_steps": consistent,
         "consistent_with_1gpu": consistent_1gpu,
         "roofline": {"bound": "hbm", "achieved": acc_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -793,10 +945,10 @@ def main():
             sweep[str(k)] = {"ms": round(best * 1e3, 3), "scalars_per_s": m / best}
         sweep[str(args.log_n)] = {"ms": round(ms_per_step, 3), "scalars_per_s": value}
         out["msm_sweep"] = sweep
-        # the hybrid partition's slowest rank where auto runs it (HYBRID_PLANS:
-        # N = 8, 4 point groups x 2 window groups at c = 19)
+        # the hybrid partition's slowest rank where auto runs it (the library's
+        # plan: N = 8, 4 point groups x 2 window groups at c = 19)
         hybrid = {str(w): hybrid_rank_ms(msm, "bn254_g1", d_bases, d_scalars, 1 << args.log_n, w)
-                  for w in (2, 4, 8) if ("bn254_g1", w) in HYBRID_PLANS}
+                  for w in (2, 4, 8) if hybrid_plan("bn254_g1", w)}
         out["projected_scaling"] = {"msm": project_msm_scaling("bn254_g1", args.log_n, sweep, hybrid)}
 
     # ---- NonUniform(n, 1) test set (variable_base_msm_test_set.h:43-53), the set of the reference's
@@ -808,7 +960,14 @@ def main():
         d_nu = one.repeat(max(1, n))
         torch.cuda.synchronize()
 
-        def nu_step():
+        def nu_step():  # the same partition and exchange as the headline step
+            if split == "windows":
+                return D.window_split_msm("bn254_g1", msm, d_bases, d_nu, n, split_c, device="cuda")
+            if lib_comm is not None:
+                return msm.run_sharded_plan(lib_comm, shard, d_bases, d_nu)
+            if split == "hybrid":
+                return D.sharded_msm("bn254_g1", lambda: msm.run_window_range(d_bases, d_nu, w_lo, w_hi, n),
+                                     device="cuda")
             return D.sharded_msm("bn254_g1", lambda: msm.run(d_bases, d_nu, n), device="cuda")
 
         nu_ref = nu_step()
@@ -890,13 +1049,22 @@ def main():
         M.gen_scalars("bn254_fr", SEED + 1, m, x.data_ptr(), start=rank * m)
         torch.cuda.synchronize()
         orig = x.clone()
+        y = torch.empty_like(x)
+
+        def round_trip(x):
+            if lib_comm is not None:  # stage 1, the all-to-all, stage 2 inside the library (tachyon_mi355x_bn254_ntt4_run)
+                plan.run(lib_comm, x, y)
+                plan.run(lib_comm, y, x, inverse=True)
+                return x
+            return D.sharded_ntt(plan, D.sharded_ntt(plan, x), inverse=True)
+
         for _ in range(2):
-            x = D.sharded_ntt(plan, D.sharded_ntt(plan, x), inverse=True)
+            x = round_trip(x)
         reps = max(2, args.steps)
         barrier()
         t0 = time.perf_counter()
         for _ in range(reps):
-            x = D.sharded_ntt(plan, D.sharded_ntt(plan, x), inverse=True)
+            x = round_trip(x)
         barrier()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
                          device="cuda" if backend == "nccl" else "cpu")
@@ -908,8 +1076,8 @@ def main():
         nn = 1 << args.ntt_log_n
         out["ntt"] = {"value": nn / dt, "unit": "elems/s", "log_n": args.ntt_log_n, "ms_per_transform": dt * 1e3,
                       "round_trip_ok": bool(ok.item()), "scaling": "strong",
-                      "mode": f"four-step sharded x{world}: local R/C-point NTTs (R = 2^{plan.log_r}) + one RCCL "
-                              f"all-to-all ({nn * 32 // world // world} B per rank pair)"}
+                      "mode": f"four-step sharded x{world}: local R/C-point NTTs (R = 2^{plan.log_r}) + one "
+                              f"all-to-all ({nn * 32 // world // world} B per rank pair); exchange: {comm_label}"}
         plan.close()
 
     if not args.no_ntt and world == 1:
@@ -1037,10 +1205,10 @@ def main():
         out["ntt"]["sweep"] = nsweep
 
     if args.bls_log_n:
-        out["bls12_381"] = bench_bls(args, rank, world, barrier, dist, backend)
+        out["bls12_381"] = bench_bls(args, rank, world, barrier, dist, backend, lib_comm)
 
     if args.groth16_log_n:
-        out["groth16"] = bench_groth16(args, rank, world, barrier, dist, backend)
+        out["groth16"] = bench_groth16(args, rank, world, barrier, dist, backend, lib_comm)
 
     h_bases = h_scalars = None
     if world == 1 and not (args.no_host_resident and args.no_cpu_baseline):
@@ -1071,6 +1239,8 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     msm.close()
+    if lib_comm is not None:
+        lib_comm.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -330,6 +330,34 @@ TACHYON_C_EXPORT void* tachyon_mi355x_bn254_ntt4_stream(const tachyon_mi355x_bn2
  * values. */
 TACHYON_C_EXPORT int tachyon_mi355x_bn254_ntt4_set_variant(tachyon_mi355x_bn254_ntt4* plan, int variant);
 
+/* ---- field-generic radix-2 NTT domains --------------------------------------
+ * Radix2EvaluationDomain<F> FFT / IFFT on the GPU for the scalar fields the
+ * reference's icicle backend covers: field 1 = bn254 Fr (IcicleNTT<bn254::Fr>,
+ * icicle_ntt_bn254.cc:31-116), 3 = bls12_381 Fr (IcicleNTT<bls12_381::Fr>,
+ * icicle_ntt_bls12_381.cc:31-115).  Elements are the field's 4 x uint64
+ * Montgomery limbs (tachyon_bn254_fr / tachyon_bls12_381_fr).  size =
+ * bit_ceil(num_coeffs); the root is the field's two-adic root squared down
+ * (bn254 Fr: the generator set active at creation, halo2 override included).
+ * _set_offset: the coset h * <w> of later transforms (NULL or 1 = the plain
+ * domain; GetCoset, univariate_evaluation_domain.h:102-117).
+ * _transform_host: IcicleNTT::Run -- in place on a host vector of exactly
+ * size() elements, natural order, forward (coefficients -> evaluations) or
+ * inverse (n^-1 and the coset included); synchronous.  _transform_device:
+ * `batch` consecutive device arrays in place, enqueued on _stream.  Returns
+ * NULL from _create for another field id; failures abort. */
+typedef struct tachyon_mi355x_ntt_domain tachyon_mi355x_ntt_domain;
+TACHYON_C_EXPORT tachyon_mi355x_ntt_domain* tachyon_mi355x_ntt_domain_create(int field, size_t num_coeffs);
+TACHYON_C_EXPORT void tachyon_mi355x_ntt_domain_destroy(tachyon_mi355x_ntt_domain* d);
+TACHYON_C_EXPORT size_t tachyon_mi355x_ntt_domain_size(const tachyon_mi355x_ntt_domain* d);
+TACHYON_C_EXPORT int tachyon_mi355x_ntt_domain_field(const tachyon_mi355x_ntt_domain* d);
+TACHYON_C_EXPORT void tachyon_mi355x_ntt_domain_group_gen(const tachyon_mi355x_ntt_domain* d, void* out);
+TACHYON_C_EXPORT void tachyon_mi355x_ntt_domain_set_offset(tachyon_mi355x_ntt_domain* d, const void* offset);
+TACHYON_C_EXPORT void tachyon_mi355x_ntt_domain_transform_host(tachyon_mi355x_ntt_domain* d, void* inout, size_t len,
+                                                              int inverse);
+TACHYON_C_EXPORT void tachyon_mi355x_ntt_domain_transform_device(tachyon_mi355x_ntt_domain* d, void* d_data,
+                                                                size_t batch, int inverse);
+TACHYON_C_EXPORT void* tachyon_mi355x_ntt_domain_stream(tachyon_mi355x_ntt_domain* d);
+
 /* ---- communicators and library-level sharded entry points ------------------
  * One process per MI355X: a multi-process C/C++ caller (benchmark/msm/
  * msm_benchmark_gpu.cc:57-69 or vendors/circom/prover_main.cc:116-128 under a
@@ -460,6 +488,31 @@ TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_run(int curve, void* ctx, const void
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_sharded_affine(int curve, void* ctx, tachyon_mi355x_comm* comm,
                                                            const void* bases, const void* scalars, size_t size,
                                                            void* out_affine);
+/* The partition of an n_total-point MSM over `world` ranks that this library
+ * runs fastest (measured on MI355X): point shards, or the
+ * hybrid of P = world / Q point groups x Q window groups -- rank r takes
+ * point group r / Q ([start, start + count) of the global input) over window
+ * range r % Q ([w_begin, w_end) of the W windows at window_bits).  Point
+ * shards: window_groups 1, window_bits 0 (the shard's own default), w_begin 0,
+ * w_end 0 (all windows).  Returns 1, or 0 for a rank outside [0, world). */
+typedef struct tachyon_mi355x_msm_shard {
+  size_t start, count;
+  unsigned point_groups, window_groups, window_bits, w_begin, w_end;
+} tachyon_mi355x_msm_shard;
+TACHYON_C_EXPORT int tachyon_mi355x_msm_shard_plan(int curve, size_t n_total, int world, int rank,
+                                                  tachyon_mi355x_msm_shard* out);
+/* _sharded_plan_affine: this rank's part of `plan` (its point group's
+ * bases / scalars, `plan->count` points, host or device) over `comm`: the
+ * windows [w_begin, w_end) at window_bits (all windows and the shard's
+ * default bits for a point shard), one all-gather of every rank's partial
+ * and their group sum -- every rank writes the whole MSM's affine result and
+ * returns 1.  A rank whose local part fails still enters the exchange with a
+ * failure flag, so no rank is left waiting in the collective: then EVERY rank
+ * returns 0 (out untouched, the message on stderr) instead of aborting. */
+TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_sharded_plan_affine(int curve, void* ctx, tachyon_mi355x_comm* comm,
+                                                                const tachyon_mi355x_msm_shard* plan,
+                                                                const void* bases, const void* scalars,
+                                                                void* out_affine);
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_run_points(int curve, void* ctx, const void* bases, size_t bases_size,
                                                       int base_form, const void* scalars, size_t scalars_size,
                                                       int form, void* out);
@@ -490,8 +543,10 @@ TACHYON_C_EXPORT unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const 
 /* Diagnostic: mixed additions per second (G/s) of the curve's bucket
  * accumulation field code in registers on the current device (no gathers, no
  * bucket runs; ~0.1 s): the VALU ceiling the bench prices the accumulation
- * against.  field_bits 29 (BN254 G1's 29-bit-limb field) or 32 (FIPS);
- * returns 0 for other curves or widths. */
+ * against.  field_bits: BN254 G1 29 (its 29-bit-limb field) or 32 (FIPS);
+ * BLS12-381 G1 28 (14 x 28-bit limbs); BN254 G2 29 / BLS12-381 G2 28 (the
+ * lane-pair Fq2 of the G2 accumulation, whole G2 additions, two lanes each);
+ * returns 0 for other widths. */
 TACHYON_C_EXPORT double tachyon_mi355x_msm_madd_ceiling(int curve, int field_bits);
 /* One process, several MI355X: every later MSM of this context splits its
  * points into `count` contiguous shards, shard k on device device_ids[k]
@@ -607,6 +662,22 @@ TACHYON_C_EXPORT void tachyon_mi355x_groth16_prove_sharded(tachyon_mi355x_groth1
                                                           void* out_c);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full,
                                                          size_t count, void* out_h);
+/* Proving-key setup (no reference counterpart: the reference keeps no
+ * per-key device state): builds the fixed-base fold tables the proofs of
+ * shard (rank, world) use -- B in G2, the grouped A + witness/h G1 MSM (one
+ * device) or A / B1 / witness+h (shards) -- each at the largest fold up to
+ * the variant's that fits the device next to the MSM's working set
+ * (TACHYON_MSM_MEM_LIMIT caps the free bytes, as for the MSM); no table
+ * (fold 1) runs plain MSMs, and a grouped MSM that does not fit runs as
+ * separate MSMs.  Proofs without it prepare themselves on first use.  After
+ * set_devices it prepares every device's prover for its entry of the split.
+ * Returns the table bytes held (summed over devices); _prover_folds writes
+ * the folds chosen by the last prepare: B2, grouped G1 (0 = separate MSMs),
+ * A, B1 (0 = not built), witness + h (0 = grouped). */
+TACHYON_C_EXPORT size_t tachyon_mi355x_groth16_prepare(tachyon_mi355x_groth16_prover* prover, uint32_t rank,
+                                                       uint32_t world, int with_b1);
+TACHYON_C_EXPORT void tachyon_mi355x_groth16_prover_folds(const tachyon_mi355x_groth16_prover* prover,
+                                                          uint32_t* out5);
 TACHYON_C_EXPORT void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on);
 /* A/B: variant bit 0 runs A and the witness + h MSM as two MSMs (round 4);
  * clear (default) as one grouped MSM over their own bases (one recode / sort

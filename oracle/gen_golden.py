@@ -98,8 +98,11 @@ def msm_cases():
     return out
 
 
-def ntt_cases():
-    F = pyref.Field("bn254_fr")
+def ntt_cases(field="bn254_fr", coset=5, two_adicity=28):
+    """Radix-2 FFT / IFFT golden vectors by pyref's O(n^2) DFT: plain and on
+    the coset `coset` * <w> (5 for BN254 Fr as the reference's GPU unittest,
+    7 = BLS12-381 Fr's BUILD subgroup generator)."""
+    F = pyref.Field(field)
     cases = []
     for logn in range(0, 8):
         n = 1 << logn
@@ -108,7 +111,7 @@ def ntt_cases():
                 continue
             seed = SEED + 1000 * logn + num_coeffs
             coeffs = pyref.gen_scalars(F, seed, num_coeffs)
-            for offset in (1, 5):
+            for offset in (1, coset):
                 ev = pyref.fft(F, coeffs, n, offset)
                 back = pyref.ifft(F, ev, n, offset)
                 assert back == coeffs + [] or back == list(coeffs[:len(back)])
@@ -119,8 +122,8 @@ def ntt_cases():
                     evals=[hx(F.to_bytes(e)) for e in ev],
                     ifft_of_evals=[hx(F.to_bytes(c)) for c in back],
                 ))
-    roots = {str(k): hx(F.to_bytes(F.root_of_unity(1 << k))) for k in range(0, 29)}
-    return dict(field="bn254_fr", two_adic_root_of_unity=str(F.root_of_unity(1 << 28)),
+    roots = {str(k): hx(F.to_bytes(F.root_of_unity(1 << k))) for k in range(0, two_adicity + 1)}
+    return dict(field=field, two_adic_root_of_unity=str(F.root_of_unity(1 << two_adicity)),
                 roots_of_unity_mont=roots, cases=cases)
 
 
@@ -222,14 +225,19 @@ def zkey_fixture(ref_root):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", default=None, help="write only this golden file (e.g. ntt_bls12_381_fr.json)")
     args = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
     outputs = {
-        "field_ops.json": field_ops(),
-        "msm.json": msm_cases(),
-        "ntt_bn254_fr.json": ntt_cases(),
+        "field_ops.json": field_ops,
+        "msm.json": msm_cases,
+        "ntt_bn254_fr.json": ntt_cases,
+        "ntt_bls12_381_fr.json": lambda: ntt_cases("bls12_381_fr", coset=7, two_adicity=32),
     }
-    if os.path.isdir(args.reference):
+    if args.only:
+        outputs = {args.only: outputs[args.only]}
+    outputs = {k: f() for k, f in outputs.items()}
+    if os.path.isdir(args.reference) and not args.only:
         outputs["zkey_multiplier_3.json"] = zkey_fixture(args.reference)
     for name, obj in outputs.items():
         with open(os.path.join(GOLDEN, name), "w") as f:

@@ -544,6 +544,14 @@ EXPORT int oracle_domain_info(int field, size_t num_coeffs, void* out3) {
     bn254_fr_domain_destroy(d);
     return 0;
   }
+  if (field == 3) {
+    bls12_381_fr_domain_t* d = bls12_381_fr_domain_create(num_coeffs);
+    if (!d) return -1;
+    bls12_381_fr_t* o = (bls12_381_fr_t*)out3;
+    o[0] = d->group_gen; o[1] = d->group_gen_inv; o[2] = d->size_inv;
+    bls12_381_fr_domain_destroy(d);
+    return 0;
+  }
   return -1;
 }
 

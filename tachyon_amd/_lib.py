@@ -29,6 +29,13 @@ vp, sz, i32, u8, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_
 fp = ctypes.POINTER(ctypes.c_float)
 # tachyon_mi355x_all_gather_fn / _all_to_all_fn: (user, send, recv, bytes) -> 0 on success
 COMM_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+
+class MsmShard(ctypes.Structure):
+    """tachyon_mi355x_msm_shard: one rank's part of a sharded MSM plan."""
+    _fields_ = [("start", ctypes.c_size_t), ("count", ctypes.c_size_t), ("point_groups", ctypes.c_uint),
+                ("window_groups", ctypes.c_uint), ("window_bits", ctypes.c_uint), ("w_begin", ctypes.c_uint),
+                ("w_end", ctypes.c_uint)]
 SIGNATURES = [
     # reference C-ABI: MSM
     ("tachyon_bn254_g1_init", None, []),
@@ -172,6 +179,16 @@ SIGNATURES = [
     ("tachyon_mi355x_kzg_commit", i32, [vp, i32, vp, sz, vp]),
     ("tachyon_mi355x_kzg_commit_batch", i32, [vp, i32, ctypes.POINTER(ctypes.c_void_p),
                                               ctypes.POINTER(ctypes.c_size_t), sz, vp]),
+    # field-generic NTT domains
+    ("tachyon_mi355x_ntt_domain_create", vp, [i32, sz]),
+    ("tachyon_mi355x_ntt_domain_destroy", None, [vp]),
+    ("tachyon_mi355x_ntt_domain_size", sz, [vp]),
+    ("tachyon_mi355x_ntt_domain_field", i32, [vp]),
+    ("tachyon_mi355x_ntt_domain_group_gen", None, [vp, vp]),
+    ("tachyon_mi355x_ntt_domain_set_offset", None, [vp, vp]),
+    ("tachyon_mi355x_ntt_domain_transform_host", None, [vp, vp, sz, i32]),
+    ("tachyon_mi355x_ntt_domain_transform_device", None, [vp, vp, sz, i32]),
+    ("tachyon_mi355x_ntt_domain_stream", vp, [vp]),
     # communicators and library-level sharded entry points
     ("tachyon_mi355x_comm_unique_id", i32, [vp, sz]),
     ("tachyon_mi355x_comm_init_rccl", vp, [vp, i32, i32]),
@@ -183,9 +200,13 @@ SIGNATURES = [
     ("tachyon_mi355x_comm_rank", i32, [vp]),
     ("tachyon_mi355x_comm_backend", ctypes.c_char_p, [vp]),
     ("tachyon_mi355x_msm_gpu_sharded_affine", None, [i32, vp, vp, vp, vp, sz, vp]),
+    ("tachyon_mi355x_msm_shard_plan", i32, [i32, sz, i32, i32, vp]),
+    ("tachyon_mi355x_msm_gpu_sharded_plan_affine", i32, [i32, vp, vp, vp, vp, vp, vp]),
     ("tachyon_mi355x_bn254_ntt4_run", None, [vp, vp, i32, vp, vp]),
     ("tachyon_mi355x_bn254_ntt4_set_variant", i32, [vp, i32]),
     ("tachyon_mi355x_groth16_prove_sharded", None, [vp, vp, vp, sz, vp, vp, vp, vp, vp]),
+    ("tachyon_mi355x_groth16_prepare", sz, [vp, ctypes.c_uint32, ctypes.c_uint32, i32]),
+    ("tachyon_mi355x_groth16_prover_folds", None, [vp, ctypes.POINTER(ctypes.c_uint32)]),
     ("tachyon_mi355x_jacobian_destroy", None, [i32, vp]),
     ("tachyon_mi355x_version", ctypes.c_char_p, []),
     ("tachyon_mi355x_device_count", i32, []),

@@ -232,14 +232,54 @@ template <class Curve>
 void msm_sharded_out(void* ctx, dist::Comm* comm, const void* bases, const void* scalars, size_t n, void* out) {
   using F = typename Curve::F;
   auto* c = static_cast<MsmCtx<Curve>*>(ctx);
-  const XYZZ<F> part = c->run(bases, scalars, n);
-  std::vector<XYZZ<F>> all((size_t)comm->world());
-  comm->all_gather_host(&part, all.data(), sizeof(part));
+  // (a rank whose local MSM fails still enters the exchange: dist::gather_checked)
+  const std::vector<XYZZ<F>> all = dist::gather_checked<XYZZ<F>>(comm, [&] {
+    if (!c) throw std::runtime_error("null MSM context");
+    return c->run(bases, scalars, n);
+  });
   XYZZ<F> acc = XYZZ<F>::zero();
   for (const auto& p : all) acc = acc + p;
   const Affine<F> a = acc.to_affine();
   memcpy(out, &a, sizeof(a));
 }
+
+// One rank's part of a tachyon_mi355x_msm_shard plan: its point group over
+// its window range (the hybrid partition; a point shard when window_groups
+// is 1), the all-gather of the XYZZ partials and their sum in rank order.
+// The window-range partials sum_{w in range} 2^(c w) S_w of the Q ranges of
+// one point group add up to that group's MSM, the groups' to the whole MSM.
+template <class Curve>
+void msm_sharded_plan_out(void* ctx, dist::Comm* comm, const tachyon_mi355x_msm_shard& p, const void* bases,
+                          const void* scalars, void* out) {
+  using F = typename Curve::F;
+  auto* c = static_cast<MsmCtx<Curve>*>(ctx);
+  const std::vector<XYZZ<F>> all = dist::gather_checked<XYZZ<F>>(comm, [&]() -> XYZZ<F> {
+    if (!c) throw std::runtime_error("null MSM context");
+    if (p.window_groups <= 1) return c->run(bases, scalars, p.count);
+    struct Restore {
+      msm::MsmGpu<Curve>& m;
+      unsigned c;
+      ~Restore() { m.set_force_window_bits(c); }
+    } restore{c->impl, c->impl.force_window_bits()};
+    c->impl.set_force_window_bits(p.window_bits);
+    return c->impl.run_window_range(bases, scalars, p.count, p.w_begin, p.w_end);
+  });
+  XYZZ<F> acc = XYZZ<F>::zero();
+  for (const auto& q : all) acc = acc + q;
+  const Affine<F> a = acc.to_affine();
+  memcpy(out, &a, sizeof(a));
+}
+
+// The hybrid point x window partitions (curve id, world) -> (window groups Q,
+// window bits c) that beat point shards on one MI355X (the slowest rank of
+// each partition timed with the real kernels: BN254 G1 2^26 at 8 ranks 11.45
+// vs 12.11 ms, profiles/r05c; BLS12-381 G2 2^24 at 4 / 8 ranks 31.16 / 17.21
+// vs 32.19 / 17.81 ms, profiles/r05m); point shards everywhere else.
+struct HybridPlan {
+  int curve, world;
+  unsigned q, c;
+};
+constexpr HybridPlan kHybridPlans[] = {{0, 8, 2, 19}, {3, 4, 2, 19}, {3, 8, 4, 16}};
 
 template <class Curve>
 void affine_sum(const void* pts, size_t count, void* out) {
@@ -461,6 +501,53 @@ void tachyon_mi355x_msm_gpu_sharded_affine(int curve, void* ctx, tachyon_mi355x_
   if (!comm || !comm->impl) throw std::runtime_error("null communicator");
   CURVE_DISPATCH(curve, msm_sharded_out<C>(ctx, comm->impl.get(), bases, scalars, size, out_affine))
   GUARD_END
+}
+int tachyon_mi355x_msm_shard_plan(int curve, size_t n_total, int world, int rank, tachyon_mi355x_msm_shard* out) {
+  if (!out || curve < 0 || curve > 3 || world < 1 || rank < 0 || rank >= world) return 0;
+  unsigned q = 1, c = 0;
+  for (const HybridPlan& h : kHybridPlans)
+    if (h.curve == curve && h.world == world) {
+      q = h.q;
+      c = h.c;
+    }
+  const unsigned p = (unsigned)world / q;
+  // point group rank / q: the ceil split of base::ParallelizeMap (dist.shard_range)
+  const size_t chunk = (n_total + p - 1) / p;
+  const size_t start = std::min<size_t>((size_t)(rank / q) * chunk, n_total);
+  tachyon_mi355x_msm_shard s{};
+  s.start = start;
+  s.count = std::min(chunk, n_total - start);
+  s.point_groups = p;
+  s.window_groups = q;
+  if (q > 1) {
+    const unsigned bits = curve < 2 ? Bn254Fr::Config::kModulusBits : Bls381Fr::Config::kModulusBits;
+    const unsigned W = (bits + 1 + c - 1) / c;
+    const unsigned base = W / q, extra = W % q, j = (unsigned)rank % q;  // contiguous ranges (dist.window_range)
+    s.window_bits = c;
+    s.w_begin = j * base + std::min(j, extra);
+    s.w_end = s.w_begin + base + (j < extra ? 1 : 0);
+  }
+  *out = s;
+  return 1;
+}
+int tachyon_mi355x_msm_gpu_sharded_plan_affine(int curve, void* ctx, tachyon_mi355x_comm* comm,
+                                               const tachyon_mi355x_msm_shard* plan, const void* bases,
+                                               const void* scalars, void* out_affine) {
+  // (no abort: a failure of any rank's local part reaches every rank through
+  // the exchange, and every rank returns 0 with the message on stderr)
+  try {
+    if (!comm || !comm->impl) throw std::runtime_error("null communicator");
+    if (!plan) throw std::runtime_error("null shard plan");
+    CURVE_DISPATCH(curve, msm_sharded_plan_out<C>(ctx, comm->impl.get(), *plan, bases, scalars, out_affine))
+    return 1;
+  } catch (const std::exception& e) {
+    fprintf(stderr, "[tachyon_mi355x] %s failed: %s\n", __func__, e.what());
+    fflush(stderr);
+  } catch (...) {
+    fprintf(stderr, "[tachyon_mi355x] %s failed: unknown exception\n", __func__);
+    fflush(stderr);
+  }
+  return 0;
 }
 int tachyon_mi355x_msm_gpu_run_points(int curve, void* ctx, const void* bases, size_t bases_size, int base_form,
                                       const void* scalars, size_t scalars_size, int form, void* out) {
@@ -1087,6 +1174,89 @@ void tachyon_mi355x_bn254_ntt4_synchronize(tachyon_mi355x_bn254_ntt4* plan) {
   GUARD_BEGIN
   TA_HIP(hipStreamSynchronize(plan->impl->stream()));
   GUARD_END
+}
+
+}  // extern "C"
+
+// ---- field-generic NTT domains (include/tachyon_mi355x.h) ----
+// Radix2EvaluationDomain<F> on the GPU for bn254 Fr (field 1) and bls12_381
+// Fr (field 3): the engine of the IcicleNTT<F> holder
+// (icicle_ntt_bls12_381.cc:31-115 for BLS12-381).
+struct tachyon_mi355x_ntt_domain {
+  int field = 0;
+  std::unique_ptr<ntt::NttDomain<Bn254Fr>> bn;
+  std::unique_ptr<ntt::NttDomain<Bls381Fr>> bls;
+};
+
+namespace {
+template <class Fn>
+void ntt_dispatch(const tachyon_mi355x_ntt_domain* d, Fn&& fn) {
+  if (d->bn) fn(*d->bn);
+  else fn(*d->bls);
+}
+}  // namespace
+
+extern "C" {
+
+tachyon_mi355x_ntt_domain* tachyon_mi355x_ntt_domain_create(int field, size_t num_coeffs) {
+  if (field != 1 && field != 3) return nullptr;
+  GUARD_BEGIN
+  auto d = std::make_unique<tachyon_mi355x_ntt_domain>();
+  d->field = field;
+  if (field == 1) d->bn = std::make_unique<ntt::NttDomain<Bn254Fr>>(num_coeffs);
+  else d->bls = std::make_unique<ntt::NttDomain<Bls381Fr>>(num_coeffs);
+  return d.release();
+  GUARD_END
+  return nullptr;
+}
+void tachyon_mi355x_ntt_domain_destroy(tachyon_mi355x_ntt_domain* d) { delete d; }
+size_t tachyon_mi355x_ntt_domain_size(const tachyon_mi355x_ntt_domain* d) {
+  size_t n = 0;
+  ntt_dispatch(d, [&](auto& dom) { n = dom.size(); });
+  return n;
+}
+int tachyon_mi355x_ntt_domain_field(const tachyon_mi355x_ntt_domain* d) { return d->field; }
+void tachyon_mi355x_ntt_domain_group_gen(const tachyon_mi355x_ntt_domain* d, void* out) {
+  ntt_dispatch(d, [&](auto& dom) { memcpy(out, &dom.group_gen(), sizeof(dom.group_gen())); });
+}
+void tachyon_mi355x_ntt_domain_set_offset(tachyon_mi355x_ntt_domain* d, const void* offset) {
+  GUARD_BEGIN
+  ntt_dispatch(d, [&](auto& dom) {
+    using Fr = std::decay_t<decltype(dom.group_gen())>;
+    Fr h = Fr::one();
+    if (offset) memcpy(&h, offset, sizeof(h));
+    dom.set_offset(h);
+  });
+  GUARD_END
+}
+void tachyon_mi355x_ntt_domain_transform_host(tachyon_mi355x_ntt_domain* d, void* inout, size_t len, int inverse) {
+  GUARD_BEGIN
+  ntt_dispatch(d, [&](auto& dom) {
+    using Fr = std::decay_t<decltype(dom.group_gen())>;
+    if (len != dom.size())
+      throw std::runtime_error("transform_host: the vector must hold exactly size() elements (" +
+                               std::to_string(len) + " != " + std::to_string(dom.size()) + ")");
+    auto* v = static_cast<Fr*>(inout);
+    if (inverse) dom.inverse_host(v, len, v);
+    else dom.forward_host(v, len, v);
+  });
+  GUARD_END
+}
+void tachyon_mi355x_ntt_domain_transform_device(tachyon_mi355x_ntt_domain* d, void* d_data, size_t batch,
+                                                int inverse) {
+  GUARD_BEGIN
+  ntt_dispatch(d, [&](auto& dom) {
+    using Fr = std::decay_t<decltype(dom.group_gen())>;
+    auto* x = static_cast<Fr*>(d_data);
+    if (inverse) dom.inverse_device(x, batch);
+    else dom.forward_device(x, batch);
+  });
+  GUARD_END
+}
+void* tachyon_mi355x_ntt_domain_stream(tachyon_mi355x_ntt_domain* d) {
+  void* s = nullptr;
+  ntt_dispatch(d, [&](auto& dom) { s = static_cast<void*>(dom.stream()); });
+  return s;
 }
 
 }  // extern "C"

@@ -126,9 +126,9 @@ void sharded_prove_into(P* p, dist::Comm* comm, const void* full, size_t count, 
   using Fr = typename P::Fr;
   using Parts = PartialsOf<P*>;
   const uint32_t world = (uint32_t)comm->world(), rank = (uint32_t)comm->rank();
-  const Parts mine = p->partials(static_cast<const Fr*>(full), count, r != nullptr, rank, world);
-  std::vector<Parts> all(world);
-  comm->all_gather_host(&mine, all.data(), sizeof(Parts));
+  // (a rank whose partials fail still enters the exchange: dist::gather_checked)
+  const std::vector<Parts> all = dist::gather_checked<Parts>(
+      comm, [&] { return p->partials(static_cast<const Fr*>(full), count, r != nullptr, rank, world); });
   auto proof = p->assemble(all.data(), world, static_cast<const Fr*>(r), static_cast<const Fr*>(s));
   memcpy(a, &proof.a, sizeof(proof.a));
   memcpy(b, &proof.b, sizeof(proof.b));
@@ -283,6 +283,40 @@ void tachyon_mi355x_groth16_assemble(tachyon_mi355x_groth16_prover* prover, cons
 void tachyon_mi355x_groth16_witness_map(tachyon_mi355x_groth16_prover* prover, const void* full, size_t count,
                                         void* out_h) {
   GUARD_BEGIN PROVER_DISPATCH(prover, witness_map_into(impl, full, count, out_h)); GUARD_END
+}
+
+size_t tachyon_mi355x_groth16_prepare(tachyon_mi355x_groth16_prover* prover, uint32_t rank, uint32_t world,
+                                      int with_b1) {
+  GUARD_BEGIN
+  if (!prover->devices.empty()) {  // every device prover for its entry of the one-process split
+    const size_t N = prover->devices.size();
+    int prev = 0;
+    TA_HIP(hipGetDevice(&prev));
+    size_t bytes = 0;
+    for (size_t k = 0; k < N; ++k) {
+      TA_HIP(hipSetDevice(prover->devices[k]));
+      if (prover->curve == circom::CurveId::kBn254)
+        bytes += prover->bn_dev[k]->prepare((uint32_t)k, (uint32_t)N, with_b1 != 0);
+      else
+        bytes += prover->bls_dev[k]->prepare((uint32_t)k, (uint32_t)N, with_b1 != 0);
+    }
+    TA_HIP(hipSetDevice(prev));
+    return bytes;
+  }
+  PROVER_DISPATCH(prover, return impl->prepare(rank, world, with_b1 != 0));
+  GUARD_END
+}
+
+void tachyon_mi355x_groth16_prover_folds(const tachyon_mi355x_groth16_prover* prover, uint32_t* out5) {
+  GUARD_BEGIN
+  PROVER_DISPATCH(prover, {
+    unsigned f[5];
+    if (!prover->bn_dev.empty()) prover->bn_dev[0]->last_folds(f);
+    else if (!prover->bls_dev.empty()) prover->bls_dev[0]->last_folds(f);
+    else impl->last_folds(f);
+    for (int i = 0; i < 5; ++i) out5[i] = f[i];
+  });
+  GUARD_END
 }
 
 void tachyon_mi355x_groth16_set_profile(tachyon_mi355x_groth16_prover* prover, int on) {

@@ -21,7 +21,11 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <exception>
 #include <memory>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../common/hip_util.h"
@@ -88,6 +92,41 @@ class HostComm : public Comm {
 };
 
 ncclUniqueId rccl_unique_id();
+
+// One fixed-size record per rank, gathered in rank order, with a status
+// word: `local()` computes this rank's record; if it throws, the rank still
+// enters the all-gather (with a failure flag) so that no other rank is left
+// blocked in the collective, and after the exchange EVERY rank throws when
+// any rank failed (its own error first).
+template <class T, class Fn>
+std::vector<T> gather_checked(Comm* comm, Fn&& local) {
+  struct Rec {
+    uint32_t ok = 0, rank = 0;
+    T v{};
+  };
+  static_assert(std::is_trivially_copyable_v<Rec>);
+  Rec mine;
+  mine.rank = (uint32_t)comm->rank();
+  std::exception_ptr err;
+  try {
+    mine.v = local();
+    mine.ok = 1;
+  } catch (...) {
+    err = std::current_exception();
+  }
+  std::vector<Rec> all((size_t)comm->world());
+  comm->all_gather_host(&mine, all.data(), sizeof(Rec));
+  if (err) std::rethrow_exception(err);
+  std::vector<T> out;
+  out.reserve(all.size());
+  for (const Rec& r : all) {
+    if (!r.ok)
+      throw std::runtime_error("tachyon_mi355x: rank " + std::to_string(r.rank) +
+                               " failed its local part of a sharded call");
+    out.push_back(r.v);
+  }
+  return out;
+}
 
 }  // namespace tachyon_amd::dist
 

@@ -94,6 +94,19 @@ class Groth16Prover {
   // canonical Montgomery) written to `d_h` (device) -- for parity tests.
   void witness_map(const Fr* d_full, Fr* d_h);
 
+  // Proving-key setup (the fold tables of the fixed queries, built here
+  // instead of inside the first proof): the tables the proofs of shard
+  // (rank, world) use, each the largest fold up to the variant's that fits
+  // the device next to the MSM's working set (MsmGpu::fit_fold; fold 1 =
+  // plain MSMs, and the grouped G1 MSM falls back to separate MSMs when its
+  // working set does not fit).  Returns the table bytes held afterwards.
+  // A proof after prepare() builds nothing; one without it prepares itself.
+  size_t prepare(uint32_t rank, uint32_t world, bool with_b1);
+  size_t fold_table_bytes() const;
+  // the folds the last prepare chose: B2, the grouped G1 (0 = separate
+  // MSMs), A, B1, witness + h
+  void last_folds(unsigned out[5]) const;
+
   const Key& key() const { return key_; }
   void set_profile(bool on) { profile_ = on; }
   // window bits of the proof's MSMs (0 = each MSM's default): A (and B in G1),
@@ -123,9 +136,26 @@ class Groth16Prover {
  private:
   static unsigned fold_of(unsigned sel, unsigned dflt) { return sel == 0 ? dflt : 1u << (sel - 1); }
   struct FoldTable;
+  // one rank's point ranges of the proof's MSMs, and whether A and the
+  // witness + h MSM run as one grouped MSM
+  struct ShardPlan {
+    size_t q_lo = 0, q_len = 0;    // queries 1 .. m-1 of A, B1, B2
+    size_t lh_lo = 0, lh_len = 0;  // the merged witness + h MSM (ungrouped)
+    bool grouped = false;
+  };
+  ShardPlan shard_plan(uint32_t rank, uint32_t world) const;
+  // the fold table of `tab` for these bases, (re)built when they, the length,
+  // the window bits or the fold the memory allows changed; returns its fold
+  // (1: no table, the MSM runs plain)
+  template <class G>
+  unsigned ensure_table(msm::MsmGpu<G>& msm, FoldTable& tab, const Affine<typename G::F>* bases, size_t len,
+                        unsigned fold, unsigned c);
   template <class G>
   XYZZ<typename G::F> fixed_msm(msm::MsmGpu<G>& msm, FoldTable& tab, const Affine<typename G::F>* bases,
                                 const Fr* scalars, size_t len, unsigned fold, unsigned c);
+  // the grouped G1 MSM's table (fold 1 = none); false when the grouped MSM
+  // itself does not fit the device (separate MSMs then)
+  bool ensure_group_table(unsigned* fold_out);
   void init_device_state();
   void build_groups();
   Key key_;  // host copy: verifying-key points and the query heads used on the host
@@ -147,11 +177,13 @@ class Groth16Prover {
     DeviceBuffer buf;
     const void* src = nullptr;
     size_t len = 0;
-    unsigned fold = 0, c = 0;
+    unsigned want = 0, c = 0;  // the fold asked for and the window bits of the last decision
+    unsigned fold = 0;         // the fold built (1: none fits, plain MSM; 0: not decided)
   };
   FoldTable b2_tab_, a_tab_, b1_tab_, lh_tab_;   // G2 B; A, B in G1, witness + h (ungrouped / shards)
-  DeviceBuffer g1_fold_;                         // the grouped G1 MSM's fold table (gbases_, first use)
-  unsigned g1_fold_f_ = 0, g1_fold_c_ = 0;
+  FoldTable g1_tab_;                             // the grouped G1 MSM's table (over gbases_)
+  bool group_fits_ = true;                       // the grouped G1 MSM fits the device (ensure_group_table)
+  unsigned folds_[5] = {0, 0, 0, 0, 0};          // last_folds
   DeviceBuffer lh_;                              // scalars of the merged MSM: witness | h
   DeviceBuffer row_a_, row_b_, col_, val_;       // CSR of the A and B matrices
   DeviceBuffer full_, abc_;                      // witness, 3 x n work vectors

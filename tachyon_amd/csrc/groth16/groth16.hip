@@ -368,28 +368,135 @@ void Groth16Prover<G1, G2>::witness_map(const Fr* d_full, Fr* d_h) {
   if (d_h != abc) TA_HIP(hipMemcpyAsync(d_h, abc, n_ * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
 }
 
-// An MSM over fixed proving-key bases (the caller set the window bits c):
-// over a fold table of `fold` copies (MsmGpu::fold_bases, the largest power
-// of two up to `fold` dividing the plan's W), built on first use and kept
-// while the bases, length and window bits stay; a plain MSM for fold 1.
+// The fold table of fixed proving-key bases (the caller set the window bits
+// c on `msm`): the largest power of two up to `fold` dividing the plan's W
+// whose table fits the device beside the MSM's working set
+// (MsmGpu::fit_fold), built once and kept while the bases, length, window
+// bits and requested fold stay.  Fold 1: no table (the plain MSM, which
+// splits itself into point chunks when even that does not fit).
+template <class G1, class G2>
+template <class G>
+unsigned Groth16Prover<G1, G2>::ensure_table(msm::MsmGpu<G>& msm, FoldTable& tab, const Affine<typename G::F>* bases,
+                                             size_t len, unsigned fold, unsigned c) {
+  if (len == 0) return 1;
+  if (tab.fold != 0 && tab.want == fold && tab.c == c && tab.src == bases && tab.len == len) return tab.fold;
+  const size_t old = tab.buf.capacity();
+  const unsigned f = msm.fit_fold(len, msm.plan_windows(len), fold, msm.run_bytes(len), old);
+  tab.fold = 0;
+  if (f > 1) {
+    if (old < msm::MsmGpu<G>::fold_table_bytes(len, f)) tab.buf.release();  // (free it before the larger one)
+    msm.fold_bases(bases, len, f, tab.buf.ensure(msm::MsmGpu<G>::fold_table_bytes(len, f)));
+  } else {
+    tab.buf.release();
+  }
+  tab.fold = f;
+  tab.want = fold;
+  tab.c = c;
+  tab.src = bases;
+  tab.len = len;
+  return f;
+}
+
+// An MSM over fixed proving-key bases: over their fold table (ensure_table),
+// or plain when none fits
 template <class G1, class G2>
 template <class G>
 XYZZ<typename G::F> Groth16Prover<G1, G2>::fixed_msm(msm::MsmGpu<G>& msm, FoldTable& tab,
                                                      const Affine<typename G::F>* bases, const Fr* scalars,
                                                      size_t len, unsigned fold, unsigned c) {
   if (len == 0) return XYZZ<typename G::F>::zero();
-  while (fold > 1 && msm.plan_windows(len) % fold != 0) fold >>= 1;
-  if (fold <= 1) return msm.run(bases, scalars, len);
-  if (tab.fold != fold || tab.c != c || tab.src != bases || tab.len != len) {
-    tab.fold = 0;
-    void* t = tab.buf.ensure((size_t)fold * len * sizeof(Affine<typename G::F>));
-    msm.fold_bases(bases, len, fold, t);
-    tab.fold = fold;
-    tab.c = c;
-    tab.src = bases;
-    tab.len = len;
+  const unsigned f = ensure_table(msm, tab, bases, len, fold, c);
+  if (f <= 1) return msm.run(bases, scalars, len);
+  return msm.run_folded(tab.buf.template as<void>(), scalars, len, f);
+}
+
+// The grouped A + witness/h MSM (run_groups over 3 x glen_ points): whether
+// its working set fits the device at all, and its fold table if one fits
+template <class G1, class G2>
+bool Groth16Prover<G1, G2>::ensure_group_table(unsigned* fold_out) {
+  *fold_out = 1;
+  msm1_->set_force_window_bits(c_a_);
+  const unsigned want = g1_fold();
+  FoldTable& tab = g1_tab_;
+  if (tab.fold != 0 && tab.want == want && tab.c == c_a_ && tab.len == glen_) {
+    *fold_out = tab.fold;
+    return group_fits_;
   }
-  return msm.run_folded(tab.buf.template as<void>(), scalars, len, fold);
+  const size_t run_b = msm1_->batch_run_bytes(glen_, 3);
+  const size_t old = tab.buf.capacity();
+  group_fits_ = run_b <= msm1_->device_budget() + old;
+  unsigned f = 1;
+  if (group_fits_) f = msm1_->fit_fold(3 * glen_, msm1_->batch_windows(glen_), want, run_b, old);
+  tab.fold = 0;
+  if (f > 1) {
+    const size_t bytes = msm::MsmGpu<G1>::fold_table_bytes(3 * glen_, f);
+    if (old < bytes) tab.buf.release();
+    msm1_->fold_bases_groups(gbases_.as<Affine<F1>>(), glen_, 3, f, tab.buf.ensure(bytes));
+  } else {
+    tab.buf.release();
+  }
+  tab.fold = f;
+  tab.want = want;
+  tab.c = c_a_;
+  tab.src = gbases_.as<void>();
+  tab.len = glen_;
+  *fold_out = f;
+  return group_fits_;
+}
+
+template <class G1, class G2>
+typename Groth16Prover<G1, G2>::ShardPlan Groth16Prover<G1, G2>::shard_plan(uint32_t rank, uint32_t world) const {
+  // this rank's chunk [lo, lo + len) of an MSM over `total` points
+  auto shard = [&](size_t total, size_t* lo) {
+    const size_t chunk = (total + world - 1) / world;
+    *lo = std::min<size_t>((size_t)rank * chunk, total);
+    return std::min(chunk, total - *lo);
+  };
+  ShardPlan p;
+  const size_t m = key_.num_vars;
+  p.q_len = m > 1 ? shard(m - 1, &p.q_lo) : 0;
+  p.lh_len = shard(key_.num_witness() + n_, &p.lh_lo);
+  // one process, one device: A and the witness + h MSM as ONE grouped MSM
+  // (run_groups over the padded group layout of build_groups)
+  p.grouped = world == 1 && glen_ > 0 && !(variant_ & 1);
+  return p;
+}
+
+template <class G1, class G2>
+size_t Groth16Prover<G1, G2>::prepare(uint32_t rank, uint32_t world, bool with_b1) {
+  if (world == 0 || rank >= world) throw std::runtime_error("tachyon_mi355x: Groth16 shard rank >= world");
+  ShardPlan sp = shard_plan(rank, world);
+  const Affine<F1>* a1 = a1_.as<Affine<F1>>();
+  const Affine<F1>* b1 = b1_.as<Affine<F1>>();
+  const Affine<F2>* b2 = b2_.as<Affine<F2>>();
+  msm2_->set_force_window_bits(c_b2_);
+  folds_[0] = ensure_table(*msm2_, b2_tab_, b2 + 1 + sp.q_lo, sp.q_len, b2_fold(), c_b2_);
+  folds_[1] = 0;
+  if (sp.grouped) {
+    unsigned f = 1;
+    if (ensure_group_table(&f)) folds_[1] = f;
+    else sp.grouped = false;
+  }
+  msm1_->set_force_window_bits(c_a_);
+  folds_[2] = sp.grouped ? 0 : ensure_table(*msm1_, a_tab_, a1 + 1 + sp.q_lo, sp.q_len, g1_fold(), c_a_);
+  folds_[3] = with_b1 ? ensure_table(*msm1_, b1_tab_, b1 + 1 + sp.q_lo, sp.q_len, g1_fold(), c_a_) : 0;
+  folds_[4] = 0;
+  if (!sp.grouped) {
+    msm1_->set_force_window_bits(c_lh_);
+    folds_[4] = ensure_table(*msm1_, lh_tab_, lh1_.as<Affine<F1>>() + sp.lh_lo, sp.lh_len, g1_fold(), c_lh_);
+  }
+  return fold_table_bytes();
+}
+
+template <class G1, class G2>
+size_t Groth16Prover<G1, G2>::fold_table_bytes() const {
+  return b2_tab_.buf.capacity() + a_tab_.buf.capacity() + b1_tab_.buf.capacity() + lh_tab_.buf.capacity() +
+         g1_tab_.buf.capacity();
+}
+
+template <class G1, class G2>
+void Groth16Prover<G1, G2>::last_folds(unsigned out[5]) const {
+  for (int i = 0; i < 5; ++i) out[i] = folds_[i];
 }
 
 template <class G1, class G2>
@@ -421,23 +528,20 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
     TA_HIP(hipStreamSynchronize(stream_));
     timings_.upload = ms_since(t0);
   }
-  // this rank's chunk [lo, lo + len) of an MSM over `total` points
-  auto shard = [&](size_t total, size_t* lo) {
-    const size_t chunk = (total + world - 1) / world;
-    *lo = std::min<size_t>((size_t)rank * chunk, total);
-    return std::min(chunk, total - *lo);
-  };
   ProofPartials<G1, G2> out;
   out.with_b1 = with_b1 ? 1u : 0u;
   out.rank = rank;
   out.world = world;
+  // the fold tables of this shard (a no-op after prepare() for it)
+  prepare(rank, world, with_b1);
+  const ShardPlan sp = shard_plan(rank, world);
 
   // MSMs over device-resident bases and scalars (prove.h:95-146)
   const Affine<F1>* a1 = a1_.as<Affine<F1>>();
   const Affine<F1>* b1 = b1_.as<Affine<F1>>();
   const Affine<F2>* b2 = b2_.as<Affine<F2>>();
-  size_t q_lo = 0;  // queries 1 .. m-1 (index 0 is added on the host)
-  const size_t q_len = m > 1 ? shard(m - 1, &q_lo) : 0;
+  const size_t q_lo = sp.q_lo;  // queries 1 .. m-1 (index 0 is added on the host)
+  const size_t q_len = sp.q_len;
   // The G2 MSM (about 3x the work of a G1 one) needs only the witness: it
   // starts on its own stream from a second host thread as soon as the
   // witness is on the device, beside the witness map and the G1 MSMs here;
@@ -471,8 +575,9 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   // scalars of the merged witness + h MSM: [witness values | h]
   const size_t nw = key_.num_witness();
   // one process, one device: A and the witness + h MSM as ONE grouped MSM
-  // (run_groups over the padded group layout of build_groups)
-  const bool grouped = world == 1 && glen_ > 0 && !(variant_ & 1);
+  // (run_groups over the padded group layout of build_groups), when its
+  // working set fits the device (prepare decided it: folds_[1] != 0)
+  const bool grouped = sp.grouped && folds_[1] != 0;
   Fr* d_lh = grouped ? gscalars_.as<Fr>() + glen_ : lh_.as<Fr>();
   if (grouped && q_len)
     TA_HIP(hipMemcpyAsync(gscalars_.as<Fr>(), d_full + 1, q_len * sizeof(Fr), hipMemcpyDeviceToDevice, stream_));
@@ -491,19 +596,11 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   msm1_->set_force_window_bits(c_a_);
   if (grouped) {
     // groups: [A | pad], [witness + h, first glen], [the rest | pad]
-    // the group bases are fixed too: their fold table (built on first use)
-    unsigned f1 = g1_fold();
-    while (f1 > 1 && msm1_->batch_windows(glen_) % f1 != 0) f1 >>= 1;
+    // the group bases are fixed too: their fold table (prepare)
+    const unsigned f1 = folds_[1];
     std::vector<P1> r;
     if (f1 > 1) {
-      if (g1_fold_f_ != f1 || g1_fold_c_ != c_a_) {
-        g1_fold_f_ = 0;
-        void* tab = g1_fold_.ensure((size_t)f1 * 3 * glen_ * sizeof(Affine<F1>));
-        msm1_->fold_bases_groups(gbases_.as<Affine<F1>>(), glen_, 3, f1, tab);
-        g1_fold_f_ = f1;
-        g1_fold_c_ = c_a_;
-      }
-      r = msm1_->run_groups_folded(g1_fold_.as<Affine<F1>>(), gscalars_.as<Fr>(), glen_, 3, f1);
+      r = msm1_->run_groups_folded(g1_tab_.buf.template as<Affine<F1>>(), gscalars_.as<Fr>(), glen_, 3, f1);
     } else {
       r = msm1_->run_groups(gbases_.as<Affine<F1>>(), gscalars_.as<Fr>(), glen_, 3);
     }
@@ -521,8 +618,7 @@ ProofPartials<G1, G2> Groth16Prover<G1, G2>::partials(const Fr* full, size_t cou
   // witness (l) and h MSMs merged; h_coefficients.size() == h_g1_query.size()
   // == domain size: the else branch of prove.h:103-112
   if (!grouped) {
-    size_t lh_lo = 0;
-    const size_t lh_len = shard(nw + n_, &lh_lo);
+    const size_t lh_lo = sp.lh_lo, lh_len = sp.lh_len;
     msm1_->set_force_window_bits(c_lh_);
     out.lh = fixed_msm(*msm1_, lh_tab_, lh1_.as<Affine<F1>>() + lh_lo, d_lh + lh_lo, lh_len, g1_fold(), c_lh_);
   }

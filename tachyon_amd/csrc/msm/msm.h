@@ -211,12 +211,34 @@ class MsmGpu {
     const unsigned c = batch_window_bits(len);
     return (Fr::Config::kModulusBits + 1 + c - 1) / c;
   }
+  // Memory planning for fixed-base callers (a proving key's fold tables):
+  //  * device_budget: the bytes one run may use -- free device memory plus
+  //    the buffers this context already holds (they are reused), capped by
+  //    TACHYON_MSM_MEM_LIMIT, minus 10 % (memory_divisions uses the same);
+  //  * run_bytes / batch_run_bytes: the working set of an n-point run, and of
+  //    run_groups / run_batch over count x len points;
+  //  * fit_fold(points, windows, want, reusable): the largest power of two <=
+  //    want dividing `windows` whose table (fold x points affine bases), its
+  //    build staging and the run's working set fit device_budget() +
+  //    `reusable` (an older table the caller will drop), with fold x points <
+  //    2^31 base indices; 1 = no table (run / run_groups instead).
+  size_t device_budget() const;
+  size_t run_bytes(size_t n) const { return work_bytes(n, force_c_); }
+  size_t batch_run_bytes(size_t len, size_t count) const { return work_bytes(len * count, batch_window_bits(len)); }
+  unsigned fit_fold(size_t points, unsigned windows, unsigned want, size_t run_bytes, size_t reusable = 0) const;
+  static size_t fold_table_bytes(size_t points, unsigned fold) { return (size_t)fold * points * sizeof(Aff); }
+  // staging of fold_bases: XYZZ copies + Montgomery-trick prefixes of one
+  // point chunk (the table is built chunk by chunk, kFoldChunkBytes at most)
+  static size_t fold_staging_bytes(size_t points, unsigned fold);
+  static constexpr size_t kFoldChunkBytes = size_t(1) << 30;
 
   static Point combine_windows(const std::vector<Point>& window_sums, unsigned c);
   // Mixed additions per second (G/s) of this curve's accumulation field code
   // in registers on the current device -- no gathers, no run logic: the VALU
   // ceiling the bench prices the accumulation against, measured on the same
-  // box.  field_bits 29 (BN254 G1's default field) or 32 (FIPS); 0 for others.
+  // box.  field_bits: BN254 G1 29 (its default field) or 32 (FIPS); BLS12-381
+  // G1 28; G2 the lane-pair limb fields, BN254 29 / BLS12-381 28 (G additions
+  // of whole G2 points, two lanes each); 0.0 for other values.
   static double madd_ceiling(int field_bits);
 
   void set_force_window_bits(unsigned c) { force_c_ = c; }
@@ -250,7 +272,7 @@ class MsmGpu {
   void fold_bases_c(const void* bases, size_t n, unsigned fold, void* out, unsigned c);
   void enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, const MsmPlan& plan, Point* d_windows);
   Point run_host_pipelined(const void* bases, const void* scalars, size_t n, size_t chunks);
-  size_t work_bytes(size_t n) const;
+  size_t work_bytes(size_t n, unsigned c) const;
   size_t held_bytes() const;
   size_t memory_divisions(size_t n, size_t resident_bytes) const;
   void ensure_group_events(unsigned groups);

@@ -2181,9 +2181,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // contiguous entry range [w0*n, w1*n); its sort (sort stream) overlaps the
   // accumulation of the previous group (MSM stream) -- the sort is HBM-bound,
   // the accumulation VALU-bound, so they share the CUs well
-  // (a batch sorts all its windows together: the recode writes the entries
-  // by scalar window, not by key window)
-  const unsigned G = batch_ > 1 ? W : std::max(1u, std::min(plan.group, W));
+  // (a batch or a fold sorts all its windows together: the recode writes the
+  // entries by scalar window, not by key window)
+  const unsigned G = (batch_ > 1 || fold_ > 1) ? W : std::max(1u, std::min(plan.group, W));
   const unsigned ngroups = (W + G - 1) / G;
   const size_t epw = entries / W;  // entries per key window's share of the array (n without a batch)
   size_t T = 0;  // accumulation threads over all groups
@@ -2886,52 +2886,113 @@ __global__ __launch_bounds__(kBlock, 3) void madd_ceiling32_kernel(const Affine<
   for (int i = 0; i < iters; ++i) acc = acc.madd_nz(q, &zero);
   out[t] = XYZZ<Bn254Fq>{acc.x, acc.y, zero ? Bn254Fq::zero() : Bn254Fq(acc.zz), acc.zzz};
 }
+// ... BLS12-381 G1's 14 x 28-bit field (Pol28), at seg_acc28_kernel's 2 waves per SIMD
+__global__ __launch_bounds__(kBlock, 2) void madd_ceiling28_kernel(const Affine<Bls381Fq>* __restrict__ pts,
+                                                                   XYZZ<Bls381Fq>* __restrict__ out, int iters) {
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  const Affine<Bls381Fq> p = pts[t & 1023], q = pts[(t + 5) & 1023];
+  const Pol28::F x2 = Pol28::shift_repack(q.x.v), y2 = Pol28::shift_repack(q.y.v);
+  Pol28::Acc acc = Pol28::from_shifted(Pol28::shift_repack(p.x.v), Pol28::shift_repack(p.y.v));
+  int special = 0;
+  for (int i = 0; i < iters; ++i) acc = Pol28::madd(acc, x2, y2, &special);
+  XYZZ<Bls381Fq> r = Pol28::to_xyzz(acc);
+  r.zz.v[0] ^= (uint32_t)special;
+  out[t] = r;
+}
+// ... the G2 lane pairs over the limb fields (PairPol28 / PairPol29, as
+// seg_acc_pair_limb_kernel): lane h of a pair holds component h; pts are Fq2
+// affine points as 4 base-field components (x0 x1 y0 y1)
+template <class Pol>
+__global__ __launch_bounds__(kBlock) void madd_ceiling_pair_kernel(const typename Pol::Fb* __restrict__ comps,
+                                                                   typename Pol::Fb* __restrict__ out, int iters) {
+  using Fb = typename Pol::Fb;
+  const uint32_t h = threadIdx.x & 1u;
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  const int pair = t >> 1;
+  const Fb* p = comps + 4 * (pair & 1023);
+  const Fb* q = comps + 4 * ((pair + 5) & 1023);
+  const typename Pol::F x2 = Pol::repack(q[h].v), y2 = Pol::repack(q[2 + h].v);
+  typename Pol::Acc acc = Pol::start(Pol::repack(p[h].v), Pol::repack(p[2 + h].v), h != 0);
+  int special = 0;
+  for (int i = 0; i < iters; ++i) acc = Pol::madd(acc, x2, y2, h != 0, &special);
+  Fb v;
+  Pol::to32(acc.x, v.v);
+  v.v[0] ^= (uint32_t)special;
+  out[4 * (size_t)t] = v;
+  Pol::to32(acc.y, v.v);
+  out[4 * (size_t)t + 1] = v;
+  Pol::to32(acc.zz, v.v);
+  out[4 * (size_t)t + 2] = v;
+  Pol::to32(acc.zzz, v.v);
+  out[4 * (size_t)t + 3] = v;
+}
+
+// Best-of-3 rate (G additions/s) of a ceiling kernel over `pts_words`
+// pseudo-random field words below the modulus (not curve points: the formula
+// does not care), `lanes_per_add` lanes per addition
+template <class In, class Out, class Kern>
+double time_ceiling(Kern kern, size_t in_words, size_t out_bytes_per_thread, unsigned top_mask_words,
+                    uint32_t top_mask, unsigned lanes_per_add) {
+  constexpr int kBlocks = 256 * 12, kIters = 400;
+  std::vector<uint32_t> h(in_words);
+  uint64_t s = 0x9e3779b97f4a7c15ull;
+  for (size_t i = 0; i < h.size(); ++i) {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    h[i] = (uint32_t)(s >> 32);
+    if (i % top_mask_words == top_mask_words - 1) h[i] &= top_mask;  // the top word of each element
+  }
+  void* pts = nullptr;
+  void* out = nullptr;
+  hipEvent_t e0, e1;
+  TA_HIP(hipMalloc(&pts, h.size() * 4));
+  TA_HIP(hipMalloc(&out, (size_t)kBlocks * kBlock * out_bytes_per_thread));
+  TA_HIP(hipMemcpy(pts, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  TA_HIP(hipEventCreate(&e0));
+  TA_HIP(hipEventCreate(&e1));
+  hipLaunchKernelGGL(kern, dim3(kBlocks), dim3(kBlock), 0, 0, static_cast<const In*>(pts), static_cast<Out*>(out), 4);
+  float best = 1e30f;
+  for (int r = 0; r < 3; ++r) {
+    TA_HIP(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(kern, dim3(kBlocks), dim3(kBlock), 0, 0, static_cast<const In*>(pts), static_cast<Out*>(out),
+                       kIters);
+    TA_HIP(hipEventRecord(e1, 0));
+    TA_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    TA_HIP(hipEventElapsedTime(&ms, e0, e1));
+    best = std::min(best, ms);
+  }
+  TA_HIP(hipGetLastError());
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(pts);
+  (void)hipFree(out);
+  return (double)kBlocks * kBlock / lanes_per_add * kIters / (best * 1e-3) / 1e9;
+}
 }  // namespace
 }  // namespace detail
 
 template <class Curve>
 double MsmGpu<Curve>::madd_ceiling(int field_bits) {
-  if constexpr (!std::is_same_v<Curve, Bn254G1>) {
-    (void)field_bits;
-    return 0.0;
-  } else {
+  using namespace detail;
+  if constexpr (std::is_same_v<Curve, Bn254G1>) {
     if (field_bits != 29 && field_bits != 32) return 0.0;
     require_gpu();
-    constexpr int kBlocks = 256 * 12, kIters = 400;
-    std::vector<Affine<Bn254Fq>> h(1024);  // field values below p (not curve points: the formula does not care)
-    uint64_t s = 0x9e3779b97f4a7c15ull;
-    for (auto& a : h)
-      for (Bn254Fq* f : {&a.x, &a.y})
-        for (int j = 0; j < 8; ++j) {
-          s = s * 6364136223846793005ull + 1442695040888963407ull;
-          f->v[j] = j == 7 ? (uint32_t)(s >> 32) & 0x0fffffffu : (uint32_t)(s >> 32);
-        }
-    Affine<Bn254Fq>* pts = nullptr;
-    XYZZ<Bn254Fq>* out = nullptr;
-    hipEvent_t e0, e1;
-    TA_HIP(hipMalloc(&pts, h.size() * sizeof(h[0])));
-    TA_HIP(hipMalloc(&out, (size_t)kBlocks * kBlock * sizeof(XYZZ<Bn254Fq>)));
-    TA_HIP(hipMemcpy(pts, h.data(), h.size() * sizeof(h[0]), hipMemcpyHostToDevice));
-    TA_HIP(hipEventCreate(&e0));
-    TA_HIP(hipEventCreate(&e1));
     auto* kern = field_bits == 29 ? &madd_ceiling29_kernel : &madd_ceiling32_kernel;
-    hipLaunchKernelGGL(kern, dim3(kBlocks), dim3(kBlock), 0, 0, pts, out, 4);
-    float best = 1e30f;
-    for (int r = 0; r < 3; ++r) {
-      TA_HIP(hipEventRecord(e0, 0));
-      hipLaunchKernelGGL(kern, dim3(kBlocks), dim3(kBlock), 0, 0, pts, out, kIters);
-      TA_HIP(hipEventRecord(e1, 0));
-      TA_HIP(hipEventSynchronize(e1));
-      float ms = 0;
-      TA_HIP(hipEventElapsedTime(&ms, e0, e1));
-      best = std::min(best, ms);
-    }
-    TA_HIP(hipGetLastError());
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipFree(pts);
-    (void)hipFree(out);
-    return (double)kBlocks * kBlock * kIters / (best * 1e-3) / 1e9;
+    return time_ceiling<Affine<Bn254Fq>, XYZZ<Bn254Fq>>(kern, 1024 * 16, sizeof(XYZZ<Bn254Fq>), 8, 0x0fffffffu, 1);
+  } else if constexpr (std::is_same_v<Curve, Bls381G1>) {
+    if (field_bits != 28) return 0.0;
+    require_gpu();
+    return time_ceiling<Affine<Bls381Fq>, XYZZ<Bls381Fq>>(&madd_ceiling28_kernel, 1024 * 24, sizeof(XYZZ<Bls381Fq>), 12, 0x0fffffffu, 1);
+  } else if constexpr (std::is_same_v<Curve, Bls381G2>) {
+    if (field_bits != 28) return 0.0;
+    require_gpu();
+    return time_ceiling<Bls381Fq, Bls381Fq>(&madd_ceiling_pair_kernel<PairPol28>, 1024 * 48, 4 * sizeof(Bls381Fq), 12,
+                                  0x0fffffffu, 2);
+  } else {
+    if (field_bits != 29) return 0.0;
+    require_gpu();
+    return time_ceiling<Bn254Fq, Bn254Fq>(&madd_ceiling_pair_kernel<PairPol29>, 1024 * 32, 4 * sizeof(Bn254Fq), 8,
+                                 0x0fffffffu, 2);
   }
 }
 
@@ -3040,8 +3101,8 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_host_pipelined(const void* base
 // (keys/values and their sort double buffers, sort scratch, accumulation
 // pieces and chain tables, bucket and segment sums), plus 10 %.
 template <class Curve>
-size_t MsmGpu<Curve>::work_bytes(size_t n) const {
-  const MsmPlan p = MsmPlan::make(n, Fr::Config::kModulusBits, force_c_, range_begin_, range_end_);
+size_t MsmGpu<Curve>::work_bytes(size_t n, unsigned c) const {
+  const MsmPlan p = MsmPlan::make(n, Fr::Config::kModulusBits, c, range_begin_, range_end_);
   const size_t entries = n * p.active();
   const size_t T = (entries + p.K - 1) / p.K;
   size_t bytes = entries * 16 + entries / 2;                 // entries (x2) + onesweep scratch
@@ -3073,21 +3134,53 @@ size_t MsmGpu<Curve>::held_bytes() const {
 // Free memory = hipMemGetInfo + the buffers this context already holds
 // (they are reused); TACHYON_MSM_MEM_LIMIT (bytes) caps it for tests.
 template <class Curve>
-size_t MsmGpu<Curve>::memory_divisions(size_t n, size_t resident_bytes) const {
+size_t MsmGpu<Curve>::device_budget() const {
   size_t free_b = 0, total_b = 0;
   TA_HIP(hipMemGetInfo(&free_b, &total_b));
   size_t avail = free_b + held_bytes();
   if (const char* e = getenv("TACHYON_MSM_MEM_LIMIT")) avail = std::min<size_t>(avail, strtoull(e, nullptr, 10));
-  avail = avail / 10 * 9;
+  return avail / 10 * 9;
+}
+
+template <class Curve>
+size_t MsmGpu<Curve>::memory_divisions(size_t n, size_t resident_bytes) const {
+  const size_t avail = device_budget();
   size_t d = 1;
-  while (resident_bytes + work_bytes((n + d - 1) / d) > avail) {
+  while (resident_bytes + work_bytes((n + d - 1) / d, force_c_) > avail) {
     if ((n + d - 1) / d <= (size_t(1) << 16))
       throw std::runtime_error("tachyon_mi355x: not enough device memory for the MSM (need " +
-                               std::to_string(resident_bytes + work_bytes((n + d - 1) / d)) + " B, have " +
+                               std::to_string(resident_bytes + work_bytes((n + d - 1) / d, force_c_)) + " B, have " +
                                std::to_string(avail) + " B)");
     d *= 2;
   }
   return d;
+}
+
+template <class Curve>
+size_t MsmGpu<Curve>::fold_staging_bytes(size_t points, unsigned fold) {
+  const size_t per_point = (size_t)fold * 5 * sizeof(F);  // XYZZ copies + prefixes
+  const size_t chunk = std::max<size_t>(1, std::min(points, kFoldChunkBytes / per_point));
+  return chunk * per_point;
+}
+
+template <class Curve>
+unsigned MsmGpu<Curve>::fit_fold(size_t points, unsigned windows, unsigned want, size_t run_b, size_t reusable) const {
+  if (points == 0 || want <= 1) return 1;
+  unsigned f = 1;
+  while (f * 2 <= want) f *= 2;
+  // the run may reuse this context's buffers; the table and its staging are
+  // new allocations, so they must also fit the free memory alone
+  const size_t avail = device_budget() + reusable;
+  size_t free_b = 0, total_b = 0;
+  TA_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (const char* e = getenv("TACHYON_MSM_MEM_LIMIT")) free_b = std::min<size_t>(free_b, strtoull(e, nullptr, 10));
+  const size_t avail_new = free_b / 10 * 9 + reusable;
+  for (; f > 1; f /= 2) {
+    if (windows % f != 0 || (uint64_t)f * points >= (uint64_t(1) << 31)) continue;
+    const size_t table = fold_table_bytes(points, f), staging = fold_staging_bytes(points, f);
+    if (table + staging + run_b <= avail && table + staging <= avail_new) return f;
+  }
+  return 1;
 }
 
 template <class Curve>
@@ -3176,19 +3269,29 @@ void MsmGpu<Curve>::fold_bases_c(const void* bases, size_t n, unsigned fold, voi
   const MsmPlan plan = MsmPlan::make(n, Fr::Config::kModulusBits, c);
   if (fold < 1 || plan.windows % fold != 0)
     throw std::runtime_error("tachyon_mi355x: an MSM fold must divide the plan's window count");
+  // (folded base indices vi + part n share the 32-bit entry value with the sign bit)
+  if ((uint64_t)fold * n >= (uint64_t(1) << 31))
+    throw std::runtime_error("tachyon_mi355x: fold x points must be < 2^31 (folded base indices)");
   if (n == 0) return;
   const unsigned shift = plan.c * (plan.windows / fold);
-  const size_t total = (size_t)fold * n;
-  F* xyzz = static_cast<F*>(norm_in_.ensure(total * 4 * sizeof(F)));
-  F* prefix = static_cast<F*>(norm_prefix_.ensure(total * sizeof(F)));
-  hipLaunchKernelGGL(detail::fold_points_kernel<F>, dim3(ceil_div(n, detail::kBlock)), dim3(detail::kBlock), 0,
-                     stream_, static_cast<const Aff*>(bases), n, fold, shift, xyzz);
+  // chunk by chunk of points, so the XYZZ staging stays <= kFoldChunkBytes
+  // whatever the table size (copy k of point i lands at out[k n + i])
+  const size_t m = fold_staging_bytes(n, fold) / ((size_t)fold * 5 * sizeof(F));
+  F* xyzz = static_cast<F*>(norm_in_.ensure((size_t)fold * m * 4 * sizeof(F)));
+  F* prefix = static_cast<F*>(norm_prefix_.ensure((size_t)fold * m * sizeof(F)));
   constexpr uint32_t kChunk = 16;
-  hipLaunchKernelGGL(detail::points_to_affine_kernel<F>, dim3(ceil_div(ceil_div(total, kChunk), detail::kBlock)),
-                     dim3(detail::kBlock), 0, stream_, xyzz, 3, static_cast<Aff*>(out), prefix, total, kChunk);
-  TA_HIP(hipGetLastError());
+  for (size_t lo = 0; lo < n; lo += m) {
+    const size_t len = std::min(m, n - lo);
+    hipLaunchKernelGGL(detail::fold_points_kernel<F>, dim3(ceil_div(len, detail::kBlock)), dim3(detail::kBlock), 0,
+                       stream_, static_cast<const Aff*>(bases) + lo, len, fold, shift, xyzz);
+    for (unsigned k = 0; k < fold; ++k)
+      hipLaunchKernelGGL(detail::points_to_affine_kernel<F>, dim3(ceil_div(ceil_div(len, kChunk), detail::kBlock)),
+                         dim3(detail::kBlock), 0, stream_, xyzz + (size_t)k * len * 4, 3,
+                         static_cast<Aff*>(out) + (size_t)k * n + lo, prefix + (size_t)k * len, len, kChunk);
+    TA_HIP(hipGetLastError());
+  }
   TA_HIP(hipStreamSynchronize(stream_));
-  // a one-time build: its XYZZ staging (4 x the table) is not kept
+  // a one-time build: its XYZZ staging is not kept
   norm_in_.release();
   norm_prefix_.release();
 }
@@ -3202,6 +3305,8 @@ typename MsmGpu<Curve>::Point MsmGpu<Curve>::run_folded(const void* folded_bases
   if (fold <= 1) return run(folded_bases, scalars, n);
   if (!is_device_pointer(folded_bases) || !is_device_pointer(scalars))
     throw std::runtime_error("tachyon_mi355x: a folded MSM takes device-resident bases and scalars");
+  if ((uint64_t)fold * n >= (uint64_t(1) << 31))
+    throw std::runtime_error("tachyon_mi355x: fold x points must be < 2^31 (folded base indices)");
   if (memory_divisions(n, 0) != 1)
     throw std::runtime_error("tachyon_mi355x: a folded MSM must fit the device in one piece");
   struct Reset {
@@ -3289,6 +3394,8 @@ std::vector<typename MsmGpu<Curve>::Point> MsmGpu<Curve>::run_batch_impl(const v
   const size_t total = len * count;
   if (total >= (size_t(1) << 31) || count > 4096)
     throw std::runtime_error("tachyon_mi355x: MSM batch too large (< 2^31 scalars, <= 4096 MSMs)");
+  if (fold > 1 && (uint64_t)fold * total >= (uint64_t(1) << 31))
+    throw std::runtime_error("tachyon_mi355x: fold x points must be < 2^31 (folded base indices)");
   // (window size: batch_window_bits)
   struct Reset {
     MsmGpu* m;

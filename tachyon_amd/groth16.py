@@ -139,6 +139,20 @@ class Groth16Prover:
         part = self.prove_partials(full, rank, world, with_b1)
         return self.assemble(all_gather_bytes(part, group, device), r, s)
 
+    def prepare(self, rank: int = 0, world: int = 1, with_b1: bool = False) -> int:
+        """Proving-key setup: build the fixed-base fold tables the proofs of
+        shard (rank, world) use, each the largest fold that fits the device
+        beside the MSM's working set (tachyon_mi355x_groth16_prepare); returns
+        the table bytes held.  A proof without it prepares itself."""
+        return lib().tachyon_mi355x_groth16_prepare(self._h, rank, world, 1 if with_b1 else 0)
+
+    def folds(self) -> dict:
+        """Folds the last prepare chose (1 = no table; grouped_g1 0 = A and the
+        witness + h MSM ran as separate MSMs; a1 / b1 / lh 0 = not built)."""
+        out = (ctypes.c_uint32 * 5)()
+        lib().tachyon_mi355x_groth16_prover_folds(self._h, out)
+        return dict(zip(("b2", "grouped_g1", "a1", "b1", "lh"), list(out)))
+
     def set_devices(self, device_ids):
         """One-process multi-device proofs: every later prove() runs the
         multi-rank split with one host thread per device entry (ids may

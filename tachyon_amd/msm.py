@@ -13,7 +13,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import CURVE_INFO, CURVES, FIELD_BYTES, lib
+from ._lib import CURVE_INFO, CURVES, FIELD_BYTES, MsmShard, lib
 
 _CREATE = {
     "bn254_g1": ("tachyon_bn254_g1_create_msm_gpu", "tachyon_bn254_g1_destroy_msm_gpu", "tachyon_bn254_g1_affine_msm_gpu"),
@@ -92,6 +92,21 @@ class VariableBaseMSMGpu:
         out = ctypes.create_string_buffer(self.point_bytes)
         lib().tachyon_mi355x_msm_gpu_sharded_affine(self.curve_id, self._ctx, comm.handle, pb, ps, n, out)
         del keep
+        return out.raw
+
+    def run_sharded_plan(self, comm, shard, bases, scalars) -> bytes:
+        """This rank's part of a shard_plan() partition (its point group's
+        bases / scalars over its window range) over a library communicator:
+        partial, all-gather and group sum inside the library
+        (tachyon_mi355x_msm_gpu_sharded_plan_affine); every rank returns the
+        whole MSM (affine bytes)."""
+        pb, ps, _, keep = self._args(bases, scalars, shard.count)
+        out = ctypes.create_string_buffer(self.point_bytes)
+        ok = lib().tachyon_mi355x_msm_gpu_sharded_plan_affine(self.curve_id, self._ctx, comm.handle,
+                                                              ctypes.byref(shard), pb, ps, out)
+        del keep
+        if not ok:
+            raise RuntimeError("sharded MSM failed on some rank (see stderr)")
         return out.raw
 
     def run_batch(self, d_bases, scalars, length: int, count: int) -> list:
@@ -205,6 +220,16 @@ class VariableBaseMSMGpu:
         out = (ctypes.c_float * 8)()
         lib().tachyon_mi355x_msm_gpu_last_timings(self.curve_id, self._ctx, out)
         return dict(zip(("h2d", "recode", "sort", "prep", "acc", "reduce", "total", "acc_launches"), list(out)))
+
+
+def shard_plan(curve: str, n_total: int, world: int, rank: int) -> MsmShard:
+    """The library's partition of an n_total-point MSM over `world` ranks for
+    `rank` (tachyon_mi355x_msm_shard_plan): point shards, or the hybrid point
+    group x window range where it measured faster."""
+    s = MsmShard()
+    if not lib().tachyon_mi355x_msm_shard_plan(CURVES[curve], n_total, world, rank, ctypes.byref(s)):
+        raise ValueError(f"rank {rank} outside a world of {world}")
+    return s
 
 
 def plan(curve: str, n: int):

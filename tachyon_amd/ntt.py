@@ -179,6 +179,71 @@ class Radix2EvaluationDomain:
             self._d, d_ptr, batch, 1 if inverse else 0)
 
 
+NTT_FIELDS = {"bn254_fr": 1, "bls12_381_fr": 3}
+
+
+class FieldEvaluationDomain:
+    """Radix2EvaluationDomain<F> for F = bn254 Fr or bls12_381 Fr over the
+    field-generic C-ABI domain (tachyon_mi355x_ntt_domain_*): the engine of
+    IcicleNTT<bls12_381::Fr> (icicle_ntt_bls12_381.cc:31-115).  fft / ifft
+    take and return the full domain (size x 32 Montgomery bytes; shorter
+    inputs are zero-padded), natural order, on the domain's coset."""
+
+    def __init__(self, field: str, num_coeffs: int):
+        if field not in NTT_FIELDS:
+            raise ValueError(f"no GPU NTT for {field}")
+        self.field = field
+        self._d = lib().tachyon_mi355x_ntt_domain_create(NTT_FIELDS[field], num_coeffs)
+        if not self._d:
+            raise RuntimeError("domain creation failed")
+        self.size = lib().tachyon_mi355x_ntt_domain_size(self._d)
+        self.log_size_of_group = self.size.bit_length() - 1
+
+    def close(self):
+        if self._d:
+            lib().tachyon_mi355x_ntt_domain_destroy(self._d)
+            self._d = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def group_gen(self) -> bytes:
+        out = ctypes.create_string_buffer(FR_BYTES)
+        lib().tachyon_mi355x_ntt_domain_group_gen(self._d, out)
+        return out.raw
+
+    def set_offset(self, offset_mont: bytes = None):
+        """Coset h*<w> of later transforms (GetCoset); None = the plain domain."""
+        buf = ctypes.create_string_buffer(offset_mont, FR_BYTES) if offset_mont is not None else None
+        lib().tachyon_mi355x_ntt_domain_set_offset(self._d, buf)
+
+    def _host(self, data: bytes, inverse: bool) -> bytes:
+        if len(data) > self.size * FR_BYTES:
+            raise ValueError("more elements than the domain size")
+        buf = ctypes.create_string_buffer(bytes(data) + b"\x00" * (self.size * FR_BYTES - len(data)),
+                                          self.size * FR_BYTES)
+        lib().tachyon_mi355x_ntt_domain_transform_host(self._d, buf, self.size, 1 if inverse else 0)
+        return buf.raw
+
+    def fft(self, coeffs: bytes) -> bytes:
+        return self._host(coeffs, False)
+
+    def ifft(self, evals: bytes) -> bytes:
+        return self._host(evals, True)
+
+    def transform_device(self, d_ptr: int, batch: int = 1, inverse: bool = False):
+        """In place on `batch` device arrays of size elements (on self.stream, not synchronised)."""
+        lib().tachyon_mi355x_ntt_domain_transform_device(self._d, d_ptr, batch, 1 if inverse else 0)
+
+    @property
+    def stream(self) -> int:
+        return lib().tachyon_mi355x_ntt_domain_stream(self._d)
+
+
 class FourStepNtt:
     """One rank's plan of the distributed four-step NTT (include/tachyon_mi355x.h,
     tachyon_mi355x_bn254_ntt4_*).  n = 2^log_n = R*C, R = 2^floor(log_n/2), or

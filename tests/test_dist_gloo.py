@@ -256,3 +256,62 @@ def test_library_host_comm_world3():
     want = b"".join(bytes((r * 53 + i) & 0xFF for i in range(777)) for r in range(3))
     for rank, (backend, world, rk, g, empty) in got:
         assert (backend, world, rk) == ("host", 3, rank) and g == want and empty == b""
+
+
+def _plan_worker(rank, world, port, curve, n, q):
+    """One rank of the LIBRARY's partition (tachyon_mi355x_msm_shard_plan):
+    its point group over its window range.  The window-range partial
+    sum_{w in [w0, w1)} 2^(c w) S_w is the MSM of the scalars' c-bit digits of
+    that range (the oracle computes it here -- no GPU on this box); the
+    partials go through the library's host-staged communicator
+    (tachyon_mi355x_comm_all_gather, the exchange of
+    tachyon_mi355x_msm_gpu_sharded_plan_affine) and the library's host group
+    sum."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from tachyon_amd import dist as D
+        from tachyon_amd import msm as M
+        pb, sf = O.CURVE_INFO[curve]
+        bases = O.gen_bases(curve, 123, n, 16).tobytes()
+        scalars = O.gen_scalars(sf, 123, n).tobytes()
+        s = M.shard_plan(curve, n, world, rank)
+        lo, m = s.start, s.count
+        sc = scalars[lo * 32:(lo + m) * 32]
+        if s.window_groups > 1:  # keep the digits of [w_begin, w_end) of every scalar of the group
+            mask = sum(((1 << s.window_bits) - 1) << (s.window_bits * w) for w in range(s.w_begin, s.w_end))
+            out = b""
+            for i in range(m):
+                k = int.from_bytes(O.field_op(sf, "from_mont", sc[32 * i:32 * (i + 1)]), "little") & mask
+                out += O.field_op(sf, "to_mont", k.to_bytes(32, "little"))
+            sc = out
+        part = O.msm(curve, bases[lo * pb:(lo + m) * pb], sc)[0] if m else bytes(pb)
+        comm = D.LibComm.from_process_group()
+        total = M.affine_sum(curve, comm.all_gather(part))
+        comm.close()
+        q.put((rank, (s.point_groups, s.window_groups), total, O.msm(curve, bases, scalars)[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libtachyon_mi355x.so not built")
+@pytest.mark.parametrize("curve,n,world,groups", [("bn254_g1", 90, 8, (4, 2)), ("bls12_381_g2", 21, 4, (2, 2)),
+                                                  ("bn254_g1", 50, 4, (4, 1))])
+def test_library_shard_plan_gloo(curve, n, world, groups):
+    """The hybrid point x window partition the library runs at N = 8 (BN254
+    G1: 4 point groups x 2 window ranges, c = 19) and N = 4 (BLS12-381 G2),
+    and point shards elsewhere: every rank's partial through the library's
+    communicator sums to the oracle's MSM on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, curve, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, g, total, want in got:
+        assert g == groups and total == want, rank

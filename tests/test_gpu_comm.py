@@ -25,7 +25,9 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 import torch.distributed as dist  # noqa: E402
 
-from test_gpu_dist import _run  # noqa: E402  (spawned gloo ranks on the one GPU)
+import torch.multiprocessing as mp  # noqa: E402
+
+from test_gpu_dist import _free_port, _run  # noqa: E402  (spawned gloo ranks on the one GPU)
 
 
 def _g16_inputs(curve="bn254", log_n=7):
@@ -162,3 +164,121 @@ def test_cpp_sharded_client_world1(tmp_path):
     assert bytes.fromhex(res["msm"]) == want
     C = pyref.Curve("bn254_g1")
     assert want == C.to_bytes(C.mul(C.G, O.dlog_dot("bn254_fr", seed, 16, scalars)))
+
+
+def test_rccl_sharded_plan_entry_world1():
+    """tachyon_mi355x_msm_gpu_sharded_plan_affine over the RCCL communicator at
+    world 1: the library's own plan (one point shard: the whole MSM), and a
+    hybrid shard of two window ranges (each range's partial is the window-range
+    MSM at the shard's window bits; the two partials add up to the MSM)."""
+    from tachyon_amd import dist as D
+    from tachyon_amd import msm as M
+    from tachyon_amd._lib import MsmShard
+    comm = D.LibComm.rccl()
+    n = 6000
+    bases = O.gen_bases("bn254_g1", 8, n, 64).tobytes()
+    scalars = O.gen_scalars("bn254_fr", 8, n).tobytes()
+    want = O.msm("bn254_g1", bases, scalars)[0]
+    db = torch.frombuffer(bytearray(bases), dtype=torch.uint8).cuda()
+    ds = torch.frombuffer(bytearray(scalars), dtype=torch.uint8).cuda()
+    m = M.VariableBaseMSMGpu("bn254_g1")
+    s = M.shard_plan("bn254_g1", n, 1, 0)
+    assert (s.start, s.count, s.window_groups) == (0, n, 1)
+    assert m.run_sharded_plan(comm, s, db, ds) == want
+    c = 13
+    W = D._windows_for("bn254_g1", c)
+    parts = []
+    for w0, w1 in (D.window_range(W, 0, 2), D.window_range(W, 1, 2)):
+        got = m.run_sharded_plan(comm, MsmShard(0, n, 1, 2, c, w0, w1), db, ds)
+        m.set_window_bits(c)
+        assert got == m.run_window_range(db, ds, w0, w1, n), (w0, w1)
+        m.set_window_bits(0)
+        parts.append(got)
+    assert M.affine_sum("bn254_g1", b"".join(parts)) == want
+    assert m.window_bits == 0 and m.run(db, ds) == want  # the entry restored the context's window bits
+    m.close()
+    comm.close()
+
+
+def _hybrid_worker(rank, world, port, q, curve, n):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tachyon_amd import dist as D
+        from tachyon_amd import msm as M
+        from tachyon_amd._lib import MsmShard
+        pb, sf = O.CURVE_INFO[curve]
+        bases = O.gen_bases(curve, 31, n, 64).view(np.uint8).reshape(n, pb)
+        scalars = O.gen_scalars(sf, 31, n).view(np.uint8).reshape(n, 32)
+        comm = D.LibComm.from_process_group()
+        # the hybrid at world 2: one point group (all points) x two window ranges, c = 16
+        c = 16
+        w0, w1 = D.window_range(D._windows_for(curve, c), rank, world)
+        shard = MsmShard(0, n, 1, world, c, w0, w1)
+        db = torch.from_numpy(np.ascontiguousarray(bases).reshape(-1)).cuda()
+        ds = torch.from_numpy(np.ascontiguousarray(scalars).reshape(-1)).cuda()
+        m = M.VariableBaseMSMGpu(curve)
+        got = m.run_sharded_plan(comm, shard, db, ds)
+        # and the library's own plan at world 2 (point shards)
+        s = M.shard_plan(curve, n, world, rank)
+        db2 = torch.from_numpy(np.ascontiguousarray(bases[s.start:s.start + s.count]).reshape(-1)).cuda()
+        ds2 = torch.from_numpy(np.ascontiguousarray(scalars[s.start:s.start + s.count]).reshape(-1)).cuda()
+        got2 = m.run_sharded_plan(comm, s, db2, ds2)
+        m.close()
+        comm.close()
+        q.put((rank, got, got2))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("curve,n", [("bn254_g1", 5000), ("bls12_381_g2", 700)])
+def test_host_staged_sharded_plan_world2(curve, n):
+    """Two gloo ranks sharing the GPU through the library's host-staged
+    communicator: a hybrid shard (window ranges of all points) and the
+    library's own world-2 plan; every rank's result is the oracle's MSM."""
+    got = _run(_hybrid_worker, 2, curve, n)
+    pb, sf = O.CURVE_INFO[curve]
+    want = O.msm(curve, O.gen_bases(curve, 31, n, 64).tobytes(), O.gen_scalars(sf, 31, n).tobytes())[0]
+    for rank, hyb, pts in got:
+        assert hyb == want and pts == want, rank
+
+
+def _failing_rank_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ctypes
+        import time
+        from tachyon_amd import dist as D
+        from tachyon_amd import msm as M
+        from tachyon_amd._lib import lib
+        comm = D.LibComm.from_process_group()
+        n = 3000
+        bases = O.gen_bases("bn254_g1", 5, n, 64).tobytes()
+        scalars = O.gen_scalars("bn254_fr", 5, n).tobytes()
+        s = M.shard_plan("bn254_g1", n, world, rank)
+        m = M.VariableBaseMSMGpu("bn254_g1")
+        ctx = m._ctx if rank == 0 else None  # rank 1's local part fails (null context)
+        out = ctypes.create_string_buffer(64)
+        t0 = time.time()
+        rc = lib().tachyon_mi355x_msm_gpu_sharded_plan_affine(0, ctx, comm.handle, ctypes.byref(s),
+                                                             bases[s.start * 64:], scalars[s.start * 32:], out)
+        dt = time.time() - t0
+        # the communicator still works after the failed call
+        after = comm.all_gather(bytes([rank]))
+        m.close()
+        comm.close()
+        q.put((rank, rc, out.raw == bytes(64), dt, after))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_failing_rank_does_not_hang_the_others():
+    """A rank whose local part throws still enters the all-gather with a
+    failure flag, so rank 0 -- whose MSM succeeded -- is not left waiting in
+    the collective: tachyon_mi355x_msm_gpu_sharded_plan_affine returns 0 on
+    BOTH ranks (out untouched, no abort) and the communicator stays usable."""
+    got = _run(_failing_rank_worker, 2, timeout=180)
+    for rank, rc, untouched, dt, after in got:
+        assert rc == 0 and untouched and after == bytes([0, 1]), rank
+        assert dt < 120, rank

@@ -74,9 +74,10 @@ def test_synthetic_parity(curve, log_n, num_public, seed):
     prover.set_variant(1)
     assert list(prover.prove(fb)) == list(OG.prove(zk, full, h=h))
     # the fixed-base fold tables of the G2 B MSM (variant bits 1-3) and the
-    # grouped G1 MSM (bits 4-6): none (18), two copies each (36), B2 sixteen
-    # and G1 eight (74); the default is B2 eight, G1 four (where they divide W)
-    for v in (18, 36, 74):
+    # grouped G1 MSM (bits 4-6): none (18), two copies each (36), B2 eight with
+    # the default G1 (8), B2 sixteen and G1 eight (74); the default is B2
+    # sixteen, G1 four (groth16.h kB2Fold / kG1Fold, where they divide W)
+    for v in (18, 36, 8, 74):
         prover.set_variant(v)
         assert list(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == want_zk, v
     prover.set_variant(0)
@@ -125,10 +126,60 @@ def test_configs4_size_parity():
     assert tuple(prover.prove(fb, Fr.to_bytes(r), Fr.to_bytes(s))) == tuple(OG.prove_np(zkey, full, r, s))
     prover.set_variant(1)  # the round-4 separate A and witness + h MSMs: the same proof
     assert tuple(prover.prove(fb)) == tuple(OG.prove_np(zkey, full))
-    for v in (18, 36, 74):  # fold tables off, two copies each, B2 x16 + G1 x8 (default: B2 x8, G1 x4)
+    for v in (18, 36, 8, 74):  # fold tables off, two copies each, B2 x8, B2 x16 + G1 x8 (default: B2 x16, G1 x4)
         prover.set_variant(v)
         assert tuple(prover.prove(fb)) == tuple(OG.prove_np(zkey, full)), v
     prover.close()
+
+
+_FALLBACK_CHILD = r"""
+import json, os, sys
+sys.path.insert(0, os.environ["REPO"])
+import bench
+from tachyon_amd.groth16 import Groth16Prover
+zkey, full = bench.synth_groth16_zkey(int(os.environ["LOG_N"]))
+p = Groth16Prover(zkey)
+bytes_held = p.prepare()
+folds = p.folds()
+proof = p.prove(full.tobytes())
+print(json.dumps({"bytes": bytes_held, "folds": folds, "proof": [x.hex() for x in proof]}))
+"""
+
+
+def _prove_child(log_n, limit):
+    """A proof in a child process (an MSM that cannot fit aborts the process,
+    like the reference's CHECKs): prepare() + prove() under TACHYON_MSM_MEM_LIMIT."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, REPO=repo, LOG_N=str(log_n))
+    env.pop("TACHYON_MSM_MEM_LIMIT", None)
+    if limit:
+        env["TACHYON_MSM_MEM_LIMIT"] = str(limit)
+    r = subprocess.run([sys.executable, "-c", _FALLBACK_CHILD], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_fold_tables_memory_fallback():
+    """The proving key's fold tables are an explicit setup step (prepare) and
+    memory-aware: with the device capped (TACHYON_MSM_MEM_LIMIT = 256 MiB) a
+    2^17-constraint key gets no tables (fold 1) and A and the witness + h MSM
+    run as separate MSMs instead of the grouped one; without a cap both get
+    tables.  Both proofs equal the CPU oracle's."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    log_n = 17
+    zkey, full = bench.synth_groth16_zkey(log_n)
+    want = [x.hex() for x in OG.prove_np(zkey, full)]
+    free = _prove_child(log_n, None)
+    capped = _prove_child(log_n, 256 << 20)
+    # (at 2^17 the MSMs' c = 10 gives W = 26 windows: the folds that divide it are 2)
+    assert free["folds"]["b2"] > 1 and free["folds"]["grouped_g1"] > 1, free["folds"]
+    assert capped["folds"]["b2"] == 1 and capped["folds"]["grouped_g1"] == 0, capped["folds"]
+    assert capped["bytes"] == 0 < free["bytes"]
+    assert free["proof"] == want and capped["proof"] == want
 
 
 def test_all_public_no_witness():

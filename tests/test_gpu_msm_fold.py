@@ -84,3 +84,32 @@ def test_msm_folded_default_plan_2_16():
             assert m.run(d_bases, d_scalars, n) == want
         finally:
             m.close()
+
+
+@pytest.mark.parametrize("variant", [4, 8, 12])
+def test_msm_folded_under_pipelined_group_variants(variant):
+    """set_variant bits 2-3 (pipelined window groups: group = 1 or 2 windows)
+    are accepted for every MSM, but a folded run's recode writes its entries
+    by scalar window, so the fold keeps one group of all key windows
+    (run_windows forces G = W under a fold, as under a batch): the folded MSM
+    still equals the oracle's, and so does the plain one under the variant."""
+    torch = pytest.importorskip("torch")
+    from tachyon_amd.msm import VariableBaseMSMGpu
+    curve = "bn254_g1"
+    pb, sf = O.CURVE_INFO[curve]
+    n = 2000
+    bases = O.gen_bases(curve, 404, n, 64).tobytes()
+    scalars = O.gen_scalars(sf, 4040, n).tobytes()
+    want = O.msm(curve, bases, scalars)[0]
+    m = VariableBaseMSMGpu(curve)
+    try:
+        m.set_window_bits(16)  # W = 16
+        m.set_variant(variant)
+        d_bases, d_scalars = _dev(torch, bases), _dev(torch, scalars)
+        assert m.run(d_bases, d_scalars, n) == want
+        for fold in (2, 4, 8):
+            d_tab = torch.empty(fold * n * pb, dtype=torch.uint8, device="cuda")
+            m.fold_bases(d_bases, n, fold, d_tab)
+            assert m.run_folded(d_tab, d_scalars, n, fold) == want, fold
+    finally:
+        m.close()

@@ -1,8 +1,10 @@
 """bench.py's multi-GPU MSM partitions (msm_partition: point shards, the window
-split and the hybrid of HYBRID_PLANS): for every curve and world size the
-ranks' (point range, window range) shares tile the (point, window) pairs of the
-MSM exactly once -- the property that makes the all-gather + group sum of the
-partials the MSM.  Host logic only, no GPU."""
+split and the hybrid; auto = the library's plan, tachyon_mi355x_msm_shard_plan):
+for every curve and world size the ranks' (point range, window range) shares
+tile the (point, window) pairs of the MSM exactly once -- the property that
+makes the all-gather + group sum of the partials the MSM -- and the shard the
+library's sharded entry takes says the same.  Host logic only (the library
+loads without a GPU; the plan is pure host code)."""
 import argparse
 import os
 import sys
@@ -23,9 +25,13 @@ def _args(split, window_groups=2, window_bits=0):
 def _tiles(curve, world, args, n_total):
     cover = {}
     for rank in range(world):
-        split, start, n, wrange, c, p, q = bench.msm_partition(args, curve, world, rank, n_total)
+        split, start, n, wrange, c, p, q, shard = bench.msm_partition(args, curve, world, rank, n_total)
         W = D._windows_for(curve, c) if c else 1
         w0, w1 = wrange if wrange is not None else (0, W)
+        if shard is not None:  # the library's shard record agrees
+            assert (shard.start, shard.count, shard.point_groups, shard.window_groups) == (start, n, p, q)
+            if q > 1:
+                assert (shard.window_bits, shard.w_begin, shard.w_end) == (c, w0, w1)
         for w in range(w0, w1):
             cover.setdefault(w, []).append((start, start + n))
         assert p * q == world
@@ -47,11 +53,24 @@ def test_partition_tiles_every_point_window_pair_once(curve, world, split):
 
 
 def test_auto_follows_the_plan_table():
-    for (curve, world), (q, c) in bench.HYBRID_PLANS.items():
-        split, _, n, wrange, cc, p, qq = bench.msm_partition(_args("auto"), curve, world, 0, 1 << 20)
+    plans = bench.hybrid_plans()
+    # the measured table in capi.hip (kHybridPlans)
+    assert plans == {("bn254_g1", 8): (2, 19), ("bls12_381_g2", 4): (2, 19), ("bls12_381_g2", 8): (4, 16)}
+    for (curve, world), (q, c) in plans.items():
+        split, _, n, wrange, cc, p, qq, _ = bench.msm_partition(_args("auto"), curve, world, 0, 1 << 20)
         assert (split, qq, cc, p) == ("hybrid", q, c, world // q)
         assert n == (1 << 20) // p and wrange == D.window_range(D._windows_for(curve, c), 0, q)
     # no plan: point shards (BN254 at 2 and 4 GPUs measured no faster as the hybrid)
     for world in (2, 4):
         assert bench.msm_partition(_args("auto"), "bn254_g1", world, 1, 1 << 20)[0] == "points"
     assert bench.msm_partition(_args("auto"), "bn254_g1", 1, 0, 1 << 20)[0] == "points"
+
+
+def test_library_shard_plan_refuses_bad_ranks():
+    from tachyon_amd import msm as M
+    with pytest.raises(ValueError):
+        M.shard_plan("bn254_g1", 100, 4, 4)
+    with pytest.raises(ValueError):
+        M.shard_plan("bn254_g1", 100, 0, 0)
+    s = M.shard_plan("bn254_g1", 0, 8, 7)  # an empty MSM: empty shards
+    assert s.count == 0

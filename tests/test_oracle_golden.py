@@ -63,16 +63,35 @@ def test_input_generator_matches_golden(curve):
         assert bs == b"".join(B(x) for x in c["bases"])
 
 
-def test_ntt_golden():
-    g = load("ntt_bn254_fr.json")
+@pytest.mark.parametrize("field", ["bn254_fr", "bls12_381_fr"])
+def test_ntt_golden(field):
+    g = load(f"ntt_{field}.json")
     for c in g["cases"]:
         n = 1 << c["log_n"]
         coeffs = b"".join(B(x) for x in c["coeffs"])
         off = B(c["offset_mont"]) if c["offset"] != 1 else None
-        ev = O.fft(coeffs, n, off)
+        ev = O.fft(coeffs, n, off, field=field)
         assert ev.hex() == "".join(c["evals"]), c
-        back = O.ifft(ev, n, off)
+        back = O.ifft(ev, n, off, field=field)
         assert back.hex() == "".join(c["ifft_of_evals"]), c
+
+
+def test_bls12_381_fr_roots_of_unity():
+    """BLS12-381 Fr: the BUILD subgroup generator 7
+    (tachyon/math/elliptic_curves/bls12/bls12_381/BUILD.bazel:62-65) gives
+    arkworks' two-adic root of unity (2-adicity 32), and the oracle's domain
+    roots equal the golden file's w_(2^k)."""
+    import ctypes
+    g = load("ntt_bls12_381_fr.json")
+    assert g["two_adic_root_of_unity"] == \
+        "10238227357739495823651030575849232062558860180284477541189508159991286009131"
+    r = pyref.Field("bls12_381_fr").p
+    w32 = int(g["two_adic_root_of_unity"])
+    assert pow(w32, 1 << 31, r) == r - 1  # a primitive 2^32-th root
+    for k in range(1, 17):  # (a domain builds its twiddle cache: sizes up to 2^16 here)
+        out = ctypes.create_string_buffer(96)
+        assert O.lib().oracle_domain_info(3, 1 << k, out) == 0
+        assert out.raw[:32].hex() == g["roots_of_unity_mont"][str(k)], k
 
 
 def test_roots_of_unity():
