@@ -315,12 +315,12 @@ CEILING_FIELD = {"bn254_g1": 29, "bls12_381_g1": 28, "bn254_g2": 29, "bls12_381_
 
 def acc_kernel_name(curve, schedule):
     """The accumulation kernel the last run launched (rocprofv3's short name)."""
+    if schedule["lane_pair"]:  # (G2; the BLS12-381 G2 run also reports the 28-bit field bit)
+        return "seg_acc_pair_limb_kernel" if not curve.endswith("g1") else "seg_acc_kernel"
     if schedule["acc29"]:
         return "seg_acc29_kernel"
     if schedule["acc28"]:
         return "seg_acc28_kernel"
-    if schedule["lane_pair"]:
-        return "seg_acc_pair_limb_kernel"
     return "seg_acc_kernel"
 
 

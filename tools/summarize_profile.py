@@ -41,6 +41,13 @@ def main(d):
             print(f"| {short(r['Name'])} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
                   f"{float(r['AverageNs']) / 1e6:.4f} | {float(r['Percentage']):.2f} |")
         print()
+    # average dispatch duration per short kernel name (instantiations merged)
+    dur = collections.defaultdict(lambda: [0.0, 0])
+    if os.path.exists(stats):
+        for r in csv.DictReader(open(stats)):
+            d = dur[short(r["Name"])]
+            d[0] += float(r["TotalDurationNs"])
+            d[1] += int(r["Calls"])
     agg = collections.defaultdict(list)
     meta = {}
     for sub in ("fetch", "write", "valu"):
@@ -66,9 +73,13 @@ def main(d):
             valu = f"{100.0 * act / wave:.1f}" if act and wave else "-"
             fmt = (lambda x: f"{x:.4g}" if x is not None else "-")
             v, s, sc, l = meta[k]
+            clock = "-"
+            if grbm and dur[k][1]:  # GRBM_GUI_ACTIVE summed over the 8 XCDs / 8 / the dispatch's duration
+                clock = f"{grbm / 8 / (dur[k][0] / dur[k][1]):.2f}"
             print(f"| {k} | {v} | {sc} | {l} | {fmt(fetch * 2 if fetch else None)} | {fmt(write)} | {fmt(insts)} | "
-                  f"{valu} | - |")
-        print("\nVALU busy % = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of wave-cycles issuing VALU).")
+                  f"{valu} | {clock} |")
+        print("\nVALU busy % = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of wave-cycles issuing VALU); eff. clock "
+              "= GRBM_GUI_ACTIVE / 8 XCDs / the kernel's average trace duration.")
         # per-dispatch HBM traffic for bench.py's roofline "traffic" field
         # (FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE counts half of a
         # wide streaming read -- MI355X_MICROARCH.md, HBM/rocprofv3 -- so the x2
@@ -85,7 +96,30 @@ def main(d):
                           "traffic_bytes": 2 * fb + wb}
         with open(os.path.join(d, "pmc_traffic.json"), "w") as fh:
             json.dump(traffic, fh, indent=1)
-        derived(agg, traffic)
+        if os.environ.get("PROFILE_UNITS"):
+            derived_units(agg, traffic, os.environ["PROFILE_UNITS"])
+        else:
+            derived(agg, traffic)
+
+
+def derived_units(agg, traffic, spec):
+    """PROFILE_UNITS='kernel=units[:lanes],...': VALU instructions per unit
+    (SQ_INSTS_VALU x 64 / (units x lanes)) and HBM bytes per unit of those
+    kernels (e.g. the BLS12-381 accumulations: units = n x W additions,
+    lanes = 2 for the G2 lane pairs)."""
+    print("\n## Per-unit figures (PROFILE_UNITS)\n")
+    for item in spec.split(","):
+        k, _, u = item.partition("=")
+        units, _, lanes = u.partition(":")
+        units, lanes = float(units), float(lanes or 1)
+        v = agg.get((k, "SQ_INSTS_VALU"))
+        t = traffic.get(k)
+        if v:
+            print(f"* `{k}`: {sum(v) / len(v) * 64 / (units * lanes):.0f} VALU instructions per unit per lane "
+                  f"({units:.4g} units x {lanes:g} lanes per dispatch)")
+        if t:
+            print(f"* `{k}`: {t['traffic_bytes'] / units:.1f} HBM B per unit ({t['fetch_bytes_raw'] / units:.1f} raw "
+                  f"FETCH + {t['write_bytes'] / units:.1f} written)")
 
 
 def derived(agg, traffic, msm_log_n=26, windows=13, ntt_log_n=24):
