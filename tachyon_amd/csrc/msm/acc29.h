@@ -23,8 +23,9 @@ TA_HD Acc from_shifted(const F29& x2, const F29& y2) {
 // R T + (4p - Y1) PPP.  Value bounds (in units of p; a product of A and B
 // leaves < A B / 128 + 1 + addend), invariant acc X < 10, Y, ZZ, ZZZ < 3 (a
 // run's first point and the doubling's output come in through from32, < 3p);
-// base coordinates x~ << 5 < 32:
-//   P   = x2 ZZ1 + (16p - X1)  < 17.75    R  = y2 ZZZ1 + (4p - Y1) < 5.75
+// base coordinates x~ << 5 < 32, y2 < 33 (a negative digit's y is 33p - y~ << 5
+// in kK33's raised limbs, limbs < 2^30):
+//   P   = x2 ZZ1 + (16p - X1)  < 17.75    R  = y2 ZZZ1 + (4p - Y1) < 5.78
 //   PP  = P^2 < 3.47  PPP = P PP < 1.49   Q  = X1 PP < 1.28
 //   X3  = R^2 + (8p - PPP - 2Q) < 9.26    T  = Q + (16p - X3) < 17.3
 //   Y3  = R T + (4p - Y1) PPP < 1.83      ZZ3, ZZZ3 < 1.09

@@ -666,9 +666,13 @@ __device__ __forceinline__ Pt add(const Pt& a, const Pt& b) {
 struct alignas(16) Raw {
   F29 x, y, zz, zzz;
 };
+// the identity is zz = 0 alone (load_raw tests zz; x, y, zzz are not read
+// then): one 9-limb select instead of four in the run-end stores
 __device__ __forceinline__ Raw raw_of(const Acc& a, bool zero) {
-  if (zero) return Raw{};
-  return {a.x, a.y, a.zz, a.zzz};
+  Raw r{a.x, a.y, a.zz, a.zzz};
+#pragma unroll
+  for (int k = 0; k < 9; ++k) r.zz.l[k] = zero ? 0u : a.zz.l[k];
+  return r;
 }
 __device__ __forceinline__ Pt load_raw(const void* __restrict__ p, size_t i) {
   const Raw r = static_cast<const Raw*>(p)[i];
@@ -703,6 +707,17 @@ struct Pol29 {
   using Acc = acc29::Acc;
   using Raw = acc29::Raw;
   static __device__ __forceinline__ F shift_repack(const uint32_t* w) { return f29::shl5_repack(w); }
+  // the base's y for a digit of sign `neg`: y~ << 5 (< 32p), negated in the
+  // 29-bit limbs as 33p - y~ << 5 (kK33's raised limbs: no borrows; the value
+  // stays < 33p, which madd's bounds allow) -- 9 subtractions and 9 selects
+  // instead of a borrow chain over the canonical 32-bit words
+  static __device__ __forceinline__ F repack_y(const Fq& y, uint32_t neg) {
+    F r = f29::shl5_repack(y.v);
+    const F m = f29::ksub(f29::kK33, r);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.l[i] = neg ? m.l[i] : r.l[i];
+    return r;
+  }
   static __device__ __forceinline__ Acc from_shifted(const F& x, const F& y) { return acc29::from_shifted(x, y); }
   static __device__ __forceinline__ Acc madd(const Acc& a, const F& x, const F& y, int* sp) {
     return acc29::madd(a, x, y, sp);
@@ -717,6 +732,9 @@ struct Pol28 {
   using Acc = acc28_core::Acc;
   using Raw = Acc;  // (no raw stores: the BLS12-381 reductions are the FIPS kernels)
   static __device__ __forceinline__ F shift_repack(const uint32_t* w) { return f28::shl8_repack(w); }
+  static __device__ __forceinline__ F repack_y(const Fq& y, uint32_t neg) {
+    return f28::shl8_repack(y.cond_neg_canonical(neg).v);
+  }
   static __device__ __forceinline__ Acc from_shifted(const F& x, const F& y) { return acc28_core::from_shifted(x, y); }
   static __device__ __forceinline__ Acc madd(const Acc& a, const F& x, const F& y, int* sp) {
     return acc28_core::madd(a, x, y, sp);
@@ -824,8 +842,7 @@ __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>
         acc_zero = true;
       }
       if (!P.is_zero_canonical()) {
-        P.y = P.y.cond_neg_canonical(v0 & kSignBit);
-        const F x2 = Pol::shift_repack(P.x.v), y2 = Pol::shift_repack(P.y.v);  // both paths
+        const F x2 = Pol::shift_repack(P.x.v), y2 = Pol::repack_y(P.y, v0 & kSignBit);  // both paths
         if (acc_zero) {
           acc = Pol::from_shifted(x2, y2);
           acc_zero = false;

@@ -279,6 +279,18 @@ def test_point_formulas_at_bounds(point_harness):
         # the negated base (the kernel's p - y~ for a negative digit)
         lines.append(" ".join(map(str, ["madd"] + acc_a + limbs(xt << 5) + limbs((P - yt) << 5))))
         want.append(("madd", _affine_add(A, (B[0], P - B[1])), 0))
+        xa, ya = A[0] * 2**256 % P, A[1] * 2**256 % P
+        # the kernel's negation in 29-bit limbs (msm_impl.h Pol29::repack_y): 33p - y~ << 5 with
+        # kK33's raised limbs, at the top of its bound (y~ = 0 gives 33p itself)
+        k33 = [0x281ca627, 0x2190778e, 0x2ac70d2f, 0x3d797cec, 0x26410879, 0x3e4358d5, 0x35830962,
+               0x39e0ecb3, 0x063cee1b]
+        assert value(k33) == 33 * P
+        lines.append(" ".join(map(str, ["madd"] + acc_a + limbs(xt << 5) +
+                                  [k - l for k, l in zip(k33, limbs(yt << 5))])))
+        want.append(("madd", _affine_add(A, (B[0], P - B[1])), 0))
+        lines.append(" ".join(map(str, ["madd"] + acc_a + limbs(xa << 5) +
+                                  [k - l for k, l in zip(k33, limbs(ya << 5))])))
+        want.append(("madd", None, 1))
         # specials: base = acc point (double in the caller), base = -acc (identity)
         xa, ya = A[0] * 2**256 % P, A[1] * 2**256 % P
         lines.append(" ".join(map(str, ["madd"] + acc_a + limbs(xa << 5) + limbs(ya << 5))))

@@ -412,7 +412,12 @@ def test_madd_ceiling():
     r29, r32 = g1.madd_ceiling(29), g1.madd_ceiling(32)
     assert 1.0 < r29 < 200.0 and 1.0 < r32 < 200.0, (r29, r32)
     assert g1.madd_ceiling(31) == 0.0
-    assert M.VariableBaseMSMGpu("bn254_g2").madd_ceiling(29) == 0.0
+    # BLS12-381 G1's 28-bit field and the G2 lane pairs (whole G2 additions): slower than G1's
+    bls = M.VariableBaseMSMGpu("bls12_381_g1").madd_ceiling(28)
+    g2 = M.VariableBaseMSMGpu("bn254_g2").madd_ceiling(29)
+    bls2 = M.VariableBaseMSMGpu("bls12_381_g2").madd_ceiling(28)
+    assert 0.5 < bls2 < g2 < r29 and 0.5 < bls2 < bls < r29, (r29, bls, g2, bls2)
+    assert M.VariableBaseMSMGpu("bn254_g2").madd_ceiling(28) == 0.0
 
 
 def _neg_point(curve, p: bytes) -> bytes:

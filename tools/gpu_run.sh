@@ -6,7 +6,8 @@
 #
 # STEP is one of
 #   smoke              python __graft_entry__.py smoke
-#   tests=ARGS         python -u -m pytest -m gpu -x -v --timeout 300 ARGS   (ARGS default: tests)
+#   tests=ARGS         python -u -m pytest -m gpu -x -v --timeout 300 ARGS   (ARGS default: tests;
+#                      evaluated by the shell: quote a -k expression inside it)
 #   bench=ARGS         python bench.py ARGS; the JSON line -> gpurun_out/TAG/bench_<k>.json
 #   profile=ARGS       tools/profile_round.sh TAG ARGS (trace + PMC passes of a bench command)
 #   pmc=COUNTERS@ARGS  one rocprofv3 --pmc pass over python bench.py ARGS (counters space-separated)
@@ -33,9 +34,9 @@ for step in "$@"; do
   echo "[$(date +%T)] step $k: $step" | tee -a "$OUT/steps.log"
   case $kind in
     smoke) timeout -k 10 "$LIMIT" python __graft_entry__.py smoke > "$log" 2>&1 ;;
-    tests) timeout -k 10 "$LIMIT" python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread \
-             ${arg:-tests} > "$log" 2>&1 ;;
-    bench) timeout -k 10 "$LIMIT" python bench.py $arg > "$log" 2>&1 ;;
+    tests) eval "timeout -k 10 $LIMIT python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread \
+             ${arg:-tests}" > "$log" 2>&1 ;;
+    bench) eval "timeout -k 10 $LIMIT python bench.py $arg" > "$log" 2>&1 ;;
     profile) timeout -k 10 "$LIMIT" bash tools/profile_round.sh "$TAG" $arg > "$log" 2>&1 ;;
     pmc) counters=${arg%%@*}
          bargs=${arg#*@}
