@@ -732,8 +732,18 @@ struct Pol28 {
   using Acc = acc28_core::Acc;
   using Raw = Acc;  // (no raw stores: the BLS12-381 reductions are the FIPS kernels)
   static __device__ __forceinline__ F shift_repack(const uint32_t* w) { return f28::shl8_repack(w); }
+  // 257p with the low limbs raised by 2^28 (limbs < 2^29): 257p - y~ << 8 is a
+  // borrow-free negation of the shifted canonical y~ (< 256p), < 257p -- inside
+  // acc28's base bound of 512p (tests/test_f28_host.py)
+  static constexpr uint32_t kK257[14] = {0x1faa55abu, 0x1feffffeu, 0x13ffb9b7u, 0x1feb0054u, 0x1a42caaau,
+                                         0x197a7a70u, 0x16980372u, 0x17897d21u, 0x1bc2d077u, 0x1f8843bcu,
+                                         0x135df98du, 0x180e566bu, 0x1c23b965u, 0x01a1b12eu};
   static __device__ __forceinline__ F repack_y(const Fq& y, uint32_t neg) {
-    return f28::shl8_repack(y.cond_neg_canonical(neg).v);
+    F r = f28::shl8_repack(y.v);
+    const F m = f28::ksub(kK257, r);
+#pragma unroll
+    for (int i = 0; i < 14; ++i) r.l[i] = neg ? m.l[i] : r.l[i];
+    return r;
   }
   static __device__ __forceinline__ Acc from_shifted(const F& x, const F& y) { return acc28_core::from_shifted(x, y); }
   static __device__ __forceinline__ Acc madd(const Acc& a, const F& x, const F& y, int* sp) {
@@ -834,8 +844,11 @@ __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>
     if (b != kNoBucket) {
       if (b != cur) {
         if (cur != kNoBucket) {
-          if (runs == 1 && cur == prev_b) { put(pieces, 2 * t); flags |= kHead; }
-          else put(bucket_sum, cur);
+          // one store for both destinations (a head piece or the bucket's
+          // sum): a single conversion block when the wave's lanes differ
+          const bool head = runs == 1 && cur == prev_b;
+          if (head) flags |= kHead;
+          put(head ? pieces : bucket_sum, head ? 2 * t : cur);
         }
         cur = b;
         ++runs;
@@ -1109,9 +1122,10 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_limb_kernel(const Affine<
       const Fb px = pt[h];
       Fb py = pt[2 + h];
       if (b != cur) {
-        if (cur != kNoBucket) {
-          if (runs == 1 && cur == prev_b) { store(pcs, 2 * t); flags |= kHead; }
-          else store(bsum, cur);
+        if (cur != kNoBucket) {  // (one store block for both destinations, as seg_acc_limb_body)
+          const bool head = runs == 1 && cur == prev_b;
+          if (head) flags |= kHead;
+          store(head ? pcs : bsum, head ? 2 * t : cur);
         }
         cur = b;
         ++runs;
@@ -1636,7 +1650,10 @@ __global__ __launch_bounds__(kBlock, 2) void seg_reduce_pair_kernel(const XYZZ<t
 // without spills measured slower: reduction 14.1 -> 14.7 ms at 2^24,
 // profiles/r04b/ab_window_segment_one_wave_rejected.log)
 template <class Curve, class Ar = FipsPairArith<Curve>>
-__global__ __launch_bounds__(kBlock, 2) void window_segment_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
+#ifndef TACHYON_SEG_PAIR_WAVES
+#define TACHYON_SEG_PAIR_WAVES 2  // (A/B builds: 1 lifts the VGPR cap that makes the BLS12-381 G2 segment sums spill)
+#endif
+__global__ __launch_bounds__(kBlock, TACHYON_SEG_PAIR_WAVES) void window_segment_pair_kernel(const XYZZ<typename Curve::F>* __restrict__ bucket_sum,
                                                                      unsigned W, unsigned B, unsigned L,
                                                                      XYZZ<typename Curve::F>* __restrict__ out) {
   using Fb = typename Ar::Fb;

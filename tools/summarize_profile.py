@@ -45,9 +45,9 @@ def main(d):
     dur = collections.defaultdict(lambda: [0.0, 0])
     if os.path.exists(stats):
         for r in csv.DictReader(open(stats)):
-            d = dur[short(r["Name"])]
-            d[0] += float(r["TotalDurationNs"])
-            d[1] += int(r["Calls"])
+            acc = dur[short(r["Name"])]
+            acc[0] += float(r["TotalDurationNs"])
+            acc[1] += int(r["Calls"])
     agg = collections.defaultdict(list)
     meta = {}
     for sub in ("fetch", "write", "valu"):
