@@ -520,9 +520,10 @@ TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_window_bits(int curve, void* ct
 TACHYON_C_EXPORT void tachyon_mi355x_msm_gpu_set_profile(int curve, void* ctx, int on);
 /* kernel-variant bits for A/B tuning in one process (0 = default schedule).
  * Every accepted variant computes the same MSM; returns 0 (nothing changed)
- * for bits outside 0x1FFFFBF (bits 0-24 but 6; bit 23: two-level window sums
+ * for bits outside 0x3FFFFBF (bits 0-25 but 6; bit 23: two-level window sums
  * for the G2 / BLS12-381 G1 / FIPS reductions, measured slower; bit 24: the
- * G2 window segment sums in two passes). */
+ * G2 window segment sums in two passes; bit 25: the limb-field G1
+ * accumulations read their entries by 8-byte loads, not LDS-staged chunks). */
 TACHYON_C_EXPORT int tachyon_mi355x_msm_gpu_set_variant(int curve, void* ctx, int variant);
 /* device ms of the last run with profiling on: h2d, recode, sort, prep (bounds +
  * chunk scan), acc (the bucket-accumulation kernel alone), reduce, total,

@@ -28,13 +28,14 @@
 namespace tachyon_amd::msm {
 
 // MsmGpu::set_variant bits that exist (A/B tuning only; all compute the same MSM)
-constexpr int kMsmVariantMask = 0x1FFFFBF;  // bits 0-24 except 6 (21: a debug check, not a schedule)
+constexpr int kMsmVariantMask = 0x3FFFFBF;  // bits 0-25 except 6 (21: a debug check, not a schedule)
 // schedule of the last run (last_schedule()): the recode fused with the first
 // radix pass, the onesweep passes fed by the recode's digit counts, 7-byte LDS
 // staging in the recode scatter, the 29-bit-limb G1 accumulation, the lane-pair
-// G2 accumulation
+// G2 accumulation, the 28-bit-limb BLS12-381 G1 accumulation, the pre-derived
+// chain flags checked, the limb-field accumulation's entries staged in LDS
 constexpr unsigned kSchedFusedRecode = 1, kSchedRecodeFedSort = 2, kSchedNarrowStaging = 4, kSchedAcc29 = 8,
-                   kSchedLanePair = 16, kSchedAcc28 = 32, kSchedChainsChecked = 64;
+                   kSchedLanePair = 16, kSchedAcc28 = 32, kSchedChainsChecked = 64, kSchedEntStaged = 128;
 
 struct MsmPlan {
   unsigned c = 0;        // window bits

@@ -766,13 +766,33 @@ struct Pol28 {
 // LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR destination, so the
 // kernel keeps its 3-wave register budget with the gather one iteration ahead)
 typedef __attribute__((address_space(3))) void lds_void_t;
-template <class Pol, int kPrefetch, bool kRaw>
+#ifndef TACHYON_GATHER_NT
+#define TACHYON_GATHER_NT 0  // 1: nontemporal base gathers (A/B build)
+#endif
+// kEnt: how a lane reads its K sorted entries.  A lane's entries sit K x 8
+// bytes from its neighbours', so a wave's entry load touches 64 lines, and
+// the bases' gathers (~3.5 TB/s of lines) evict them from the XCD's L2
+// before the lane's next iteration: an 8-byte load per iteration fetched a
+// line per entry (123 vs 72 algorithmic HBM bytes per entry, FETCH_SIZE).
+//   0: one 8-byte load per iteration, two ahead (rounds 1-6a)
+//   1: aligned 16-byte pairs (entries 2m, 2m + 1), the next pair an iteration
+//      ahead -- a line per two entries (FETCH 93.7 B per entry; 2^26
+//      accumulation 59.6 -> 58.9 ms, profiles/r06h/ab_ent_pairs.log)
+//   2: 64-byte chunks (8 entries) through LDS by LDS-DMA, the next chunk
+//      8 iterations ahead, double-buffered: 4 KiB per wave, no VGPRs; the
+//      lane's first entry must be 16-byte aligned (g0 even: gbeg and K even)
+//      and the entry array 64 bytes longer than gend (MsmGpu::enqueue's
+//      slack).  FETCH 72.4 B per entry = the 64-byte base + 8; 2^26
+//      accumulation 58.8 -> 57.0 ms, BLS12-381 G1 2^24 31.4 -> 30.8 ms
+//      (profiles/r06i/ab_entries_staged.log).  The default where g0 is even.
+template <class Pol, int kPrefetch, bool kRaw, int kEnt = 0>
 __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>* __restrict__ bases,
                                                   const uint64_t* __restrict__ ents, uint32_t c, uint64_t gbeg,
                                                   uint64_t gend, uint64_t tbase, uint32_t K, uint32_t idx_mask,
                                                   XYZZ<typename Pol::Fq>* __restrict__ bucket_sum,
                                                   XYZZ<typename Pol::Fq>* __restrict__ pieces,
                                                   uint32_t* __restrict__ tflags, uint32_t* __restrict__ tlast) {
+  static_assert(kEnt != 2 || kPrefetch == 0, "LDS-staged entries only with the unprefetched base gather");
   using Fq = typename Pol::Fq;
   using F = typename Pol::F;
   using Acc = typename Pol::Acc;
@@ -807,8 +827,39 @@ __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>
       dst[i] = s;
     }
   };
-  uint64_t e0 = ents[g0];
-  uint64_t e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
+  uint64_t e0 = 0, e1 = 0;
+  uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;  // kEnt 1: entries 2m .. 2m + 3, m = g / 2
+  auto load_pair = [&](uint64_t i, uint64_t& a, uint64_t& b) {  // entries i, i + 1 (i even), zeros past gend
+    if (i + 1 < gend) {
+      const uint4 v = *reinterpret_cast<const uint4*>(ents + i);
+      a = (uint64_t)v.y << 32 | v.x;
+      b = (uint64_t)v.w << 32 | v.z;
+    } else {
+      a = i < gend ? ents[i] : 0;
+      b = 0;
+    }
+  };
+  // kEnt 2: [buffer][wave][16-byte piece][lane]; chunk j of a lane (entries
+  // g0 + 8j ..) in buffer j & 1
+  __shared__ uint4 estage[kEnt == 2 ? 2 : 1][kEnt == 2 ? kBlock / 64 : 1][4][kEnt == 2 ? 64 : 1];
+  const uint32_t ewave = threadIdx.x >> 6, elane = threadIdx.x & 63;
+  auto fetch_chunk = [&](uint64_t first, uint32_t buf) {
+    const uint4* src = reinterpret_cast<const uint4*>(ents + first);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds(src + q, (lds_void_t*)&estage[buf][ewave][q][0], 16, 0, 0);
+  };
+  if constexpr (kEnt == 1) {
+    load_pair(g0 & ~uint64_t(1), q0, q1);
+    load_pair((g0 & ~uint64_t(1)) + 2, q2, q3);
+    e0 = (g0 & 1) ? q1 : q0;
+    e1 = (g0 & 1) ? q2 : q1;
+  } else if constexpr (kEnt == 2) {
+    fetch_chunk(g0, 0);
+  } else {
+    e0 = ents[g0];
+    e1 = (g0 + 1 < g1) ? ents[g0 + 1] : 0;
+  }
   Affine<Fq> P;
   // LDS-DMA staging: [slot][wave][16-byte chunk][lane], 32 KiB per workgroup; a
   // wave-instruction writes its 64 lanes' chunks contiguously (base + 16 lane)
@@ -818,13 +869,34 @@ __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>
     const uint4* src = reinterpret_cast<const uint4*>(bases + (entry_val(e) & idx_mask));
 #pragma unroll
     for (int ch = 0; ch < 4; ++ch)
-      __builtin_amdgcn_global_load_lds(src + ch, (lds_void_t*)&stage[slot][wave][ch][0], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src + ch, (lds_void_t*)&stage[slot][wave][ch][0], 16, 0, TACHYON_GATHER_NT ? 2 : 0);
   };
   if constexpr (kPrefetch == 1) P = bases[entry_val(e0) & idx_mask];
   if constexpr (kPrefetch == 2) issue(e0, 0);
   uint32_t it = 0;  // iteration count: the same for every lane of the wave (K entries each)
   for (uint64_t g = g0; g < g1; ++g, ++it) {
-    const uint64_t e2 = (g + 2 < g1) ? ents[g + 2] : 0;
+    uint64_t e2 = 0;
+    if constexpr (kEnt == 1) {
+      // (g & 1 is the same for every lane of the wave when K and gbeg are even)
+      if (g & 1) {  // entry g + 2 opens the next pair: shift, and load the one after
+        e2 = q3;
+        q0 = q2;
+        q1 = q3;
+        load_pair(g + 3, q2, q3);
+      } else {
+        e2 = q2;
+      }
+    } else if constexpr (kEnt == 2) {
+      if ((it & 7) == 0) {  // a new chunk: it has landed (this wave's own LDS-DMA); fetch the next one
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (g + 8 < g1) fetch_chunk(g + 8, ((it >> 3) + 1) & 1);
+      }
+      const uint32_t sl = it & 7;
+      const uint2 w = reinterpret_cast<const uint2*>(&estage[(it >> 3) & 1][ewave][sl >> 1][elane])[sl & 1];
+      e0 = (uint64_t)w.y << 32 | w.x;
+    } else {
+      e2 = (g + 2 < g1) ? ents[g + 2] : 0;
+    }
     Affine<Fq> Pn;
     if constexpr (kPrefetch == 1) {
       Pn = bases[entry_val(e1) & idx_mask];
@@ -836,6 +908,14 @@ __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>
       for (int q = 0; q < 4; ++q) ch[q] = stage[slot][wave][q][lane];
       memcpy(&P, ch, sizeof(P));
       if (g + 1 < g1) issue(e1, slot ^ 1);  // the next base, under this iteration's madd
+    } else if constexpr (TACHYON_GATHER_NT) {  // A/B: the base gather with the nontemporal policy
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4* src = reinterpret_cast<const u32x4*>(bases + (entry_val(e0) & idx_mask));
+      constexpr int kChunks = sizeof(Affine<Fq>) / 16;
+      u32x4 ch[kChunks];
+#pragma unroll
+      for (int q = 0; q < kChunks; ++q) ch[q] = __builtin_nontemporal_load(src + q);
+      memcpy(&P, ch, sizeof(P));
     } else {
       P = bases[entry_val(e0) & idx_mask];
     }
@@ -891,19 +971,20 @@ __device__ __forceinline__ void seg_acc_limb_body(const Affine<typename Pol::Fq>
 
 // (4 waves per SIMD -- <= 128 VGPRs, 14 spilled -- measured slower at 2^26:
 // 76.1-76.4 vs 75.0-75.5 ms, profiles/r04b/tune_sort_tiles_recode_spt_4waves_2_24_26.log)
-template <int kPrefetch, bool kRaw>
+template <int kPrefetch, bool kRaw, int kEnt>
 __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kernel(const Affine<Bn254Fq>* __restrict__ bases,
                                                            const uint64_t* __restrict__ ents, uint32_t c,
                                                            uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
                                                            uint32_t idx_mask, XYZZ<Bn254Fq>* __restrict__ bucket_sum,
                                                            XYZZ<Bn254Fq>* __restrict__ pieces,
                                                            uint32_t* __restrict__ tflags, uint32_t* __restrict__ tlast) {
-  seg_acc_limb_body<Pol29, kPrefetch, kRaw>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces, tflags,
-                                            tlast);
+  seg_acc_limb_body<Pol29, kPrefetch, kRaw, kEnt>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces,
+                                                  tflags, tlast);
 }
 // BLS12-381 G1 over the 14 x 28-bit field: R-form stores (the FIPS chain join
 // and window reductions read them); 2 waves per SIMD (the 14-limb madd holds
 // ~4 x 14 accumulator + 2 x 14 base words)
+template <int kEnt>
 __global__ __launch_bounds__(kBlock, 2) void seg_acc28_kernel(const Affine<Bls381Fq>* __restrict__ bases,
                                                               const uint64_t* __restrict__ ents, uint32_t c,
                                                               uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
@@ -912,8 +993,8 @@ __global__ __launch_bounds__(kBlock, 2) void seg_acc28_kernel(const Affine<Bls38
                                                               XYZZ<Bls381Fq>* __restrict__ pieces,
                                                               uint32_t* __restrict__ tflags,
                                                               uint32_t* __restrict__ tlast) {
-  seg_acc_limb_body<Pol28, 0, false>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces, tflags,
-                                     tlast);
+  seg_acc_limb_body<Pol28, 0, false, kEnt>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces, tflags,
+                                           tlast);
 }
 
 // ---------------------------------------------------------------------------
@@ -1061,7 +1142,10 @@ struct PairPol29 {
 // G2 with a lane pair per point over a limb field: seg_acc_pair_kernel's run
 // logic; the stores convert this lane's components to the R form the
 // lane-pair FIPS reductions read.  set_variant bit 20 restores the FIPS pair.
-template <class Pol>
+// kStaged: the entries in 64-byte chunks through LDS as seg_acc_limb_body's
+// kEnt 2 (a pair's two lanes DMA the chunk's four 16-byte pieces, two each;
+// g0 even and 64 bytes of slack after the entry array)
+template <class Pol, bool kStaged>
 __global__ __launch_bounds__(kBlock) void seg_acc_pair_limb_kernel(const Affine<typename Pol::F2>* __restrict__ bases,
                                                                    const uint64_t* __restrict__ ents, uint32_t c,
                                                                    uint64_t gbeg, uint64_t gend, uint64_t tbase,
@@ -1112,9 +1196,33 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_limb_kernel(const Affine<
     }
   };
   uint32_t flags = 0, runs = 0, cur = kNoBucket;
-  uint64_t e0 = ents[g0];
-  for (uint64_t g = g0; g < g1; ++g) {
-    const uint64_t e1 = (g + 1 < g1) ? ents[g + 1] : 0;
+  // [buffer][wave][piece pair q][lane]: lane 2 vt + h' holds piece 2q + h' of virtual thread vt's chunk
+  __shared__ uint4 estage[kStaged ? 2 : 1][kStaged ? kBlock / 64 : 1][2][kStaged ? 64 : 1];
+  const uint32_t ewave = threadIdx.x >> 6, elane = threadIdx.x & 63;
+  auto fetch_chunk = [&](uint64_t first, uint32_t buf) {
+    const uint4* src = reinterpret_cast<const uint4*>(ents + first) + h;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      __builtin_amdgcn_global_load_lds(src + 2 * q, (lds_void_t*)&estage[buf][ewave][q][0], 16, 0, 0);
+  };
+  uint64_t e0 = 0;
+  if constexpr (kStaged) fetch_chunk(g0, 0);
+  else e0 = ents[g0];
+  uint32_t it = 0;  // (the same for both lanes of a pair and every pair of the wave)
+  for (uint64_t g = g0; g < g1; ++g, ++it) {
+    uint64_t e1 = 0;
+    if constexpr (kStaged) {
+      if ((it & 7) == 0) {  // a new chunk: landed (this wave's own LDS-DMA); fetch the next one
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (g + 8 < g1) fetch_chunk(g + 8, ((it >> 3) + 1) & 1);
+      }
+      const uint32_t sl = it & 7, piece = sl >> 1;
+      const uint2 w = reinterpret_cast<const uint2*>(
+          &estage[(it >> 3) & 1][ewave][piece >> 1][(elane & ~1u) | (piece & 1)])[sl & 1];
+      e0 = (uint64_t)w.y << 32 | w.x;
+    } else {
+      e1 = (g + 1 < g1) ? ents[g + 1] : 0;
+    }
     const uint32_t k0 = entry_key(e0), v0 = entry_val(e0);
     const uint32_t b = bucket_of_key(k0);
     if (b != kNoBucket) {
@@ -1146,7 +1254,7 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_limb_kernel(const Affine<
         }
       }
     }
-    e0 = e1;
+    if constexpr (!kStaged) e0 = e1;
   }
   if (cur != kNoBucket) {
     const bool head = runs == 1 && cur == prev_b;
@@ -2233,8 +2341,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   if (ngroups > 1 && !sort_stream_) TA_HIP(hipStreamCreateWithFlags(&sort_stream_, hipStreamNonBlocking));
   hipStream_t sort_stream = ngroups > 1 ? sort_stream_ : stream_;
 
-  uint64_t* ents = static_cast<uint64_t*>(ents_.ensure(entries * 8));
-  uint64_t* ents2 = static_cast<uint64_t*>(ents2_.ensure(entries * 8));
+  // (64 bytes of slack: the LDS-staged entry chunks read up to 7 entries past a lane's last)
+  uint64_t* ents = static_cast<uint64_t*>(ents_.ensure(entries * 8 + 64));
+  uint64_t* ents2 = static_cast<uint64_t*>(ents2_.ensure(entries * 8 + 64));
   // bucket sums and pieces in the 144-byte Raw format after the 29-bit
   // accumulation (not with the workgroup-tree window sums, an A/B path in R form)
   bool raw = false;
@@ -2425,12 +2534,21 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       TA_HIP(hipEventRecord(ev_[7], stream_));
     }
     if (profile_) TA_HIP(hipEventRecord(gev_acc0_[g], stream_));
+    // the entry reads of the limb-field accumulations (seg_acc_limb_body's
+    // kEnt): LDS-staged chunks when every lane's first entry is 16-byte
+    // aligned, else 16-byte pairs; set_variant bit 25: the 8-byte loads (A/B)
+    const int ent_mode = (variant_ & (1u << 25)) ? 0 : (K % 2 == 0 && e0 % 2 == 0) ? 2 : 1;
     if constexpr (std::is_same_v<Curve, Bn254G1>) {
       if (acc29_) last_schedule_ |= kSchedAcc29;
+      if (acc29_ && acc29_mode_ == 0 && ent_mode == 2) last_schedule_ |= kSchedEntStaged;
+      using Acc29K = decltype(&seg_acc29_kernel<0, true, 0>);
+      const Acc29K k0 = ent_mode == 2 ? (raw ? seg_acc29_kernel<0, true, 2> : seg_acc29_kernel<0, false, 2>)
+                        : ent_mode == 1 ? (raw ? seg_acc29_kernel<0, true, 1> : seg_acc29_kernel<0, false, 1>)
+                                        : (raw ? seg_acc29_kernel<0, true, 0> : seg_acc29_kernel<0, false, 0>);
       if (acc29_)  // 29-bit-limb accumulation (BN254 G1 default; set_variant bits 13 / 17: base prefetch A/B)
-        hipLaunchKernelGGL(acc29_mode_ == 2 ? (raw ? seg_acc29_kernel<2, true> : seg_acc29_kernel<2, false>)
-                           : acc29_mode_ == 1 ? (raw ? seg_acc29_kernel<1, true> : seg_acc29_kernel<1, false>)
-                                              : (raw ? seg_acc29_kernel<0, true> : seg_acc29_kernel<0, false>),
+        hipLaunchKernelGGL(acc29_mode_ == 2 ? (raw ? seg_acc29_kernel<2, true, 0> : seg_acc29_kernel<2, false, 0>)
+                           : acc29_mode_ == 1 ? (raw ? seg_acc29_kernel<1, true, 0> : seg_acc29_kernel<1, false, 0>)
+                                              : k0,
                            dim3(grid_for(Tg)),
                            dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
@@ -2442,7 +2560,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     } else if constexpr (std::is_same_v<Curve, Bls381G1>) {
       if (acc28_) {
         last_schedule_ |= kSchedAcc28;
-        hipLaunchKernelGGL(seg_acc28_kernel, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+        if (ent_mode == 2) last_schedule_ |= kSchedEntStaged;
+        hipLaunchKernelGGL(ent_mode == 2 ? seg_acc28_kernel<2> : ent_mode == 1 ? seg_acc28_kernel<1> : seg_acc28_kernel<0>,
+                           dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                            tflags, tlast);
       } else {
@@ -2460,7 +2580,12 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
       if (pair_acc_ && pair_limb_) {
         last_schedule_ |= std::is_same_v<Curve, Bls381G2> ? kSchedAcc28 : kSchedAcc29;
-        hipLaunchKernelGGL(seg_acc_pair_limb_kernel<LimbPol>, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_,
+        // staged entries for BLS12-381 (2^24 accumulation 88.7 -> 88.0 ms); BN254 G2
+        // measured 12.21 -> 12.32 ms at 2^22 with them (profiles/r06i/ab_entries_staged.log)
+        const bool staged = ent_mode == 2 && std::is_same_v<Curve, Bls381G2>;
+        if (staged) last_schedule_ |= kSchedEntStaged;
+        auto* limb_kernel = staged ? &seg_acc_pair_limb_kernel<LimbPol, true> : &seg_acc_pair_limb_kernel<LimbPol, false>;
+        hipLaunchKernelGGL(limb_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_,
                            d_bases, ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_,
                            bucket_sum, pieces, tflags, tlast);
       } else if (pair_acc_)

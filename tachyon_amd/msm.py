@@ -210,7 +210,7 @@ class VariableBaseMSMGpu:
         b = lib().tachyon_mi355x_msm_gpu_last_schedule(self.curve_id, self._ctx)
         return {"fused_recode": bool(b & 1), "recode_fed_sort": bool(b & 2), "narrow_staging": bool(b & 4),
                 "acc29": bool(b & 8), "lane_pair": bool(b & 16), "acc28": bool(b & 32),
-                "chains_checked": bool(b & 64)}
+                "chains_checked": bool(b & 64), "entries_staged": bool(b & 128)}
 
     def last_divisions(self) -> int:
         """Point chunks the last run was split into (device memory or host-upload pipeline)."""

@@ -378,7 +378,7 @@ def test_msm_schedule_variants_agree(curve, logn):
             2048: (True, True, False), 1024 | 2048: (True, False, False)}
     try:
         for v in (0, 128, 1024, 2048, 1024 | 2048, 16, 32, 48, 4, 256, 4096, 4096 | 128, 8192, 8192 | 4096, 16384,
-                  32768, 65536, 131072, 262144, 524288, 1 << 20, (1 << 20) | 65536, 1 << 21, 1 << 22):
+                  32768, 65536, 131072, 262144, 524288, 1 << 20, (1 << 20) | 65536, 1 << 21, 1 << 22, 1 << 25):
             m.set_variant(v)
             assert m.run(bases, scalars) == expect, hex(v)
             if v in want:
@@ -387,18 +387,48 @@ def test_msm_schedule_variants_agree(curve, logn):
             s = m.last_schedule()
             if curve == "bn254_g1":  # the 29-bit field by default; bit 18 the FIPS 32-bit field
                 assert s["acc29"] == (v != 262144), (hex(v), s)
+                # its entries LDS-staged unless bit 25 (or a base-prefetch mode, bits 13 / 17)
+                assert s["entries_staged"] == (s["acc29"] and v not in (1 << 25, 8192, 8192 | 4096, 131072)), (hex(v), s)
             elif curve == "bls12_381_g1":  # the 28-bit field by default; bit 20 the FIPS 32-bit field
                 assert s["acc28"] == (not v & (1 << 20)), (hex(v), s)
+                assert s["entries_staged"] == (s["acc28"] and v != 1 << 25), (hex(v), s)
             else:  # G2: the lane pair by default; bit 15 the one-lane kernel
                 assert s["lane_pair"] == (v != 32768), (hex(v), s)
                 limb = v != 32768 and not v & (1 << 20)
+                # staged entries for the BLS12-381 pair (BN254 G2 measured faster without)
+                assert s["entries_staged"] == (limb and v != 1 << 25 and curve == "bls12_381_g2"), (hex(v), s)
                 if curve == "bls12_381_g2":  # the pair over 28-bit limbs; bit 20 the FIPS pair
                     assert s["acc28"] == limb, (hex(v), s)
                 else:  # BN254 G2: the pair over 29-bit limbs; bit 20 the FIPS pair
                     assert s["acc29"] == limb, (hex(v), s)
-        for bad in (64, 1 << 25):
+        for bad in (64, 1 << 26):
             with pytest.raises(ValueError):
                 m.set_variant(bad)
+    finally:
+        m.set_variant(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("curve", ["bn254_g1", "bls12_381_g1", "bn254_g2", "bls12_381_g2"])
+def test_msm_entry_reads_odd_sizes(curve):
+    """The limb-field accumulations' ways of reading the sorted entries
+    (seg_acc_limb_body's kEnt; the G2 lane pairs' kStaged) on sizes that
+    stress their edges: odd n (a lane's
+    last LDS-staged chunk runs past the entry array's end into its slack; the
+    last 16-byte pair is cut at gend), one window per sort group (variant 4:
+    groups start at odd entries when n is odd, so the 16-byte pairs take over
+    from the staged chunks), accumulation chunks K / 2 and 2 K (variants 3, 1),
+    and bit 25 (8-byte loads).  Every schedule equals the oracle."""
+    from tachyon_amd import msm as M
+    m = ctx(curve)
+    try:
+        for n in (1, 7, 4097, 12289):
+            bases = O.gen_bases(curve, 23, n, 16).tobytes()
+            scalars = O.gen_scalars(O.CURVE_INFO[curve][1], 23 + n, n).tobytes()
+            expect, _ = O.msm(curve, bases, scalars)
+            for v in (0, 4, 3, 1, 4 | 3, 1 << 25, (1 << 25) | 4):
+                m.set_variant(v)
+                assert m.run(bases, scalars) == expect, (n, hex(v))
     finally:
         m.set_variant(0)
 
