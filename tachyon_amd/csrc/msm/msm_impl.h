@@ -730,7 +730,9 @@ struct Pol28 {
   using Fq = Bls381Fq;
   using F = f28::F28;
   using Acc = acc28_core::Acc;
-  using Raw = Acc;  // (no raw stores: the BLS12-381 reductions are the FIPS kernels)
+  // Raw: the accumulator as it is (14 x 28-bit limbs per coordinate, 224 B);
+  // the identity is zz = 0 alone, as acc29::Raw
+  using Raw = Acc;
   static __device__ __forceinline__ F shift_repack(const uint32_t* w) { return f28::shl8_repack(w); }
   // 257p with the low limbs raised by 2^28 (limbs < 2^29): 257p - y~ << 8 is a
   // borrow-free negation of the shifted canonical y~ (< 256p), < 257p -- inside
@@ -750,7 +752,12 @@ struct Pol28 {
     return acc28_core::madd(a, x, y, sp);
   }
   static __device__ __forceinline__ Acc dbl_slow(const Acc& a) { return acc28_core::dbl(a); }
-  static __device__ __forceinline__ Raw raw_of(const Acc& a, bool) { return a; }
+  static __device__ __forceinline__ Raw raw_of(const Acc& a, bool zero) {
+    Raw r = a;
+#pragma unroll
+    for (int k = 0; k < 14; ++k) r.zz.l[k] = zero ? 0u : a.zz.l[k];
+    return r;
+  }
   static __device__ __forceinline__ XYZZ<Fq> to_xyzz(const Acc& a) {
     XYZZ<Fq> r;
     f28::to32(a.x, r.x.v);
@@ -984,7 +991,7 @@ __global__ __launch_bounds__(kBlock, kPrefetch == 1 ? 1 : 3) void seg_acc29_kern
 // BLS12-381 G1 over the 14 x 28-bit field: R-form stores (the FIPS chain join
 // and window reductions read them); 2 waves per SIMD (the 14-limb madd holds
 // ~4 x 14 accumulator + 2 x 14 base words)
-template <int kEnt>
+template <int kEnt, bool kRaw>
 __global__ __launch_bounds__(kBlock, 2) void seg_acc28_kernel(const Affine<Bls381Fq>* __restrict__ bases,
                                                               const uint64_t* __restrict__ ents, uint32_t c,
                                                               uint64_t gbeg, uint64_t gend, uint64_t tbase, uint32_t K,
@@ -993,8 +1000,8 @@ __global__ __launch_bounds__(kBlock, 2) void seg_acc28_kernel(const Affine<Bls38
                                                               XYZZ<Bls381Fq>* __restrict__ pieces,
                                                               uint32_t* __restrict__ tflags,
                                                               uint32_t* __restrict__ tlast) {
-  seg_acc_limb_body<Pol28, 0, false, kEnt>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces, tflags,
-                                           tlast);
+  seg_acc_limb_body<Pol28, 0, kRaw, kEnt>(bases, ents, c, gbeg, gend, tbase, K, idx_mask, bucket_sum, pieces, tflags,
+                                          tlast);
 }
 
 // ---------------------------------------------------------------------------
@@ -1504,18 +1511,36 @@ struct FipsArith {
   static __device__ __forceinline__ A dbl(const A& a) { return a.dbl(); }
   static __device__ __forceinline__ bool is_zero(const A& a) { return a.is_zero(); }
 };
-struct Limb28Arith {
+// kRawIn / kRawOut: the arrays hold Pol28::Raw (224-byte accumulator limbs,
+// the identity as zz = 0) instead of R-form XYZZ -- the accumulation's raw
+// stores read by the chain join and the window segments without conversions
+// (madd's and add's outputs, X < 9.02p, Y, ZZ, ZZZ < 1.05p, are inside add's
+// input invariant, msm/acc28.h)
+template <bool kRawIn, bool kRawOut>
+struct Limb28ArithT {
   using Fq = Bls381Fq;
   struct A {
     acc28_core::Acc a;
     bool zero;
   };
   static __device__ __forceinline__ A load(const XYZZ<Fq>* p, size_t i) {
-    const XYZZ<Fq> q = p[i];
-    if (q.is_zero()) return {acc28_core::Acc{}, true};
-    return {{f28::from32(q.x.v), f28::from32(q.y.v), f28::from32(q.zz.v), f28::from32(q.zzz.v)}, false};
+    if constexpr (kRawIn) {
+      const acc28_core::Acc r = reinterpret_cast<const acc28_core::Acc*>(p)[i];
+      uint32_t nz = 0;
+#pragma unroll
+      for (int k = 0; k < 14; ++k) nz |= r.zz.l[k];
+      return {r, nz == 0};
+    } else {
+      const XYZZ<Fq> q = p[i];
+      if (q.is_zero()) return {acc28_core::Acc{}, true};
+      return {{f28::from32(q.x.v), f28::from32(q.y.v), f28::from32(q.zz.v), f28::from32(q.zzz.v)}, false};
+    }
   }
   static __device__ __forceinline__ void store(XYZZ<Fq>* p, size_t i, const A& a) {
+    if constexpr (kRawOut) {
+      reinterpret_cast<acc28_core::Acc*>(p)[i] = Pol28::raw_of(a.a, a.zero);
+      return;
+    }
     if (a.zero) {
       p[i] = XYZZ<Fq>::zero();
       return;
@@ -1541,6 +1566,7 @@ struct Limb28Arith {
   }
   static __device__ __forceinline__ bool is_zero(const A& a) { return a.zero; }
 };
+using Limb28Arith = Limb28ArithT<false, false>;
 
 // One K2-ary level of the segmented tree: output q of segment s is the sum of
 // in[beg[s] + q*K2 .. min(end[s], +K2)).  On the last level every segment has
@@ -2346,12 +2372,23 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   uint64_t* ents2 = static_cast<uint64_t*>(ents2_.ensure(entries * 8 + 64));
   // bucket sums and pieces in the 144-byte Raw format after the 29-bit
   // accumulation (not with the workgroup-tree window sums, an A/B path in R form)
+  // (BLS12-381 G1: 224-byte Pol28::Raw after the 28-bit accumulation, read by
+  // the 28-bit reductions -- not with the FIPS reductions of bit 22 or the
+  // two-level window sums of bit 23; every join level raw, so the level buffer
+  // takes the raw slot too)
   bool raw = false;
-  if constexpr (std::is_same_v<Curve, Bn254G1>) raw = acc29_ && !tree_reduce_;
-  const size_t slot = raw ? sizeof(acc29::Raw) : sizeof(Point);
+  size_t slot = sizeof(Point), lvl_slot = sizeof(Point);
+  if constexpr (std::is_same_v<Curve, Bn254G1>) {
+    raw = acc29_ && !tree_reduce_;
+    if (raw) slot = sizeof(acc29::Raw);
+  }
+  if constexpr (std::is_same_v<Curve, Bls381G1>) {
+    raw = acc28_ && !tree_reduce_ && !(variant_ & ((1 << 22) | (1 << 23)));
+    if (raw) slot = lvl_slot = sizeof(Pol28::Raw);
+  }
   Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * slot));
   Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * slot));
-  Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / kJoinFanLong + T + 2) * sizeof(Point)));
+  Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / kJoinFanLong + T + 2) * lvl_slot));
   // Where the chain tables (and the join levels' offsets) are built -- they
   // depend only on the sorted keys (chain_flags_kernel), so they need not wait
   // for the accumulation:
@@ -2561,8 +2598,12 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
       if (acc28_) {
         last_schedule_ |= kSchedAcc28;
         if (ent_mode == 2) last_schedule_ |= kSchedEntStaged;
-        hipLaunchKernelGGL(ent_mode == 2 ? seg_acc28_kernel<2> : ent_mode == 1 ? seg_acc28_kernel<1> : seg_acc28_kernel<0>,
-                           dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
+        using Acc28K = decltype(&seg_acc28_kernel<0, false>);
+        const Acc28K k28 = raw ? (ent_mode == 2 ? seg_acc28_kernel<2, true> : ent_mode == 1 ? seg_acc28_kernel<1, true>
+                                                                                          : seg_acc28_kernel<0, true>)
+                               : (ent_mode == 2 ? seg_acc28_kernel<2, false> : ent_mode == 1 ? seg_acc28_kernel<1, false>
+                                                                                           : seg_acc28_kernel<0, false>);
+        hipLaunchKernelGGL(k28, dim3(grid_for(Tg)), dim3(kBlock), 0, stream_, d_bases, ents2, c,
                            (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_, bucket_sum, pieces,
                            tflags, tlast);
       } else {
@@ -2639,8 +2680,9 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
   // (set_variant bit 22: the FIPS reductions)
   if constexpr (std::is_same_v<Curve, Bls381G1>) {
     if (acc28_ && !(variant_ & (1 << 22))) {
-      seg_reduce = &seg_reduce_kernel<Curve, Limb28Arith>;
-      win_segment = &window_segment_kernel<Curve, Limb28Arith>;
+      seg_reduce = raw ? &seg_reduce_kernel<Curve, Limb28ArithT<true, true>> : &seg_reduce_kernel<Curve, Limb28Arith>;
+      win_segment = raw ? &window_segment_kernel<Curve, Limb28ArithT<true, false>>
+                        : &window_segment_kernel<Curve, Limb28Arith>;
       win_reduce = &reduce_uniform_kernel<Curve, Limb28Arith>;
     }
   }
