@@ -1152,7 +1152,7 @@ struct PairPol29 {
 // kStaged: the entries in 64-byte chunks through LDS as seg_acc_limb_body's
 // kEnt 2 (a pair's two lanes DMA the chunk's four 16-byte pieces, two each;
 // g0 even and 64 bytes of slack after the entry array)
-template <class Pol, bool kStaged>
+template <class Pol, bool kStaged, bool kRaw>
 __global__ __launch_bounds__(kBlock) void seg_acc_pair_limb_kernel(const Affine<typename Pol::F2>* __restrict__ bases,
                                                                    const uint64_t* __restrict__ ents, uint32_t c,
                                                                    uint64_t gbeg, uint64_t gend, uint64_t tbase,
@@ -1181,9 +1181,20 @@ __global__ __launch_bounds__(kBlock) void seg_acc_pair_limb_kernel(const Affine<
   Fb* bsum = reinterpret_cast<Fb*>(bucket_sum);
   Fb* pcs = reinterpret_cast<Fb*>(pieces);
   const Fb one_h = h ? Fb::zero() : Fb::one();
-  Acc acc;
+  Acc acc{};  // (any defined value: the raw stores mask it while acc_zero)
   bool acc_zero = true;
   auto store = [&](Fb* dst, uint64_t idx) {  // this lane's components of the run sum (identity if none)
+    if constexpr (kRaw) {  // the limbs as they are (LimbPairArith<Pol, true>::load), identity = zz zero
+      F* o = reinterpret_cast<F*>(dst) + 8 * idx;
+      F zz = acc.zz;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(F) / 4); ++k) zz.l[k] = acc_zero ? 0u : zz.l[k];
+      o[h] = acc.x;
+      o[2 + h] = acc.y;
+      o[4 + h] = zz;
+      o[6 + h] = acc.zzz;
+      return;
+    }
     Fb* o = dst + 8 * idx;
     if (acc_zero) {
       o[h] = one_h;
@@ -1702,14 +1713,30 @@ struct FipsPairArith {
   static __device__ __forceinline__ A zero(bool h) { return pair::zero<H>(h); }
   static __device__ __forceinline__ A small_mul(const A& P, uint32_t m, bool h) { return pair::small_mul(P, m, h); }
 };
-template <class Pol>
+// kRawIn / kRawOut: the arrays hold the lane pair's limb-field components
+// as they are (8 Pol::F per point: x, y, zz, zzz x 2 components; the identity
+// = zz zero in both) instead of R-form Fq2 XYZZ: the raw accumulation stores,
+// read by the chain join and the window segments (madd's and add's outputs
+// keep add's input invariant X < 10p, Y < 6p, ZZ, ZZZ < 3p, msm/pair28.h,
+// pair29.h)
+template <class Pol, bool kRawIn = false, bool kRawOut = false>
 struct LimbPairArith {
   using Fb = typename Pol::Fb;
+  using F = typename Pol::F;
   struct A {
     typename Pol::Acc a;
     bool zero;
   };
   static __device__ __forceinline__ A load(const Fb* p, size_t i, uint32_t h) {
+    if constexpr (kRawIn) {
+      const F* o = reinterpret_cast<const F*>(p) + 8 * i;
+      const F x = o[h], y = o[2 + h], zz = o[4 + h], zzz = o[6 + h];
+      uint32_t nz = 0;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(F) / 4); ++k) nz |= zz.l[k];
+      nz |= pair::dpp<pair::kSwap>(nz);
+      return {{x, y, zz, zzz}, nz == 0};
+    }
     const Fb* o = p + 8 * i;
     const Fb x = o[h], y = o[2 + h], zz = o[4 + h], zzz = o[6 + h];
     uint32_t nz = 0;
@@ -1719,6 +1746,17 @@ struct LimbPairArith {
     return {{Pol::from32(x.v), Pol::from32(y.v), Pol::from32(zz.v), Pol::from32(zzz.v)}, nz == 0};
   }
   static __device__ __forceinline__ void store(Fb* p, size_t i, uint32_t h, const A& a) {
+    if constexpr (kRawOut) {
+      F* o = reinterpret_cast<F*>(p) + 8 * i;
+      F zz = a.a.zz;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(F) / 4); ++k) zz.l[k] = a.zero ? 0u : zz.l[k];
+      o[h] = a.a.x;
+      o[2 + h] = a.a.y;
+      o[4 + h] = zz;
+      o[6 + h] = a.a.zzz;
+      return;
+    }
     Fb* o = p + 8 * i;
     if (a.zero) {
       const Fb one_h = h ? Fb::zero() : Fb::one();
@@ -2386,6 +2424,14 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     raw = acc28_ && !tree_reduce_ && !(variant_ & ((1 << 22) | (1 << 23)));
     if (raw) slot = lvl_slot = sizeof(Pol28::Raw);
   }
+  // (G2 lane pairs over the limb fields: 8 raw components per point -- 448 B
+  // BLS12-381, 288 B BN254 -- not with the FIPS pair reductions (bit 22), the
+  // two-level (bit 23) or two-pass (bit 24) window sums)
+  if constexpr (std::is_same_v<Curve, Bn254G2> || std::is_same_v<Curve, Bls381G2>) {
+    using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
+    raw = pair_acc_ && pair_limb_ && !tree_reduce_ && !(variant_ & ((1 << 22) | (1 << 23) | (1 << 24)));
+    if (raw) slot = lvl_slot = 8 * sizeof(typename LimbPol::F);
+  }
   Point* bucket_sum = static_cast<Point*>(buckets_.ensure(nb * slot));
   Point* pieces = static_cast<Point*>(part_a_.ensure(2 * T * slot));
   Point* lvl_buf = static_cast<Point*>(part_b_.ensure((2 * T / kJoinFanLong + T + 2) * lvl_slot));
@@ -2625,7 +2671,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
         // measured 12.21 -> 12.32 ms at 2^22 with them (profiles/r06i/ab_entries_staged.log)
         const bool staged = ent_mode == 2 && std::is_same_v<Curve, Bls381G2>;
         if (staged) last_schedule_ |= kSchedEntStaged;
-        auto* limb_kernel = staged ? &seg_acc_pair_limb_kernel<LimbPol, true> : &seg_acc_pair_limb_kernel<LimbPol, false>;
+        auto* limb_kernel = staged ? (raw ? &seg_acc_pair_limb_kernel<LimbPol, true, true>
+                                          : &seg_acc_pair_limb_kernel<LimbPol, true, false>)
+                                   : (raw ? &seg_acc_pair_limb_kernel<LimbPol, false, true>
+                                          : &seg_acc_pair_limb_kernel<LimbPol, false, false>);
         hipLaunchKernelGGL(limb_kernel, dim3(grid_for(2 * Tg)), dim3(kBlock), 0, stream_,
                            d_bases, ents2, c, (uint64_t)e0, (uint64_t)(e0 + ecount), (uint64_t)tbase, K, idx_mask_,
                            bucket_sum, pieces, tflags, tlast);
@@ -2660,8 +2709,10 @@ void MsmGpu<Curve>::enqueue(const Aff* d_bases, const Fr* d_scalars, size_t n, c
     if (pair_reduce) {
       using LimbPol = std::conditional_t<std::is_same_v<Curve, Bls381G2>, PairPol28, PairPol29>;
       if (pair_limb_ && !(variant_ & (1 << 22))) {  // the limb-field pair additions (bit 22: the FIPS pair)
-        seg_reduce = &seg_reduce_pair_kernel<Curve, LimbPairArith<LimbPol>>;
-        win_segment = &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        seg_reduce = raw ? &seg_reduce_pair_kernel<Curve, LimbPairArith<LimbPol, true, true>>
+                         : &seg_reduce_pair_kernel<Curve, LimbPairArith<LimbPol>>;
+        win_segment = raw ? &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol, true, false>>
+                          : &window_segment_pair_kernel<Curve, LimbPairArith<LimbPol>>;
         win_reduce = &reduce_uniform_pair_kernel<Curve, LimbPairArith<LimbPol>>;
         rsum_pass1 = &window_rsum_pair_kernel<Curve, LimbPairArith<LimbPol>>;
         rsum_pass2 = &window_rsum_total_pair_kernel<Curve, LimbPairArith<LimbPol>>;
