@@ -475,6 +475,17 @@ template <class Curve>
 struct AccWaves {
   static constexpr int value = 1;
 };
+// BLS12-381 G1: two waves per SIMD for the 28-bit reductions (the window
+// segment kernel then spills 348 B per lane, but at one wave it ran 1664 waves
+// of dependent products on 1024 SIMDs): 2^24 reduction 5.5 -> 5.0 ms
+// (profiles/r06p/ab_bls_g1_reduction_waves.log)
+#ifndef TACHYON_BLS_G1_RED_WAVES
+#define TACHYON_BLS_G1_RED_WAVES 2
+#endif
+template <>
+struct AccWaves<Bls381G1> {
+  static constexpr int value = TACHYON_BLS_G1_RED_WAVES;
+};
 template <>
 struct AccWaves<Bn254G2> {
   static constexpr int value = 2;
