@@ -539,7 +539,9 @@ TACHYON_C_EXPORT size_t tachyon_mi355x_msm_gpu_last_divisions(int curve, const v
  * counts, bit 2 7-byte LDS staging in the recode scatter, bit 3 an
  * accumulation over the 29-bit-limb field (BN254 G1; BN254 G2's lane pair),
  * bit 4 the lane-pair G2 accumulation, bit 5 over the 28-bit-limb field
- * (BLS12-381 G1 / G2), bit 6 the chain-flag debug check ran. */
+ * (BLS12-381 G1 / G2), bit 6 the chain-flag debug check ran, bit 7 the
+ * limb-field accumulation read its sorted entries through LDS (64-byte chunks
+ * by LDS-DMA; BN254 / BLS12-381 G1, BLS12-381 G2). */
 TACHYON_C_EXPORT unsigned tachyon_mi355x_msm_gpu_last_schedule(int curve, const void* ctx);
 /* Diagnostic: mixed additions per second (G/s) of the curve's bucket
  * accumulation field code in registers on the current device (no gathers, no
