@@ -434,6 +434,28 @@ def test_msm_entry_reads_odd_sizes(curve):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("curve,n", [("bn254_g1", 307919), ("bls12_381_g1", 300000)])
+def test_msm_entry_pairs_odd_chunk(curve, n):
+    """Sizes whose plan gives an odd accumulation chunk K (39 and 41 entries
+    per thread): a lane's first entry is then 16-byte aligned on every other
+    lane, so the accumulation reads its entries as 16-byte pairs (kEnt 1) with
+    the pair shift taken per lane, not LDS-staged chunks -- equal to the
+    oracle, as are the 8-byte loads of set_variant bit 25."""
+    from tachyon_amd import msm as M
+    bases = O.gen_bases(curve, 29, n, 64).tobytes()
+    scalars = O.gen_scalars(O.CURVE_INFO[curve][1], 29, n).tobytes()
+    expect, _ = O.msm(curve, bases, scalars)
+    m = ctx(curve)
+    try:
+        assert m.run(bases, scalars) == expect
+        assert not m.last_schedule()["entries_staged"]
+        m.set_variant(1 << 25)
+        assert m.run(bases, scalars) == expect
+    finally:
+        m.set_variant(0)
+
+
+@pytest.mark.gpu
 def test_madd_ceiling():
     """The bench's VALU ceiling (tachyon_mi355x_msm_madd_ceiling): a positive
     rate for BN254 G1's two field widths, 0 where not provided."""
