@@ -109,6 +109,7 @@ inline MsmPlan MsmPlan::make(size_t n, unsigned scalar_bits, unsigned force_c, u
                                             : std::clamp<size_t>(entries >> 18, 16, 64);
   if (p.group == 1) k = n >> 18;  // ~1024 workgroups per window launch
   p.K = (unsigned)std::clamp<size_t>(k, 8, 256);
+  p.K += p.K & 1;  // even: every lane's first entry 16-byte aligned (the LDS-staged entry reads)
   // first-level fan-in; the join drops to 4-ary levels when the longest chain
   // is longer than 16 pieces (kJoinFanLong, chosen after the chain read-back)
   p.K2 = 16;

@@ -434,19 +434,22 @@ def test_msm_entry_reads_odd_sizes(curve):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("curve,n", [("bn254_g1", 307919), ("bls12_381_g1", 300000)])
+@pytest.mark.parametrize("curve,n", [("bn254_g1", 300000), ("bls12_381_g1", 300000)])
 def test_msm_entry_pairs_odd_chunk(curve, n):
-    """Sizes whose plan gives an odd accumulation chunk K (39 and 41 entries
-    per thread): a lane's first entry is then 16-byte aligned on every other
-    lane, so the accumulation reads its entries as 16-byte pairs (kEnt 1) with
-    the pair shift taken per lane, not LDS-staged chunks -- equal to the
-    oracle, as are the 8-byte loads of set_variant bit 25."""
-    from tachyon_amd import msm as M
+    """The plan rounds the accumulation chunk K up to even (here 38 / 42), so
+    every lane's first entry is 16-byte aligned and the entries are
+    LDS-staged; set_variant bit 0-1 = 3 halves K to an odd 19 / 21, where the
+    lanes' alignment alternates and the accumulation reads 16-byte pairs
+    (kEnt 1, the pair shift taken per lane); bit 25 the 8-byte loads. All
+    three equal the oracle."""
     bases = O.gen_bases(curve, 29, n, 64).tobytes()
     scalars = O.gen_scalars(O.CURVE_INFO[curve][1], 29, n).tobytes()
     expect, _ = O.msm(curve, bases, scalars)
     m = ctx(curve)
     try:
+        assert m.run(bases, scalars) == expect
+        assert m.last_schedule()["entries_staged"]
+        m.set_variant(3)
         assert m.run(bases, scalars) == expect
         assert not m.last_schedule()["entries_staged"]
         m.set_variant(1 << 25)
